@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Benchmark of the GP log-marginal-likelihood hot path on MI355X.
+
+Metric (BASELINE.json): LML evaluations per second at N = 8192, fp64, SE kernel, D = 1
+(SURVEY §8d "Metric" row).  One step = one full evaluation -- kernel-matrix build, blocked
+Cholesky with the fused forward solve, read-out of -LML -- from inputs already resident in HBM.
+With --gpus N (torchrun, one process per GPU) every rank evaluates its own hyperparameter
+candidate per step (weak scaling) and the step ends with the sweep's one collective, an
+all-gather of the per-rank (nlml, info) pairs over RCCL.
+
+Prints ONE JSON line on rank 0 (fields per the driver contract) including
+  roofline      the trailing-update MFMA kernel (the dominant one): algorithmic flops of the
+                lower-triangular SYRK ÷ its HIP-event time over the timed region, vs the fp64
+                (or fp32) MFMA peak
+  cpu_baseline  the numpy/SciPy restatement of the reference path (oracle/) timed on this host
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK = {"f64": 78.6, "f32": 157.3}   # TFLOP/s dense MFMA (AMD MI355X spec; microarch guide for f32)
+HBM_PEAK = 8000.0                      # GB/s spec
+
+CONFIGS = {
+    # name: (kernel, d, n, noise, dtype, hyp)
+    "metric": ("SE", 1, 8192, 1e-2, "f64", [0.1]),
+    "C2": ("SE", 1, 4096, 1e-2, "f64", [0.1]),
+    "C3": ("MAT52-ARD", 4, 8192, 1e-1, "f32", [[0.25, 0.5, 0.75, 1.0]]),
+    "C5": ("SE-ARD+PER", 8, 16384, 1e-2, "f64", None),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=None, help="override N")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events")
+    return ap.parse_args()
+
+
+def build_kernel(name, d):
+    from gaussianprocessfundamentals_amd.KernelBasics import BaseKernels as bk
+    from gaussianprocessfundamentals_amd.KernelBasics import Operators as ops
+    if name == "SE":
+        return bk.SquaredExponentialKernel(d)
+    if name == "MAT52-ARD":
+        return bk.MaternKernel5_2(d, ard=True, standard=True)
+    if name == "SE-ARD+PER":
+        return ops.AdditionOperator(d, [bk.SquaredExponentialKernel(d, ard=True), bk.PeriodicKernel(d, standard=True)])
+    raise ValueError(name)
+
+
+def cpu_baseline(cfg_name, n, budget_s):
+    """Time the oracle (numpy/SciPy restatement of the reference path) on this host."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    from oracle import gp_oracle as o
+    threads = int(os.environ.get("GPK_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    kname, d, _, noise, _, hyp = CONFIGS[cfg_name]
+    tree = {"SE": ("SE", {}), "MAT52-ARD": ("MAT52", {"ard": True, "standard": True}),
+            "SE-ARD+PER": ("ADD", [("SE", {"ard": True}), ("PER", {"standard": True})])}[kname]
+    if hyp is None:
+        hyp = [list(np.linspace(0.4, 1.1, d)), 1.0, 0.5]
+    x, y = o.make_inputs("metric" if cfg_name == "metric" else cfg_name, n=n)
+    evals = 0
+    with threadpool_limits(limits=threads):
+        o.nlml(tree, hyp, noise, x[:512], y[:512])  # warm the BLAS pool
+        t0 = time.perf_counter()
+        while True:
+            o.nlml(tree, hyp, noise, x, y)
+            evals += 1
+            el = time.perf_counter() - t0
+            if el > budget_s or evals >= 8:
+                break
+    try:
+        cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:  # noqa: BLE001
+        cpu_model = "unknown"
+    return {"value": evals / el, "unit": "LML evals/s", "cores": threads, "kind": "port",
+            "sample": "%d full evaluations of the %s workload (N=%d, fp64) by the numpy/SciPy oracle "
+                      "(OpenBLAS dpotrf/dtrtrs), %d threads, %s, %.1f s" % (evals, cfg_name, n, threads, cpu_model, el)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import gaussianprocessfundamentals_amd.global_parameters as gp
+    gp.init(0)
+    from gaussianprocessfundamentals_amd import _native as nat
+    from gaussianprocessfundamentals_amd import engine
+    from oracle import gp_oracle as o  # input generator only (same seeds as the golden vectors)
+
+    kname, d, n, noise, dtn, hyp = CONFIGS[args.config]
+    n = args.n or n
+    if hyp is None:
+        hyp = [[0.4 + 0.1 * i for i in range(d)], 1.0, 0.5]
+    dt = torch.float64 if dtn == "f64" else torch.float32
+    x, y = o.make_inputs("metric" if args.config == "metric" else args.config, n=n)
+    dev = torch.device("cuda", local)
+    X = torch.as_tensor(x, dtype=torch.float64, device=dev).contiguous()
+    Y = torch.as_tensor(y, dtype=torch.float64, device=dev).reshape(1, n).contiguous()
+    kernel = build_kernel(kname, d)
+    kd = engine.kernel_descriptor(kernel, d)
+    flat_h = []
+    for h in hyp:
+        flat_h.extend(h if isinstance(h, list) else [h])
+    # weak scaling: every rank evaluates its own candidate (length scale offset by rank)
+    flat_h[0] = flat_h[0] * (1.0 + 0.01 * rank) if not isinstance(hyp[0], list) else flat_h[0]
+    H = torch.tensor(flat_h, dtype=torch.float64, device=dev)
+    NZ = torch.tensor([noise], dtype=torch.float64, device=dev)
+    fact = engine.AugmentedFactorization(n, d, 0, 1, dt)
+    gathered = torch.empty(2 * world, dtype=torch.float64, device=dev) if world > 1 else None
+
+    def step():
+        fact.run(kd, H, 0, NZ, 0, X, 0, Y, 0)
+        if world > 1:
+            mine = torch.stack([fact.nlml()[0], fact.info[0].to(torch.float64)])
+            dist.all_gather_into_tensor(gathered, mine)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    nat.timing_reset()
+    use_events = not args.no_events
+    nat.timing_enable(use_events)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    nat.timing_enable(False)
+    el = t1 - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    timing = nat.timing_read() if use_events else None
+    nl = float(fact.nlml()[0].item())
+    info = int(fact.info[0].item())
+
+    if rank == 0:
+        evals = args.steps * world
+        value = evals / el
+        ms = el / args.steps * 1000.0
+        lay = fact.layout
+        f_lml = n ** 3 / 3.0 + 2.0 * n * n
+        roof = None
+        breakdown = None
+        if timing:
+            up = timing["update"]
+            ach = up["flops"] / (up["ms"] * 1e-3) / 1e12 if up["ms"] > 0 else 0.0
+            roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK[dtn], "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK[dtn], 4), "traffic": None,
+                    "kernel": "gemm_kernel<UPDATE> (trailing SYRK, %s MFMA 16x16x4)" % dtn,
+                    "launches_per_step": up["launches"] // args.steps,
+                    "avg_launch_us": round(up["ms"] * 1e3 / max(1, up["launches"]), 2)}
+            asm = timing["assemble"]
+            breakdown = {k: round(v["ms"] / args.steps, 4) for k, v in timing.items()}
+            breakdown["kbuild_GBps"] = round(asm["bytes"] / (asm["ms"] * 1e-3) / 1e9, 1) if asm["ms"] > 0 else None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args.config, n, args.cpu_seconds)
+        line = {
+            "metric": "log-marginal-likelihood evals/sec at N=%d %s" % (n, "fp64" if dtn == "f64" else "fp32"),
+            "value": round(value, 3),
+            "unit": "LML evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": dtn,
+            "data": "synthetic (SURVEY §8d generator, numpy default_rng seed 5), resident in HBM",
+            "config": {"workload": "%s GP -LML, kernel=%s, D=%d, N=%d, noise=%g; one evaluation per rank per step"
+                                   % (args.config, kname, d, n, noise),
+                       "n": n, "d": d, "kernel": kname, "panel": int(lay.nb), "parallelism": "dp%d (independent candidates)" % world},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "lml_tflops": round(f_lml * value / 1e12, 3),
+            "lml_frac_of_peak": round(f_lml * value / 1e12 / PEAK[dtn], 4),
+            "kernel_ms_per_step": breakdown,
+            "check": {"nlml": nl, "info": info},
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

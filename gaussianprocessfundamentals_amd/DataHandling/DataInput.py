@@ -1,0 +1,169 @@
+"""Data inputs (gpbasics/DataHandling/AbstractDataInput.py, DataInput.py, BatchDataInput.py).
+
+Inputs are cast to fp64 (DataInput.py:198-206) and kept resident on the engine's device.
+Shapes: X [N, D], y [N, 1] (AbstractDataInput.py:17-27) or, for :class:`BatchDataInput`,
+X [B, N, D], y [B, N, 1].  Without an explicit test set, ``test_ratio`` of the points (default
+0.2) is held out by a seeded random permutation (AbstractDataInput.py:41-60); the permutation
+comes from torch's generator, not TensorFlow's, so the held-out indices differ from the
+reference's for the same seed.
+"""
+from __future__ import annotations
+
+import logging
+from typing import List
+
+import torch
+
+from .. import global_parameters as global_param
+from ..MeanFunctionBasics import BaseMeanFunctions as bmf
+
+global_param.ensure_init()
+
+
+def _dev():
+    from ..engine import device
+    try:
+        return device()
+    except Exception:  # noqa: BLE001 - no GPU: host-side data handling still works
+        return torch.device("cpu")
+
+
+def _f64(x) -> torch.Tensor:
+    t = x.detach() if isinstance(x, torch.Tensor) else torch.as_tensor(x)
+    return t.to(device=_dev(), dtype=torch.float64)
+
+
+class AbstractDataInput:
+    def __init__(self, data_x_train, data_y_train, data_x_test=None, data_y_test=None,
+                 test_ratio: float = -1, seed: int = 3061941):
+        assert (data_x_test is None or (len(data_x_train.shape) == len(data_x_test.shape)
+                                        and len(data_y_train.shape) == len(data_y_test.shape)
+                                        and len(data_x_train.shape) == len(data_y_train.shape))) and \
+            len(data_x_train.shape) in (2, 3), \
+            "Shape of input and target data (test as well as train data) needs to be either " \
+            "[instance#, length, dimensionality] or [length, dimensionality]."
+        assert data_y_train.shape[-1] == 1, \
+            "Target training data (data_y_train) has to be unidimensional, shape=[n_train, 1] / [instance#, n_train, 1]"
+        assert data_y_test is None or data_y_test.shape[-1] == 1, \
+            "Target test data (data_y_test) has to be unidimensional, shape=[n_test, 1] / [instance#, n_test, 1]"
+        assert data_x_test is None or data_x_train.shape[-1] == data_x_test.shape[-1], \
+            "Dimensionality of training and test input data (data_x_train and data_x_test) need to match"
+        assert test_ratio <= 1, "test_ratio has to be in the range [0; 1]"
+        self.seed = seed
+        if test_ratio > 0 and data_x_test is not None:
+            logging.warning("test_ratio is ignored if test_data is explicitly given.")
+        if data_x_test is None and test_ratio != 0:
+            if test_ratio < 0:
+                logging.warning("test_ratio is not given although explicit test data was not provided. "
+                                "default value '0.2' is assumed for test_ratio.")
+                test_ratio = 0.2
+            length = data_x_train.shape[0]
+            test_size = min(length - 1, int(length * test_ratio))
+            gen = torch.Generator().manual_seed(int(seed))
+            perm = torch.randperm(length, generator=gen)
+            idx_train = torch.sort(perm[:length - test_size]).values
+            idx_test = torch.sort(perm[length - test_size:]).values
+            self.data_x_train = data_x_train[idx_train.to(data_x_train.device)]
+            self.data_y_train = data_y_train[idx_train.to(data_y_train.device)]
+            self.data_x_test = data_x_train[idx_test.to(data_x_train.device)]
+            self.data_y_test = data_y_train[idx_test.to(data_y_train.device)]
+        elif data_x_test is None:
+            self.data_x_train = self.data_x_test = data_x_train
+            self.data_y_train = self.data_y_test = data_y_train
+        else:
+            self.data_x_train, self.data_y_train = data_x_train, data_y_train
+            self.data_x_test, self.data_y_test = data_x_test, data_y_test
+        self.detrended_y_test = None
+        self.detrended_y_train = None
+        self.mean_function = None
+        self.n_train = int(self.data_x_train.shape[-2])
+        self.n_test = int(self.data_x_test.shape[-2])
+        self.n_inducting_train = max(20, int(self.n_train * global_param.p_nystroem_ratio))
+        self.n_inducting_test = max(20, int(self.n_test * global_param.p_nystroem_ratio))
+
+    def get_input_dimensionality(self) -> int:
+        return int(self.data_x_train.shape[-1])
+
+    def set_seed(self, seed: int):
+        self.seed = seed
+
+    def set_mean_function(self, mean_function):
+        """Reset the detrended targets (AbstractDataInput.py:104-115)."""
+        self.detrended_y_train = None
+        self.detrended_y_test = None
+        self.mean_function = mean_function
+        if self.mean_function.get_last_hyper_parameter() is None:
+            self.mean_function.last_hyper_parameter = self.mean_function.get_default_hyper_parameter()
+
+    def is_batch(self) -> bool:
+        return self.data_x_train.dim() == 3
+
+    def _detrend(self, x, y):
+        if isinstance(self.mean_function, bmf.ZeroMeanFunction):
+            return y
+        mf = self.mean_function
+        if self.is_batch():
+            means = torch.stack([mf.get_tf_tensor(mf.get_last_hyper_parameter(), xb).reshape(-1, 1) for xb in x])
+        else:
+            means = mf.get_tf_tensor(mf.get_last_hyper_parameter(), x).reshape(-1, 1)
+        return y - means
+
+    def get_detrended_y_train(self):
+        """y - m(X) (DataInput.py:244-264); the zero mean returns y itself."""
+        if self.mean_function is None:
+            logging.error("Mean Function is None.")
+            return None
+        if self.detrended_y_train is None:
+            self.detrended_y_train = self._detrend(self.data_x_train, self.data_y_train)
+        return self.detrended_y_train
+
+    def get_detrended_y_test(self):
+        if self.mean_function is None:
+            logging.error("Mean Function is None.")
+            return None
+        if self.detrended_y_test is None:
+            self.detrended_y_test = self._detrend(self.data_x_test, self.data_y_test)
+        return self.detrended_y_test
+
+    def get_x_range(self) -> List[List[float]]:
+        """[min, max] per input dimension over train and test (DataInput.py:229-242)."""
+        d = self.get_input_dimensionality()
+        xa = torch.cat([self.data_x_train.reshape(-1, d), self.data_x_test.reshape(-1, d)], dim=0)
+        lo = torch.min(xa, dim=0).values.tolist()
+        hi = torch.max(xa, dim=0).values.tolist()
+        return [[float(a), float(b)] for a, b in zip(lo, hi)]
+
+    @staticmethod
+    def get_k_fold_data_inputs(x_train, y_train, k: int, seed: int = 3061941):
+        """k train/test folds from one seeded permutation (AbstractDataInput.py:147-168)."""
+        length = x_train.shape[0]
+        gen = torch.Generator().manual_seed(int(seed))
+        perm = torch.randperm(length, generator=gen)
+        sizes = [length // k] * (k - 1) + [length - (length // k) * (k - 1)]
+        parts = list(torch.split(perm, sizes))
+        out = []
+        for i in range(k):
+            te = torch.sort(parts[i]).values
+            tr = torch.sort(torch.cat([parts[j] for j in range(k) if j != i])).values
+            out.append(AbstractDataInput(x_train[tr], y_train[tr], x_train[te], y_train[te], seed=seed))
+        return out
+
+
+class DataInput(AbstractDataInput):
+    """Single data set: X [N, D], y [N, 1] (DataInput.py:193-206)."""
+
+    def __init__(self, data_x_train, data_y_train, data_x_test=None, data_y_test=None,
+                 test_ratio: float = -1, seed: int = 3061941):
+        if data_x_test is not None and data_y_test is not None:
+            data_x_test, data_y_test = _f64(data_x_test), _f64(data_y_test)
+        super().__init__(_f64(data_x_train), _f64(data_y_train), data_x_test, data_y_test, test_ratio, seed)
+
+
+class BatchDataInput(AbstractDataInput):
+    """B data sets evaluated together: X [B, N, D], y [B, N, 1] (BatchDataInput.py:24-28)."""
+
+    def __init__(self, data_x_train, data_y_train, data_x_test=None, data_y_test=None,
+                 test_ratio: float = -1, seed: int = 3061941):
+        if data_x_test is not None and data_y_test is not None:
+            data_x_test, data_y_test = _f64(data_x_test), _f64(data_y_test)
+        super().__init__(_f64(data_x_train), _f64(data_y_train), data_x_test, data_y_test, test_ratio, seed)

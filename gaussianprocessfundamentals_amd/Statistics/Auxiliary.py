@@ -1,0 +1,103 @@
+"""Posterior properties (gpbasics/Statistics/Auxiliary.py:14-103).
+
+The reference computes mu = K_s^T alpha and Sigma = K_ss - v^T v with v = inv(L) K_s, an explicit
+N^3 inverse (Auxiliary.py:57-93).  Here the test points become extra rows of the augmented
+matrix and ONE device factorisation yields V^T = K_s^T L^-T in those rows and the Schur
+complement K_ss - V^T V in the corner, together with mu = V^T z (include/gpk.h).  Returned
+shapes follow the reference: mu [M], variance the full [M, M] matrix, sd its elementwise sqrt
+(quirk Q8: NaN where an off-diagonal covariance is negative).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from .. import engine
+from .. import global_parameters as global_param
+from .CovarianceMatrix import noise_vector
+
+global_param.ensure_init()
+
+
+class AuxiliaryGpProperties:
+    def __init__(self, covariance_matrix, mean_function):
+        self.covariance_matrix = covariance_matrix
+        self.data_input = None
+        self.mean_function = mean_function
+        self.reset()
+
+    def reset(self):
+        self.detrended_y_train = None
+        self.inv_L_K_dot_K_s = None
+        self.posterior_mu = None
+        self.posterior_var = None
+        self.posterior_sd = None
+        self._post = None
+
+    def set_data_input(self, data_input):
+        self.data_input = data_input
+        self.reset()
+
+
+class HolisticAuxiliaryGpProperties(AuxiliaryGpProperties):
+    def _posterior_factorization(self, hyper_parameter: List, noise) -> engine.AugmentedFactorization:
+        if self._post is None:
+            di = self.data_input
+            if di.data_x_train.dim() != 2:
+                raise NotImplementedError("posterior of BatchDataInput is not provided")
+            cm = self.covariance_matrix
+            x, xt = di.data_x_train, di.data_x_test
+            n, d, m = int(x.shape[0]), int(x.shape[1]), int(xt.shape[0])
+            y = di.get_detrended_y_train().reshape(1, n).to(torch.float64).contiguous()
+            f = engine.AugmentedFactorization(n, d, m, 1, global_param.p_dtype)
+            kd = engine.kernel_descriptor(cm.kernel, d)
+            hyp = engine.pack_hyper_parameter(hyper_parameter, kd.n_hyp)
+            f.run(kd, hyp, 0, noise_vector(noise), 0, x.contiguous(), 0, y, 0, Xs=xt.contiguous(), xs_bstride=0)
+            cm.kernel._record_hyper_parameter(list(hyper_parameter))
+            f.check_info()
+            self._post = f
+        return self._post
+
+    def get_inverse_cholesky_k_times_k_s(self, hyper_parameter: List, noise):
+        """v = inv(L) K_s [N, M] (Auxiliary.py:57-66)."""
+        if self.data_input is None:
+            return None
+        if self.inv_L_K_dot_K_s is None:
+            f = self._posterior_factorization(hyper_parameter, noise)
+            self.inv_L_K_dot_K_s = f.extra_rows(0).to(torch.float64).transpose(0, 1).contiguous()
+        return self.inv_L_K_dot_K_s
+
+    def get_posterior_mu(self, hyper_parameter: List, noise):
+        """mu = K_s^T alpha, shape [M] (Auxiliary.py:68-81)."""
+        if self.data_input is None:
+            return None
+        if self.posterior_mu is None:
+            self.posterior_mu = self._posterior_factorization(hyper_parameter, noise).posterior_mu(0).clone()
+        return self.posterior_mu
+
+    def get_posterior_var(self, hyper_parameter: List, noise):
+        """K_ss - v^T v, full [M, M] (Auxiliary.py:83-93)."""
+        if self.data_input is None:
+            return None
+        if self.posterior_var is None:
+            self.posterior_var = self._posterior_factorization(hyper_parameter, noise).corner(0).to(torch.float64)
+        return self.posterior_var
+
+    def get_posterior_var_diag(self, hyper_parameter: List, noise):
+        """Diagonal of the posterior covariance [M] (build extension; no M x M read-back)."""
+        if self.data_input is None:
+            return None
+        return self._posterior_factorization(hyper_parameter, noise).posterior_var_diag(0).clone()
+
+    def get_posterior_sd(self, hyper_parameter: List, noise):
+        """Elementwise sqrt of the full posterior covariance (Auxiliary.py:95-103)."""
+        if self.data_input is None:
+            return None
+        if self.posterior_sd is None:
+            self.posterior_sd = torch.sqrt(self.get_posterior_var(hyper_parameter, noise))
+        return self.posterior_sd
+
+
+class BlockwiseAuxiliaryGpProperties(HolisticAuxiliaryGpProperties):
+    pass

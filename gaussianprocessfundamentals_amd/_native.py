@@ -1,0 +1,163 @@
+"""ctypes binding of libgpk.so (the C ABI declared in include/gpk.h).
+
+There is deliberately no CPU fallback: when the HIP extension cannot be loaded, or no GPU is
+visible, every product entry point raises :class:`NativeUnavailable`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_double, c_int, c_int32, c_int64, c_size_t, c_void_p
+
+import torch  # noqa: F401  (must be loaded first: libgpk binds to torch's HIP runtime by soname)
+
+from . import _build
+
+GPK_ABI_VERSION = 1
+GPK_F64, GPK_F32 = 0, 1
+OP_PER, OP_SE, OP_MAT32, OP_MAT52, OP_ADD, OP_MUL = 104, 105, 107, 108, 201, 202
+NODE_SCALED, NODE_ARD, NODE_SE_EXPANDED, NODE_STANDARD = 1, 2, 4, 8
+MAX_NODES, MAX_DIM, MAX_ARD, MAX_HYP = 16, 16, 2, 64
+NUM_CLASSES = 6
+TIMING_CLASSES = ("assemble", "diag", "trsm", "update", "finalize", "trsv")
+
+# every function include/gpk.h declares (checked by tests/test_abi.py against the header)
+EXPORTS = (
+    "gpk_abi_version", "gpk_last_error", "gpk_plan", "gpk_assemble", "gpk_potrf_aug",
+    "gpk_finalize", "gpk_nlml", "gpk_kernel_matrix", "gpk_trsv", "gpk_timing_enable",
+    "gpk_timing_read", "gpk_timing_reset",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    """libgpk.so (the HIP path) is missing or cannot run here."""
+
+
+class GpkError(RuntimeError):
+    """A libgpk call returned an error code."""
+
+
+class GpkNode(ctypes.Structure):
+    _fields_ = [("op", c_int32), ("hyp_offset", c_int32), ("ard_slot", c_int32), ("flags", c_int32)]
+
+
+class GpkKdesc(ctypes.Structure):
+    _fields_ = [("n_nodes", c_int32), ("n_hyp", c_int32), ("dim", c_int32), ("n_ard", c_int32),
+                ("nodes", GpkNode * MAX_NODES)]
+
+
+class GpkLayout(ctypes.Structure):
+    _fields_ = [("dtype", c_int32), ("batch", c_int32), ("n", c_int64), ("m", c_int64),
+                ("d", c_int64), ("nb", c_int64), ("n_pad", c_int64), ("y_row", c_int64),
+                ("p", c_int64), ("ld", c_int64), ("w_batch_stride", c_int64),
+                ("inv_batch_stride", c_int64), ("w_bytes", c_size_t), ("inv_bytes", c_size_t)]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib):
+    P, D = c_void_p, POINTER(c_double)
+    sig = {
+        "gpk_abi_version": (c_int, []),
+        "gpk_last_error": (ctypes.c_char_p, []),
+        "gpk_plan": (c_int, [c_int, c_int32, c_int64, c_int64, c_int64, POINTER(GpkLayout)]),
+        "gpk_assemble": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64,
+                                 P, c_int64, P, c_int64, P, c_int64, P, c_int64, P, P]),
+        "gpk_potrf_aug": (c_int, [POINTER(GpkLayout), P, P, P, P]),
+        "gpk_finalize": (c_int, [POINTER(GpkLayout), P, P, P, P, P, P]),
+        "gpk_nlml": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64, P,
+                             c_int64, P, c_int64, P, P, P, P, P]),
+        "gpk_kernel_matrix": (c_int, [POINTER(GpkKdesc), P, c_int, c_int, P, c_int64, P, c_int64,
+                                      c_int32, c_double, P, c_int64, P]),
+        "gpk_trsv": (c_int, [POINTER(GpkLayout), c_int, P, P, P, P]),
+        "gpk_timing_enable": (c_int, [c_int]),
+        "gpk_timing_read": (c_int, [D, POINTER(c_int64), D, D]),
+        "gpk_timing_reset": (c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def load_library(path: str = None):
+    """Load libgpk.so (no GPU needed for loading).  Raises NativeUnavailable if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or os.environ.get("GPK_LIB", _build.LIB_PATH)
+        if not os.path.exists(p):
+            raise NativeUnavailable(
+                "libgpk.so not found at %s: build it with __graft_entry__.build() "
+                "(hipcc --offload-arch=gfx950); there is no CPU fallback" % p)
+        try:
+            lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise NativeUnavailable("cannot load %s: %s" % (p, e)) from e
+        _declare(lib)
+        v = lib.gpk_abi_version()
+        if v != GPK_ABI_VERSION:
+            raise NativeUnavailable("libgpk ABI %d != expected %d (stale build?)" % (v, GPK_ABI_VERSION))
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def lib():
+    """The loaded library, with a GPU visible (the only configuration the product runs in)."""
+    L = load_library()
+    if not torch.cuda.is_available():
+        raise NativeUnavailable("no ROCm GPU visible: the gpk engine runs only on MI355X (gfx950)")
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.gpk_last_error().decode() if _lib is not None else ""
+        raise GpkError("%s failed (rc=%d): %s" % (what, rc, msg))
+
+
+def ptr(t) -> c_void_p:
+    if t is None:
+        return None
+    return c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None) -> c_void_p:
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def plan(dtype_code: int, batch: int, n: int, m: int, d: int) -> GpkLayout:
+    lay = GpkLayout()
+    check(load_library().gpk_plan(dtype_code, batch, n, m, d, ctypes.byref(lay)), "gpk_plan")
+    return lay
+
+
+def dtype_code(torch_dtype) -> int:
+    if torch_dtype == torch.float64:
+        return GPK_F64
+    if torch_dtype == torch.float32:
+        return GPK_F32
+    raise ValueError("unsupported dtype %r (float64 or float32)" % (torch_dtype,))
+
+
+def timing_enable(on: bool = True):
+    check(load_library().gpk_timing_enable(1 if on else 0), "gpk_timing_enable")
+
+
+def timing_reset():
+    check(load_library().gpk_timing_reset(), "gpk_timing_reset")
+
+
+def timing_read() -> dict:
+    ms = (c_double * NUM_CLASSES)()
+    nl = (c_int64 * NUM_CLASSES)()
+    fl = (c_double * NUM_CLASSES)()
+    by = (c_double * NUM_CLASSES)()
+    check(load_library().gpk_timing_read(ms, nl, fl, by), "gpk_timing_read")
+    return {name: {"ms": ms[i], "launches": nl[i], "flops": fl[i], "bytes": by[i]}
+            for i, name in enumerate(TIMING_CLASSES)}

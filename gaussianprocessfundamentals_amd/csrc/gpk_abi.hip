@@ -1,0 +1,402 @@
+// extern "C" entry points of libgpk.so (declared in include/gpk.h).
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gpk_internal.h"
+
+using namespace gpk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail_arg(int idx, const char* what) {
+  g_err = std::string("invalid argument: ") + what;
+  return -idx;
+}
+
+int fail_hip(hipError_t e, const char* where) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return (int)e > 0 ? (int)e : 1;
+}
+
+#define GPK_HIP(call, where)                         \
+  do {                                               \
+    hipError_t e_ = (call);                          \
+    if (e_ != hipSuccess) return fail_hip(e_, where); \
+  } while (0)
+
+// ------------------------------------------------------------------------------ event timing
+struct TimedLaunch {
+  int cls;
+  hipEvent_t beg, end;
+  double flops, bytes;
+};
+
+struct Timing {
+  std::mutex mu;
+  bool on = false;
+  std::vector<TimedLaunch> pending;
+  std::vector<hipEvent_t> pool;
+  double ms[GPK_NUM_CLASSES] = {0};
+  int64_t launches[GPK_NUM_CLASSES] = {0};
+  double flops[GPK_NUM_CLASSES] = {0};
+  double bytes[GPK_NUM_CLASSES] = {0};
+};
+Timing g_timing;
+
+hipEvent_t take_event() {
+  if (!g_timing.pool.empty()) {
+    hipEvent_t e = g_timing.pool.back();
+    g_timing.pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+// Run `launch` bracketed by events on stream s when timing is on.
+template <typename F>
+hipError_t timed(int cls, double flops, double bytes, hipStream_t s, F&& launch) {
+  if (!g_timing.on) return launch();
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  TimedLaunch t{cls, take_event(), take_event(), flops, bytes};
+  hipEventRecord(t.beg, s);
+  hipError_t e = launch();
+  hipEventRecord(t.end, s);
+  g_timing.pending.push_back(t);
+  return e;
+}
+
+bool valid_kdesc(const gpk_kdesc* kd, int64_t d) {
+  if (!kd || kd->n_nodes <= 0 || kd->n_nodes > GPK_MAX_NODES) return false;
+  if (kd->n_hyp < 0 || kd->n_hyp > GPK_MAX_HYP || kd->dim != d) return false;
+  if (kd->n_ard < 0 || kd->n_ard > GPK_MAX_ARD) return false;
+  int sp = 0;
+  for (int q = 0; q < kd->n_nodes; ++q) {
+    const gpk_node& nd = kd->nodes[q];
+    if (nd.op == GPK_OP_ADD || nd.op == GPK_OP_MUL) {
+      if (sp < 2) return false;
+      sp -= 1;
+    } else if (nd.op == GPK_OP_SE || nd.op == GPK_OP_PER || nd.op == GPK_OP_MAT32 ||
+               nd.op == GPK_OP_MAT52) {
+      const bool ard = (nd.flags & GPK_NODE_ARD) != 0;
+      if (ard && (nd.op == GPK_OP_PER || nd.ard_slot < 0 || nd.ard_slot >= kd->n_ard)) return false;
+      int need = (nd.op == GPK_OP_PER) ? 2 : (ard ? (int)d : 1);
+      if (nd.flags & GPK_NODE_SCALED) need += 1;
+      if (nd.hyp_offset < 0 || nd.hyp_offset + need > kd->n_hyp) return false;
+      sp += 1;
+      if (sp > 8) return false;
+    } else {
+      return false;
+    }
+  }
+  return sp == 1;
+}
+
+size_t elem_size(int dtype) { return dtype == GPK_F64 ? 8 : 4; }
+
+}  // namespace
+
+extern "C" {
+
+int gpk_abi_version(void) { return GPK_ABI_VERSION; }
+
+const char* gpk_last_error(void) { return g_err.c_str(); }
+
+int gpk_plan(int dtype, int32_t batch, int64_t n, int64_t m, int64_t d, gpk_layout* out) {
+  if (dtype != GPK_F64 && dtype != GPK_F32) return fail_arg(1, "dtype");
+  if (batch <= 0) return fail_arg(2, "batch must be > 0");
+  if (n <= 0) return fail_arg(3, "n must be > 0");
+  if (m < 0) return fail_arg(4, "m must be >= 0");
+  if (d <= 0 || d > GPK_MAX_DIM) return fail_arg(5, "d must be in [1, 16]");
+  if (!out) return fail_arg(6, "out");
+  gpk_layout L;
+  memset(&L, 0, sizeof(L));
+  L.dtype = dtype;
+  L.batch = batch;
+  L.n = n;
+  L.m = m;
+  L.d = d;
+  L.nb = NB;
+  L.n_pad = (n + NB - 1) / NB * NB;
+  L.y_row = L.n_pad + m;
+  L.p = (L.y_row + 1 + NB - 1) / NB * NB;
+  L.ld = L.p;
+  L.w_batch_stride = L.p * L.ld;
+  L.inv_batch_stride = (L.n_pad / NB) * NB * NB;
+  L.w_bytes = (size_t)batch * (size_t)L.w_batch_stride * elem_size(dtype);
+  L.inv_bytes = (size_t)batch * (size_t)L.inv_batch_stride * elem_size(dtype);
+  *out = L;
+  return 0;
+}
+
+static int check_layout(const gpk_layout* lay) {
+  if (!lay) return fail_arg(1, "layout");
+  if ((lay->dtype != GPK_F64 && lay->dtype != GPK_F32) || lay->batch <= 0 || lay->nb != NB ||
+      lay->n_pad % NB != 0 || lay->p % NB != 0 || lay->ld < lay->p || lay->y_row >= lay->p ||
+      lay->n <= 0 || lay->n > lay->n_pad)
+    return fail_arg(1, "layout (use gpk_plan)");
+  return 0;
+}
+
+int gpk_assemble(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+                 int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+                 const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
+                 const double* E, int64_t e_bstride, const double* y, int64_t y_bstride,
+                 void* W, void* stream) {
+  if (int e = check_layout(lay)) return e;
+  if (!valid_kdesc(kd, lay->d)) return fail_arg(1, "kernel descriptor");
+  if (!hyp_dev && kd->n_hyp > 0) return fail_arg(3, "hyp_dev");
+  if (!noise_dev) return fail_arg(5, "noise_dev");
+  if (!X) return fail_arg(7, "X");
+  if (lay->m > 0 && !Xs && !E) return fail_arg(9, "Xs or E");
+  if (!y) return fail_arg(13, "y");
+  if (!W) return fail_arg(15, "W");
+  AsmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.hyp = hyp_dev;
+  a.hyp_stride = hyp_stride;
+  a.noise = noise_dev;
+  a.noise_stride = noise_stride;
+  a.X = X;
+  a.x_bs = x_bstride;
+  a.Xs = Xs ? Xs : X;
+  a.xs_bs = xs_bstride;
+  a.E = (lay->m > 0) ? E : nullptr;
+  a.e_bs = e_bstride;
+  a.y = y;
+  a.y_bs = y_bstride;
+  a.W = W;
+  a.ld = lay->ld;
+  a.w_bs = lay->w_batch_stride;
+  a.n = lay->n;
+  a.m = lay->m;
+  a.n_pad = lay->n_pad;
+  a.y_row = lay->y_row;
+  a.p = lay->p;
+  a.d = (int32_t)lay->d;
+  a.dp = (lay->d % 2 == 0) ? (int32_t)lay->d + 1 : (int32_t)lay->d;
+  a.plain = 0;
+  a.ntile = lay->p / ATILE;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const double es = (double)elem_size(lay->dtype);
+  const double bytes = (double)lay->batch *
+                       (es * (double)lay->p * (double)(lay->p + ATILE) / 2.0 +
+                        8.0 * (double)(lay->n + lay->m) * (double)lay->d + 8.0 * (double)lay->n);
+  GPK_HIP(timed(0, 0.0, bytes, s, [&] { return launch_assemble(*kd, a, lay->dtype, lay->batch, s); }),
+          "assemble");
+  return 0;
+}
+
+int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, void* stream) {
+  if (int e = check_layout(lay)) return e;
+  if (!W) return fail_arg(2, "W");
+  if (!Winv) return fail_arg(3, "Winv");
+  if (!info_dev) return fail_arg(4, "info_dev");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int dt = lay->dtype;
+  const size_t es = elem_size(dt);
+  const int64_t nblk = lay->n_pad / NB;
+  for (int64_t k = 0; k < nblk; ++k) {
+    const int64_t j0 = k * NB;
+    DiagArgs da;
+    da.W = W;
+    da.ld = lay->ld;
+    da.w_bs = lay->w_batch_stride;
+    da.Winv = Winv;
+    da.inv_bs = lay->inv_batch_stride;
+    da.j0 = j0;
+    da.kblk = k;
+    da.info = info_dev;
+    GPK_HIP(timed(1, (double)lay->batch * NB * NB * NB / 3.0, 0.0, s,
+                  [&] { return launch_diag(da, dt, lay->batch, s); }),
+            "diag");
+    const int64_t row0 = j0 + NB;
+    const int32_t nt = (int32_t)((lay->p - row0) / NB);
+    if (nt <= 0) continue;
+    GemmArgs ga;
+    ga.W = W;
+    ga.ld = lay->ld;
+    ga.w_bs = lay->w_batch_stride;
+    ga.Binv = static_cast<const char*>(Winv) + (size_t)k * NB * NB * es;
+    ga.inv_bs = lay->inv_batch_stride;
+    ga.j0 = j0;
+    ga.row0 = row0;
+    ga.nt = nt;
+    ga.c_lo = 0;
+    ga.c_hi = nt;
+    // algorithmic work: rows below the block of the K part times the panel (solve)
+    const double rK = (double)(lay->n_pad - row0);
+    GPK_HIP(timed(2, (double)lay->batch * rK * NB * NB, 0.0, s,
+                  [&] { return launch_gemm(ga, dt, GEMM_TRSM, lay->batch, s); }),
+            "trsm");
+    // algorithmic work of the trailing SYRK on the K part: 2 * nb * r(r+1)/2
+    GPK_HIP(timed(3, (double)lay->batch * NB * rK * (rK + 1.0), 0.0, s,
+                  [&] { return launch_gemm(ga, dt, GEMM_UPDATE, lay->batch, s); }),
+            "update");
+  }
+  return 0;
+}
+
+int gpk_finalize(const gpk_layout* lay, const void* W, const int32_t* info_dev, double* out_dev,
+                 double* mu_dev, double* var_dev, void* stream) {
+  if (int e = check_layout(lay)) return e;
+  if (!W) return fail_arg(2, "W");
+  if (!info_dev) return fail_arg(3, "info_dev");
+  if (!out_dev) return fail_arg(4, "out_dev");
+  FinArgs f;
+  f.W = W;
+  f.ld = lay->ld;
+  f.w_bs = lay->w_batch_stride;
+  f.n = lay->n;
+  f.m = lay->m;
+  f.n_pad = lay->n_pad;
+  f.y_row = lay->y_row;
+  f.info = info_dev;
+  f.out = out_dev;
+  f.mu = mu_dev;
+  f.var = var_dev;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(timed(4, 0.0, 0.0, s, [&] { return launch_finalize(f, lay->dtype, lay->batch, s); }),
+          "finalize");
+  return 0;
+}
+
+int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, int64_t hyp_stride,
+             const double* noise_dev, int64_t noise_stride, const double* X, int64_t x_bstride,
+             const double* y, int64_t y_bstride, void* W, void* Winv, int32_t* info_dev,
+             double* out_dev, void* stream) {
+  if (int e = check_layout(lay)) return e;
+  if (lay->m != 0) return fail_arg(2, "gpk_nlml needs a layout planned with m = 0");
+  if (!info_dev) return fail_arg(13, "info_dev");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(hipMemsetAsync(info_dev, 0, sizeof(int32_t) * lay->batch, s), "memset info");
+  int e = gpk_assemble(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, nullptr,
+                       0, nullptr, 0, y, y_bstride, W, stream);
+  if (e) return e;
+  e = gpk_potrf_aug(lay, W, Winv, info_dev, stream);
+  if (e) return e;
+  return gpk_finalize(lay, W, info_dev, out_dev, nullptr, nullptr, stream);
+}
+
+int gpk_kernel_matrix(const gpk_kdesc* kd, const double* hyp_dev, int dtype, int uplo,
+                      const double* X, int64_t n, const double* Y, int64_t m, int32_t d,
+                      double diag_add, void* K, int64_t ldk, void* stream) {
+  if (!valid_kdesc(kd, d)) return fail_arg(1, "kernel descriptor");
+  if (!hyp_dev && kd->n_hyp > 0) return fail_arg(2, "hyp_dev");
+  if (dtype != GPK_F64 && dtype != GPK_F32) return fail_arg(3, "dtype");
+  if (uplo != 0 && uplo != 1) return fail_arg(4, "uplo");
+  if (!X) return fail_arg(5, "X");
+  if (n <= 0) return fail_arg(6, "n");
+  if (!Y) return fail_arg(7, "Y");
+  if (m <= 0) return fail_arg(8, "m");
+  if (d <= 0 || d > GPK_MAX_DIM) return fail_arg(9, "d");
+  if (!K) return fail_arg(11, "K");
+  if (ldk < m) return fail_arg(12, "ldk");
+  AsmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.hyp = hyp_dev;
+  a.noise = nullptr;
+  a.X = X;
+  a.Xs = Y;
+  a.W = K;
+  a.ld = ldk;
+  a.n = n;
+  a.m = m;
+  a.d = d;
+  a.dp = (d % 2 == 0) ? d + 1 : d;
+  a.plain = 1;
+  a.uplo = uplo;
+  a.diag_add = diag_add;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const double bytes = (double)elem_size(dtype) * (double)n * (double)m;
+  GPK_HIP(timed(0, 0.0, bytes, s, [&] { return launch_assemble(*kd, a, dtype, 1, s); }),
+          "kernel_matrix");
+  return 0;
+}
+
+int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, double* x,
+             void* stream) {
+  if (int e = check_layout(lay)) return e;
+  if (trans != 0 && trans != 1) return fail_arg(2, "trans");
+  if (!W) return fail_arg(3, "W");
+  if (!Winv) return fail_arg(4, "Winv");
+  if (!x) return fail_arg(5, "x");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nblk = lay->n_pad / NB;
+  TrsvArgs t;
+  t.W = W;
+  t.ld = lay->ld;
+  t.w_bs = lay->w_batch_stride;
+  t.Winv = Winv;
+  t.inv_bs = lay->inv_batch_stride;
+  t.x = x;
+  t.x_bs = lay->n_pad;
+  t.n_pad = lay->n_pad;
+  t.trans = trans;
+  for (int64_t i = 0; i < nblk; ++i) {
+    t.kblk = (trans == 0) ? i : nblk - 1 - i;
+    GPK_HIP(timed(5, 0.0, 0.0, s, [&] { return launch_trsv_diag(t, lay->dtype, lay->batch, s); }),
+            "trsv_diag");
+    GPK_HIP(timed(5, 0.0, 0.0, s, [&] { return launch_trsv_update(t, lay->dtype, lay->batch, s); }),
+            "trsv_update");
+  }
+  return 0;
+}
+
+int gpk_timing_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  g_timing.on = on != 0;
+  return 0;
+}
+
+int gpk_timing_reset(void) {
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  for (auto& t : g_timing.pending) {
+    hipEventSynchronize(t.end);
+    g_timing.pool.push_back(t.beg);
+    g_timing.pool.push_back(t.end);
+  }
+  g_timing.pending.clear();
+  for (int c = 0; c < GPK_NUM_CLASSES; ++c) {
+    g_timing.ms[c] = 0;
+    g_timing.launches[c] = 0;
+    g_timing.flops[c] = 0;
+    g_timing.bytes[c] = 0;
+  }
+  return 0;
+}
+
+int gpk_timing_read(double* ms_by_class, int64_t* launches_by_class, double* flops_by_class,
+                    double* bytes_by_class) {
+  std::lock_guard<std::mutex> lk(g_timing.mu);
+  for (auto& t : g_timing.pending) {
+    hipError_t e = hipEventSynchronize(t.end);
+    if (e != hipSuccess) return fail_hip(e, "timing sync");
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, t.beg, t.end);
+    g_timing.ms[t.cls] += ms;
+    g_timing.launches[t.cls] += 1;
+    g_timing.flops[t.cls] += t.flops;
+    g_timing.bytes[t.cls] += t.bytes;
+    g_timing.pool.push_back(t.beg);
+    g_timing.pool.push_back(t.end);
+  }
+  g_timing.pending.clear();
+  for (int c = 0; c < GPK_NUM_CLASSES; ++c) {
+    if (ms_by_class) ms_by_class[c] = g_timing.ms[c];
+    if (launches_by_class) launches_by_class[c] = g_timing.launches[c];
+    if (flops_by_class) flops_by_class[c] = g_timing.flops[c];
+    if (bytes_by_class) bytes_by_class[c] = g_timing.bytes[c];
+  }
+  return 0;
+}
+
+}  // extern "C"

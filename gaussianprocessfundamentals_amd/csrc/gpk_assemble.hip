@@ -1,0 +1,263 @@
+// Kernel-matrix build (the HBM-write-bound half of the LML hot path).
+//
+// One 256-thread workgroup writes one 64 x 64 tile.  The tile's 64 row points and 64 column
+// points (plus their per-ARD-node rescaled copies) are staged once in LDS; every lane then
+// owns one column and walks 16 rows, evaluating the postfix kernel program in registers and
+// storing whole 512-B rows (64 consecutive fp64 per wave instruction).  In the augmented
+// layout only lower-triangular tiles are launched (the factorisation never reads the upper
+// triangle), so the bytes written are p(p+64)/2 elements per batch member.
+//
+// Reference semantics (paths relative to gpbasics/):
+//   SE     KernelBasics/BaseKernels.py:277-294   exp(-0.5 * (dist^2 / l^2)), sg * (..) if scaled
+//   PER    KernelBasics/BaseKernels.py:440-457   exp((-2 sin^2(pi * (d1 / p))) / l^2)
+//   MAT32  KernelBasics/BaseKernels.py:702-720   (1 + f) e^-f,            f = (sqrt3 d1) / |l|
+//   MAT52  KernelBasics/BaseKernels.py:859-880   ((1 + f) + 5 d1^2 / (3 l^2)) e^-f,  f = (sqrt5 d1) / |l|
+//   ADD/MUL KernelBasics/Operators.py:207-225, :306-326 (left fold over children)
+//   d1 = L1 distance (Auxiliary/Distances.py:10-12); SE distance either the expanded norm of
+//   Auxiliary/Distances.py:4-7 (GPK_NODE_SE_EXPANDED) or the direct sum of squares.
+//   noise on the training diagonal only: Statistics/CovarianceMatrix.py:197-206; K_ss has none
+//   (:218-225); K_s = k(X, X_test) (:277-286).
+#include "gpk_internal.h"
+
+namespace gpk {
+namespace {
+
+constexpr double SQRT3 = 1.7320508075688772;
+constexpr double SQRT5 = 2.23606797749979;
+constexpr double PI = 3.141592653589793;
+
+__device__ __forceinline__ double base_value(const gpk_node& nd, const double* __restrict__ hyp,
+                                             const double* a, const double* b, int d) {
+  const int fl = nd.flags;
+  const bool ard = (fl & GPK_NODE_ARD) != 0;
+  const double* h = hyp + nd.hyp_offset;
+  double r;
+  int sg_at;
+  if (nd.op == GPK_OP_SE) {
+    double s;
+    if (fl & GPK_NODE_SE_EXPANDED) {
+      double na = 0.0, nb = 0.0, ab = 0.0;
+      for (int k = 0; k < d; ++k) {
+        na += a[k] * a[k];
+        nb += b[k] * b[k];
+        ab += a[k] * b[k];
+      }
+      const double dist = sqrt((na - 2.0 * ab) + nb);  // NaN on a negative argument, as the reference
+      s = dist * dist;
+    } else {
+      s = 0.0;
+      for (int k = 0; k < d; ++k) {
+        const double t = a[k] - b[k];
+        s += t * t;
+      }
+    }
+    const double l = ard ? 1.0 : h[0];
+    r = exp(-0.5 * (s / (l * l)));
+    sg_at = ard ? d : 1;
+  } else if (nd.op == GPK_OP_PER) {
+    const double l = h[0], per = h[1];
+    double sn;
+    if (fl & GPK_NODE_STANDARD) {  // product of 1-D periodic kernels
+      sn = 0.0;
+      for (int k = 0; k < d; ++k) {
+        const double t = sin(PI * (fabs(a[k] - b[k]) / per));
+        sn += t * t;
+      }
+    } else {
+      double dist = 0.0;
+      for (int k = 0; k < d; ++k) dist += fabs(a[k] - b[k]);
+      sn = sin(PI * (dist / per));
+      sn = sn * sn;
+    }
+    r = exp((-2.0 * sn) / (l * l));
+    sg_at = 2;
+  } else {  // MAT32 / MAT52
+    double dist = 0.0;
+    if (fl & GPK_NODE_STANDARD) {  // Euclidean distance
+      for (int k = 0; k < d; ++k) {
+        const double t = a[k] - b[k];
+        dist += t * t;
+      }
+      dist = sqrt(dist);
+    } else {
+      for (int k = 0; k < d; ++k) dist += fabs(a[k] - b[k]);
+    }
+    const double l = ard ? 1.0 : fabs(h[0]);
+    if (nd.op == GPK_OP_MAT52) {
+      const double frac = (SQRT5 * dist) / l;
+      const double third = (5.0 * (dist * dist)) / (3.0 * (l * l));
+      r = ((1.0 + frac) + third) * exp(-frac);
+    } else {
+      const double frac = (SQRT3 * dist) / l;
+      r = (1.0 + frac) * exp(-frac);
+    }
+    sg_at = ard ? d : 1;
+  }
+  if (fl & GPK_NODE_SCALED) r = h[sg_at] * r;
+  return r;
+}
+
+// Register stack of the postfix program.  The stack pointer is wave-uniform, so the switch
+// lowers to scalar branches and nothing is indexed dynamically (no scratch).
+struct Stack {
+  double s0, s1, s2, s3, s4, s5, s6, s7;
+  __device__ __forceinline__ double get(int i) const {
+    switch (i) {
+      case 0: return s0; case 1: return s1; case 2: return s2; case 3: return s3;
+      case 4: return s4; case 5: return s5; case 6: return s6; default: return s7;
+    }
+  }
+  __device__ __forceinline__ void set(int i, double v) {
+    switch (i) {
+      case 0: s0 = v; break; case 1: s1 = v; break; case 2: s2 = v; break; case 3: s3 = v; break;
+      case 4: s4 = v; break; case 5: s5 = v; break; case 6: s6 = v; break; default: s7 = v; break;
+    }
+  }
+};
+
+__device__ __forceinline__ double eval_tree(const gpk_kdesc& kd, const double* hyp, const double* pa,
+                                            const double* pb, int slot_stride, int d) {
+  Stack st;
+  st.s0 = 0.0;
+  int sp = 0;
+  for (int q = 0; q < kd.n_nodes; ++q) {
+    const gpk_node nd = kd.nodes[q];
+    if (nd.op == GPK_OP_ADD || nd.op == GPK_OP_MUL) {
+      const double top = st.get(sp - 1);
+      const double below = st.get(sp - 2);
+      st.set(sp - 2, nd.op == GPK_OP_ADD ? below + top : below * top);
+      sp -= 1;
+    } else {
+      const int off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
+      st.set(sp, base_value(nd, hyp, pa + off, pb + off, d));
+      sp += 1;
+    }
+  }
+  return st.s0;
+}
+
+enum { CLS_TRAIN = 0, CLS_PAD = 1, CLS_TEST = 2, CLS_Y = 3, CLS_ZERO = 4 };
+
+__device__ __forceinline__ int classify(const AsmArgs& a, int64_t g) {
+  if (g < a.n) return CLS_TRAIN;
+  if (g < a.n_pad) return CLS_PAD;
+  if (g < a.n_pad + a.m) return CLS_TEST;
+  if (g == a.y_row) return CLS_Y;
+  return CLS_ZERO;
+}
+
+// Stage 64 points (raw + per-ARD-node rescaled copies) of one tile edge into LDS.
+__device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs& a, const double* hyp,
+                                             double* dst, int64_t g0, int b, bool rows, int slot_stride) {
+  const int tid = threadIdx.x;
+  for (int e = tid; e < ATILE * a.d; e += 256) {
+    const int pt = e / a.d, k = e - pt * a.d;
+    const int64_t g = g0 + pt;
+    double v = 0.0;
+    if (a.plain) {
+      const int64_t lim = rows ? a.n : a.m;
+      const double* src = rows ? a.X : a.Xs;
+      if (g < lim) v = src[g * a.d + k];
+    } else {
+      const int c = classify(a, g);
+      if (c == CLS_TRAIN) v = a.X[(int64_t)b * a.x_bs + g * a.d + k];
+      else if (c == CLS_TEST && a.E == nullptr) v = a.Xs[(int64_t)b * a.xs_bs + (g - a.n_pad) * a.d + k];
+    }
+    dst[pt * a.dp + k] = v;
+    // ARD copies: u = x / ls (the reference kernel with l = 1 on rescaled inputs)
+    for (int q = 0; q < kd.n_nodes; ++q) {
+      const gpk_node nd = kd.nodes[q];
+      if (nd.op != GPK_OP_ADD && nd.op != GPK_OP_MUL && (nd.flags & GPK_NODE_ARD))
+        dst[(nd.ard_slot + 1) * slot_stride + pt * a.dp + k] = v / hyp[nd.hyp_offset + k];
+    }
+  }
+}
+
+template <typename TOut>
+__global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int slot_stride = ATILE * a.dp;
+  double* hyp_s = smem;                                  // GPK_MAX_HYP
+  double* prow = smem + GPK_MAX_HYP;                     // (1 + n_ard) * slot_stride
+  double* pcol = prow + (1 + kd.n_ard) * slot_stride;
+
+  const int b = blockIdx.y;
+  int64_t ti, tj;
+  if (a.plain) {
+    ti = blockIdx.x / ((a.m + ATILE - 1) / ATILE);
+    tj = blockIdx.x - ti * ((a.m + ATILE - 1) / ATILE);
+    if (a.uplo && tj > ti) return;
+  } else {
+    // lower-triangular tile enumeration, row-major
+    const int64_t t = blockIdx.x;
+    int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while (r * (r + 1) / 2 > t) --r;
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    ti = r;
+    tj = t - r * (r + 1) / 2;
+  }
+  const int tid = threadIdx.x;
+  const double* hyp_g = a.hyp + (int64_t)b * a.hyp_stride;
+  for (int e = tid; e < kd.n_hyp; e += 256) hyp_s[e] = hyp_g[e];
+  __syncthreads();
+  const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
+  stage_points(kd, a, hyp_s, prow, gi0, b, true, slot_stride);
+  stage_points(kd, a, hyp_s, pcol, gj0, b, false, slot_stride);
+  __syncthreads();
+
+  const int c = tid & 63;
+  const int r0 = tid >> 6;
+  const int64_t gj = gj0 + c;
+  TOut* W = reinterpret_cast<TOut*>(a.W) + (int64_t)b * a.w_bs;
+  if (a.plain) {
+    for (int rr = r0; rr < ATILE; rr += 4) {
+      const int64_t gi = gi0 + rr;
+      if (gi >= a.n || gj >= a.m) continue;
+      if (a.uplo && gj > gi) continue;
+      double v = eval_tree(kd, hyp_s, prow + rr * a.dp, pcol + c * a.dp, slot_stride, a.d);
+      if (gi == gj) v += a.diag_add;
+      W[gi * a.ld + gj] = (TOut)v;
+    }
+    return;
+  }
+  const double noise = a.noise[(int64_t)b * a.noise_stride];
+  const int ccls = classify(a, gj);
+  const double yv = (ccls == CLS_TRAIN) ? a.y[(int64_t)b * a.y_bs + gj] : 0.0;
+  for (int rr = r0; rr < ATILE; rr += 4) {
+    const int64_t gi = gi0 + rr;
+    const int rcls = classify(a, gi);
+    double v = 0.0;
+    if (rcls == CLS_PAD || ccls == CLS_PAD) {
+      v = (gi == gj) ? 1.0 : 0.0;
+    } else if (a.E != nullptr && rcls == CLS_TEST) {
+      v = (ccls == CLS_TRAIN) ? a.E[(int64_t)b * a.e_bs + (gi - a.n_pad) * a.n + gj] : 0.0;
+    } else if ((rcls == CLS_TRAIN || rcls == CLS_TEST) && (ccls == CLS_TRAIN || ccls == CLS_TEST)) {
+      v = eval_tree(kd, hyp_s, prow + rr * a.dp, pcol + c * a.dp, slot_stride, a.d);
+      if (rcls == CLS_TRAIN && ccls == CLS_TRAIN && gi == gj) v += noise;
+    } else if (rcls == CLS_Y && ccls == CLS_TRAIN) {
+      v = yv;
+    }
+    W[gi * a.ld + gj] = (TOut)v;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
+                           hipStream_t s) {
+  const size_t lds = sizeof(double) * (GPK_MAX_HYP + 2 * (size_t)(1 + kd.n_ard) * ATILE * a.dp);
+  dim3 grid;
+  if (a.plain) {
+    const int64_t tr = (a.n + ATILE - 1) / ATILE, tc = (a.m + ATILE - 1) / ATILE;
+    grid = dim3((unsigned)(tr * tc), 1, 1);
+  } else {
+    grid = dim3((unsigned)(a.ntile * (a.ntile + 1) / 2), (unsigned)batch, 1);
+  }
+  if (dtype == GPK_F64)
+    hipLaunchKernelGGL(assemble_kernel<double>, grid, dim3(256), lds, s, kd, a);
+  else
+    hipLaunchKernelGGL(assemble_kernel<float>, grid, dim3(256), lds, s, kd, a);
+  return hipGetLastError();
+}
+
+}  // namespace gpk

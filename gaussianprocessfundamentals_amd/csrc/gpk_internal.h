@@ -1,0 +1,101 @@
+// Internal declarations shared by the libgpk translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gpk.h"
+
+namespace gpk {
+
+constexpr int NB = 128;     // panel width == update tile edge == diagonal block edge
+constexpr int ATILE = 64;   // assemble tile edge
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ----------------------------------------------------------------------------------- launch args
+struct AsmArgs {
+  const double* hyp;
+  int64_t hyp_stride;
+  const double* noise;
+  int64_t noise_stride;
+  const double* X;
+  int64_t x_bs;
+  const double* Xs;
+  int64_t xs_bs;
+  const double* E;   // explicit extra rows (NULL: kernel rows of Xs)
+  int64_t e_bs;
+  const double* y;
+  int64_t y_bs;
+  void* W;
+  int64_t ld;
+  int64_t w_bs;
+  int64_t n, m, n_pad, y_row, p;
+  int32_t d;
+  int32_t dp;        // LDS row stride of a point (odd when d is even: no bank conflicts)
+  int32_t plain;     // 0 = augmented layout, 1 = plain rectangular kernel matrix
+  int32_t uplo;      // plain mode: 1 = write j <= i only
+  int64_t ntile;     // augmented: 64-tiles per dimension
+  double diag_add;   // plain mode
+};
+
+struct GemmArgs {
+  void* W;
+  int64_t ld;
+  int64_t w_bs;
+  const void* Binv;  // trsm: inverted diagonal block of this step
+  int64_t inv_bs;
+  int64_t j0;        // first column of the panel
+  int64_t row0;      // first row (and column) of the trailing region
+  int32_t nt;        // 128-tiles of the trailing region
+  int32_t c_lo, c_hi;  // tile-column range handled by this launch (update)
+};
+
+struct DiagArgs {
+  void* W;
+  int64_t ld;
+  int64_t w_bs;
+  void* Winv;
+  int64_t inv_bs;
+  int64_t j0;
+  int64_t kblk;
+  int32_t* info;
+};
+
+struct FinArgs {
+  const void* W;
+  int64_t ld;
+  int64_t w_bs;
+  int64_t n, m, n_pad, y_row;
+  const int32_t* info;
+  double* out;
+  double* mu;
+  double* var;
+};
+
+struct TrsvArgs {
+  const void* W;
+  int64_t ld;
+  int64_t w_bs;
+  const void* Winv;
+  int64_t inv_bs;
+  double* x;
+  int64_t x_bs;
+  int64_t kblk;
+  int64_t n_pad;
+  int32_t trans;
+};
+
+// ----------------------------------------------------------------------------------- launchers
+hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
+                           hipStream_t s);
+hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s);
+hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int32_t batch, hipStream_t s);
+hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream_t s);
+hipError_t launch_trsv_diag(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
+hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
+
+enum { GEMM_UPDATE = 0, GEMM_TRSM = 1 };
+
+}  // namespace gpk

@@ -1,0 +1,241 @@
+"""Device engine: the glue between the gpbasics-style Python objects and libgpk.
+
+* :func:`kernel_descriptor` flattens a kernel tree (KernelBasics) into the postfix program the
+  HIP kernels evaluate (include/gpk.h, ``gpk_kdesc``).
+* :func:`pack_hyper_parameter` concatenates a hyperparameter list in DFS order, the layout of
+  ``Component.serialize_hyper_parameter`` (gpbasics/Auxiliary/BasicGPComponent.py:16-23).
+* :class:`AugmentedFactorization` owns the device buffers of one factorisation of the augmented
+  matrix (training block + optional extra rows + the y row) and reads results out of it.
+
+All arithmetic runs in libgpk on the GPU; torch only allocates and views device memory.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _native as nat
+from . import global_parameters as gp
+
+
+class CholeskyError(RuntimeError):
+    """Cholesky of K + noise*I failed (not positive definite).  The reference propagates
+    TensorFlow's InvalidArgumentError from tf.linalg.cholesky
+    (gpbasics/Statistics/CovarianceMatrix.py:250)."""
+
+    def __init__(self, info):
+        super().__init__("Cholesky decomposition was not successful: leading minor of order %s is "
+                         "not positive definite" % (info,))
+        self.info = info
+
+
+def device() -> torch.device:
+    d = torch.device(gp.p_device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+def as_device_f64(x) -> torch.Tensor:
+    """fp64 device copy/view of array-like x (the reference casts every input to p_dtype=fp64,
+    gpbasics/DataHandling/DataInput.py:198-206)."""
+    if isinstance(x, torch.Tensor):
+        t = x.detach()
+    else:
+        t = torch.as_tensor(x)
+    return t.to(device=device(), dtype=torch.float64).contiguous()
+
+
+# ----------------------------------------------------------------------------- kernel programs
+def kernel_descriptor(kernel, dim: Optional[int] = None) -> nat.GpkKdesc:
+    """Flatten ``kernel`` (a Kernel tree) to the postfix program of include/gpk.h."""
+    dim = int(dim if dim is not None else kernel.get_dimensionality())
+    nodes: List[tuple] = []
+    slots: List[int] = []
+    n_hyp = kernel._emit(nodes, 0, slots, dim)
+    if len(nodes) > nat.MAX_NODES:
+        raise ValueError("kernel tree too large for the device program (%d > %d nodes)"
+                         % (len(nodes), nat.MAX_NODES))
+    if len(slots) > nat.MAX_ARD:
+        raise ValueError("at most %d ARD base kernels per tree" % nat.MAX_ARD)
+    if n_hyp > nat.MAX_HYP:
+        raise ValueError("too many hyperparameters (%d > %d)" % (n_hyp, nat.MAX_HYP))
+    if dim < 1 or dim > nat.MAX_DIM:
+        raise ValueError("input dimensionality must be in [1, %d]" % nat.MAX_DIM)
+    kd = nat.GpkKdesc()
+    kd.n_nodes = len(nodes)
+    kd.n_hyp = n_hyp
+    kd.dim = dim
+    kd.n_ard = len(slots)
+    for i, (op, off, slot, flags) in enumerate(nodes):
+        kd.nodes[i].op = op
+        kd.nodes[i].hyp_offset = off
+        kd.nodes[i].ard_slot = slot
+        kd.nodes[i].flags = flags
+    return kd
+
+
+def pack_hyper_parameter(hyper_parameter: Sequence, n_expected: Optional[int] = None) -> torch.Tensor:
+    """Flat fp64 device vector of a hyperparameter list (each entry reshaped to [-1], concatenated;
+    BasicGPComponent.serialize_hyper_parameter, gpbasics/Auxiliary/BasicGPComponent.py:16-23)."""
+    dev = device()
+    if isinstance(hyper_parameter, torch.Tensor) and hyper_parameter.dim() == 1:
+        flat = hyper_parameter.to(device=dev, dtype=torch.float64)
+    else:
+        parts = []
+        host_vals = []
+        all_host = True
+        for h in hyper_parameter:
+            if isinstance(h, torch.Tensor) and h.device.type != "cpu":
+                all_host = False
+                break
+        if all_host:
+            for h in hyper_parameter:
+                if isinstance(h, torch.Tensor):
+                    host_vals.extend(float(v) for v in h.detach().reshape(-1).tolist())
+                else:
+                    try:
+                        host_vals.extend(float(v) for v in h)
+                    except TypeError:
+                        host_vals.append(float(h))
+            flat = torch.tensor(host_vals, dtype=torch.float64, device=dev)
+        else:
+            for h in hyper_parameter:
+                parts.append(torch.as_tensor(h).to(device=dev, dtype=torch.float64).reshape(-1))
+            flat = torch.cat(parts) if parts else torch.zeros(0, dtype=torch.float64, device=dev)
+    if n_expected is not None and flat.numel() != n_expected:
+        raise ValueError("hyperparameter vector has %d values, kernel expects %d"
+                         % (flat.numel(), n_expected))
+    return flat.contiguous()
+
+
+def kernel_matrix(kernel, hyper_parameter, x, x_, diag_add: float = 0.0, lower: bool = False,
+                  out_dtype=None) -> torch.Tensor:
+    """k(x, x_) as an [n, m] device tensor via gpk_kernel_matrix (K/Kernel.py:51-52)."""
+    L = nat.lib()
+    x = as_device_f64(x)
+    x_ = as_device_f64(x_)
+    if x.dim() != 2 or x_.dim() != 2 or x.shape[1] != x_.shape[1]:
+        raise ValueError("kernel inputs must be [n, D] and [m, D]")
+    kd = kernel_descriptor(kernel, x.shape[1])
+    hyp = pack_hyper_parameter(hyper_parameter, kd.n_hyp)
+    dt = out_dtype or torch.float64
+    n, m = x.shape[0], x_.shape[0]
+    K = torch.empty((n, m), dtype=dt, device=x.device)
+    if n == 0 or m == 0:
+        return K
+    nat.check(L.gpk_kernel_matrix(ctypes.byref(kd), nat.ptr(hyp), nat.dtype_code(dt), 1 if lower else 0,
+                                  nat.ptr(x), n, nat.ptr(x_), m, x.shape[1], float(diag_add),
+                                  nat.ptr(K), m, nat.stream_handle(x.device)), "gpk_kernel_matrix")
+    return K
+
+
+# ----------------------------------------------------------------------------- factorisation
+class AugmentedFactorization:
+    """One factorisation of the augmented matrix W (include/gpk.h) for ``batch`` problems.
+
+    After :meth:`run`, W's first n_pad columns hold L, the y row holds z = L^-1 y, the extra rows
+    hold V^T = Ks^T L^-T and the corner holds the Schur complement (posterior covariance,
+    -posterior mean, -z^T z).
+    """
+
+    def __init__(self, n: int, d: int, m: int = 0, batch: int = 1, dtype=None):
+        self.L = nat.lib()
+        self.dtype = dtype or gp.p_dtype
+        self.code = nat.dtype_code(self.dtype)
+        self.n, self.d, self.m, self.batch = int(n), int(d), int(m), int(batch)
+        self.layout = nat.plan(self.code, self.batch, self.n, self.m, self.d)
+        lay = self.layout
+        dev = device()
+        es = 8 if self.code == nat.GPK_F64 else 4
+        self.W = torch.empty(lay.w_bytes // es, dtype=self.dtype, device=dev)
+        self.Winv = torch.empty(max(1, lay.inv_bytes // es), dtype=self.dtype, device=dev)
+        self.info = torch.zeros(self.batch, dtype=torch.int32, device=dev)
+        self.out = torch.empty(self.batch * 4, dtype=torch.float64, device=dev)
+        self.mu = torch.empty(max(1, self.batch * self.m), dtype=torch.float64, device=dev)
+        self.var = torch.empty(max(1, self.batch * self.m), dtype=torch.float64, device=dev)
+        self.kd = None
+        self.done = False
+        self.shape_key = None
+
+    # -- launches ---------------------------------------------------------------------------
+    def run(self, kd: nat.GpkKdesc, hyp: torch.Tensor, hyp_stride: int, noise: torch.Tensor,
+            noise_stride: int, X: torch.Tensor, x_bstride: int, y: torch.Tensor, y_bstride: int,
+            Xs: Optional[torch.Tensor] = None, xs_bstride: int = 0,
+            E: Optional[torch.Tensor] = None, e_bstride: int = 0):
+        lay = self.layout
+        s = nat.stream_handle(self.W.device)
+        L = self.L
+        self.info.zero_()
+        nat.check(L.gpk_assemble(ctypes.byref(kd), ctypes.byref(lay), nat.ptr(hyp), hyp_stride,
+                                 nat.ptr(noise), noise_stride, nat.ptr(X), x_bstride,
+                                 nat.ptr(Xs), xs_bstride, nat.ptr(E), e_bstride,
+                                 nat.ptr(y), y_bstride, nat.ptr(self.W), s), "gpk_assemble")
+        nat.check(L.gpk_potrf_aug(ctypes.byref(lay), nat.ptr(self.W), nat.ptr(self.Winv),
+                                  nat.ptr(self.info), s), "gpk_potrf_aug")
+        nat.check(L.gpk_finalize(ctypes.byref(lay), nat.ptr(self.W), nat.ptr(self.info),
+                                 nat.ptr(self.out), nat.ptr(self.mu) if self.m else None,
+                                 nat.ptr(self.var) if self.m else None, s), "gpk_finalize")
+        self.kd = kd
+        self.done = True
+        return self
+
+    # -- read-out (device views, no host synchronisation) -----------------------------------
+    def w(self, b: int = 0) -> torch.Tensor:
+        lay = self.layout
+        return self.W[b * lay.w_batch_stride:(b + 1) * lay.w_batch_stride].view(lay.p, lay.ld)
+
+    def nlml(self) -> torch.Tensor:
+        return self.out.view(self.batch, 4)[:, 0]
+
+    def fit(self) -> torch.Tensor:
+        return self.out.view(self.batch, 4)[:, 1]
+
+    def logdet(self) -> torch.Tensor:
+        return self.out.view(self.batch, 4)[:, 2]
+
+    def cholesky(self, b: int = 0) -> torch.Tensor:
+        """L (lower, [n, n], p_dtype)."""
+        return torch.tril(self.w(b)[:self.n, :self.n])
+
+    def z(self, b: int = 0) -> torch.Tensor:
+        lay = self.layout
+        return self.w(b)[lay.y_row, :self.n]
+
+    def extra_rows(self, b: int = 0) -> torch.Tensor:
+        """Rows n_pad .. n_pad+m-1 restricted to the first n columns: V^T = Ks^T L^-T (or E L^-T)."""
+        lay = self.layout
+        return self.w(b)[lay.n_pad:lay.n_pad + self.m, :self.n]
+
+    def corner(self, b: int = 0) -> torch.Tensor:
+        """Symmetrised m x m Schur complement: Kss - V^T V (or -E K^-1 E^T)."""
+        lay = self.layout
+        c = self.w(b)[lay.n_pad:lay.n_pad + self.m, lay.n_pad:lay.n_pad + self.m]
+        lo = torch.tril(c)
+        return lo + torch.tril(c, -1).transpose(0, 1)
+
+    def posterior_mu(self, b: int = 0) -> torch.Tensor:
+        return self.mu[b * self.m:(b + 1) * self.m]
+
+    def posterior_var_diag(self, b: int = 0) -> torch.Tensor:
+        return self.var[b * self.m:(b + 1) * self.m]
+
+    def alpha(self, b: int = 0) -> torch.Tensor:
+        """alpha = L^-T z = (K + noise I)^-1 y via gpk_trsv (backward solve)."""
+        lay = self.layout
+        x = torch.zeros(self.batch * lay.n_pad, dtype=torch.float64, device=self.W.device)
+        xv = x.view(self.batch, lay.n_pad)
+        for bb in range(self.batch):
+            xv[bb, :self.n] = self.z(bb).to(torch.float64)
+        nat.check(self.L.gpk_trsv(ctypes.byref(lay), 1, nat.ptr(self.W), nat.ptr(self.Winv),
+                                  nat.ptr(x), nat.stream_handle(self.W.device)), "gpk_trsv")
+        return xv[b, :self.n]
+
+    def check_info(self):
+        """Raise CholeskyError if any batch member failed (synchronises)."""
+        info = self.info.cpu()
+        bad = torch.nonzero(info).flatten()
+        if bad.numel():
+            raise CholeskyError(int(info[bad[0]]))

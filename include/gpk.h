@@ -1,0 +1,181 @@
+/*
+ * gpk.h -- C ABI of libgpk.so, the MI355X (gfx950) exact-GP likelihood engine.
+ *
+ * This is the drop-in boundary underneath the Python mirror of gpbasics' plugin API.
+ * The reference has no native layer: every entry point below replaces a TensorFlow call
+ * site on the reference's hot path (citations are relative to
+ * Bernsai/GaussianProcessFundamentals main/gpbasics/):
+ *
+ *   gpk_kernel_matrix  <- Kernel.get_tf_tensor                 KernelBasics/Kernel.py:51-52
+ *                         (SE :277-294, PER :440-457, MAT32 :702-720, MAT52 :859-880 of
+ *                          KernelBasics/BaseKernels.py; ADD/MUL KernelBasics/Operators.py:207-225,
+ *                          :306-326; distances Auxiliary/Distances.py:4-12)
+ *   gpk_assemble       <- HolisticCovarianceMatrix.get_K / get_K_noised / get_K_s / get_K_ss
+ *                                                               Statistics/CovarianceMatrix.py:187-225, :277-286
+ *   gpk_potrf_aug      <- tf.linalg.cholesky + both tf.linalg.triangular_solve of get_L_K /
+ *                         get_L_alpha                           Statistics/CovarianceMatrix.py:247-265
+ *   gpk_finalize       <- LogLikelihood.get_metric (-LML)       Metrics/LogLikelihood.py:30-65,
+ *                         Metrics/Metrics.py:138-139, :152-154;
+ *                         posterior mu / var                    Statistics/Auxiliary.py:57-93
+ *   gpk_trsv           <- the backward triangular_solve of get_L_alpha
+ *                                                               Statistics/CovarianceMatrix.py:260-262
+ *   gpk_nlml           <- LogLikelihood.get_metric, composed of the three calls above
+ *
+ * Conventions
+ *  - Every device buffer is allocated and owned by the caller (PyTorch-ROCm); the library
+ *    never allocates or frees caller memory and never synchronises the stream.
+ *  - Points are row-major fp64: X[batch][n][d] with a caller-given batch stride (0 =
+ *    shared by every batch member), y[batch][n], hyperparameters hyp[batch][n_hyp] fp64.
+ *  - Return value: 0 on success, -i for an invalid i-th argument, > 0 for a HIP error
+ *    code.  A matrix that is not positive definite is NOT an error of the call: it is
+ *    reported through info_dev[b] (LAPACK convention: 1-based index of the first
+ *    non-positive pivot, 0 when the factorisation succeeded).
+ *  - gpk_last_error() returns a thread-local description of the last failure.
+ *  - `stream` is a hipStream_t passed as void* (0 = the null stream).
+ *
+ * Augmented layout: the engine factors one matrix per batch member
+ *
+ *      W = [ K + noise*I    .      .  ]   rows 0 .. n_pad-1   (padding rows: identity)
+ *          [ Ks^T          Kss     .  ]   rows n_pad .. n_pad+m-1
+ *          [ y^T            0      0  ]   row  y_row = n_pad+m
+ *
+ * over its first n_pad columns only.  Afterwards the first n_pad columns hold L, the test
+ * rows hold V^T = Ks^T L^-T, the y row holds z^T = (L^-1 y)^T and the trailing corner holds
+ * the Schur complement  [[Kss - V^T V, .], [-mu^T, -z^T z]]: posterior covariance,
+ * posterior mean and the data-fit term of the LML fall out of one factorisation.
+ */
+#ifndef GPK_H
+#define GPK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPK_ABI_VERSION 1
+
+/* arithmetic types of the factorisation */
+enum { GPK_F64 = 0, GPK_F32 = 1 };
+
+/* kernel-tree op codes: values follow KernelManifestation (KernelBasics/Kernel.py:23-37) */
+enum {
+  GPK_OP_PER = 104,
+  GPK_OP_SE = 105,
+  GPK_OP_MAT32 = 107,
+  GPK_OP_MAT52 = 108,
+  GPK_OP_ADD = 201, /* binary: pops two, pushes sum (left fold of an n-ary ADD) */
+  GPK_OP_MUL = 202  /* binary: pops two, pushes product                         */
+};
+
+/* per-node flags of a base-kernel node */
+enum {
+  GPK_NODE_SCALED = 1,     /* p_scaled_base_kernel: signal variance sg multiplies the kernel */
+  GPK_NODE_ARD = 2,        /* build extension: one length scale per input dimension          */
+  GPK_NODE_SE_EXPANDED = 4, /* SE distance by the reference's expanded norm (Distances.py:5-7) */
+  GPK_NODE_STANDARD = 8     /* MAT: Euclidean distance; PER: sum_d sin^2 per dimension (build
+                               option; equal to the reference's L1 forms when d == 1)          */
+};
+
+#define GPK_MAX_NODES 16
+#define GPK_MAX_DIM 16
+#define GPK_MAX_ARD 2
+#define GPK_MAX_HYP 64
+
+/* one postfix-program node */
+typedef struct {
+  int32_t op;         /* GPK_OP_*                                               */
+  int32_t hyp_offset; /* first hyperparameter of a base node inside hyp[b][:]   */
+  int32_t ard_slot;   /* 0..GPK_MAX_ARD-1 for GPK_NODE_ARD nodes, else -1       */
+  int32_t flags;      /* GPK_NODE_*                                             */
+} gpk_node;
+
+/* kernel tree flattened to postfix (children left to right, binary ADD/MUL after each
+ * child beyond the first), hyperparameters in the reference's DFS order */
+typedef struct {
+  int32_t n_nodes;
+  int32_t n_hyp;
+  int32_t dim;
+  int32_t n_ard;
+  gpk_node nodes[GPK_MAX_NODES];
+} gpk_kdesc;
+
+/* sizes of the augmented factorisation of one problem shape */
+typedef struct {
+  int32_t dtype;          /* GPK_F64 / GPK_F32                                   */
+  int32_t batch;          /* independent problems factored by every launch       */
+  int64_t n;              /* training points                                     */
+  int64_t m;              /* test points carried through the factorisation       */
+  int64_t d;              /* input dimensions                                    */
+  int64_t nb;             /* panel width (columns per factorisation step)        */
+  int64_t n_pad;          /* factored columns: n rounded up to nb                */
+  int64_t y_row;          /* row holding y (= n_pad + m)                         */
+  int64_t p;              /* rows and columns of W (multiple of nb)              */
+  int64_t ld;             /* leading dimension of W in elements                  */
+  int64_t w_batch_stride; /* elements between consecutive batch members of W     */
+  int64_t inv_batch_stride; /* elements between batch members of Winv            */
+  size_t w_bytes;         /* bytes of W for the whole batch                      */
+  size_t inv_bytes;       /* bytes of Winv (inverted diagonal blocks), whole batch */
+} gpk_layout;
+
+int gpk_abi_version(void);
+const char* gpk_last_error(void);
+
+/* fill *out for the given shape (no device work) */
+int gpk_plan(int dtype, int32_t batch, int64_t n, int64_t m, int64_t d, gpk_layout* out);
+
+/* Build W (see layout above) for every batch member.  hyp_dev[b*hyp_stride ...],
+ * noise_dev[b*noise_stride]; X/Xs/E/y batch strides in elements (0 = shared).
+ * The m extra rows are either kernel rows k(Xs_t, X_j) with the Kss corner (E == NULL), or the
+ * explicit dense rows E[b][t][j] (t < m, j < n) with a zero corner (Xs ignored): E = I gives
+ * L^-T in the extra rows and -K^-1 in the corner.  Xs and E may both be NULL when m == 0. */
+int gpk_assemble(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+                 int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+                 const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
+                 const double* E, int64_t e_bstride, const double* y, int64_t y_bstride,
+                 void* W, void* stream);
+
+/* Blocked right-looking Cholesky of the first n_pad columns of every W, all rows.
+ * Winv receives the inverted nb x nb diagonal blocks (needed by gpk_trsv).
+ * info_dev[batch] must be zeroed by the caller before the call. */
+int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, void* stream);
+
+/* Read the results out of a factored W.  out_dev[b*4 + {0,1,2,3}] =
+ * {nlml, fit = y^T alpha, logdet = 2 sum log L_ii, n}; nlml = +inf where info != 0.
+ * mu_dev[b*m + t] = posterior mean (may be NULL), var_dev[b*m + t] = posterior variance
+ * diagonal (may be NULL). */
+int gpk_finalize(const gpk_layout* lay, const void* W, const int32_t* info_dev,
+                 double* out_dev, double* mu_dev, double* var_dev, void* stream);
+
+/* assemble + potrf_aug + finalize with m = 0 */
+int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+             int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+             const double* X, int64_t x_bstride, const double* y, int64_t y_bstride,
+             void* W, void* Winv, int32_t* info_dev, double* out_dev, void* stream);
+
+/* Plain kernel matrix K[i*ldk + j] = k(X_i, Y_j) (+ diag_add where i == j) for i < n, j < m.
+ * uplo: 0 = full, 1 = lower triangle only.  dtype selects the stored element type. */
+int gpk_kernel_matrix(const gpk_kdesc* kd, const double* hyp_dev, int dtype, int uplo,
+                      const double* X, int64_t n, const double* Y, int64_t m, int32_t d,
+                      double diag_add, void* K, int64_t ldk, void* stream);
+
+/* Triangular solve with the factor held in W (first n_pad columns):
+ *   trans = 0: x <- L^-1 x      trans = 1: x <- L^-T x
+ * x is fp64 of length n_pad per batch member (batch stride n_pad; entries >= n must be 0). */
+int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, double* x,
+             void* stream);
+
+/* Per-kernel-class timing with HIP events recorded on the launch stream.
+ * class: 0 assemble, 1 diag, 2 trsm, 3 update, 4 finalize, 5 trsv */
+#define GPK_NUM_CLASSES 6
+int gpk_timing_enable(int on);
+/* synchronises the recorded events; returns totals since the last reset */
+int gpk_timing_read(double* ms_by_class, int64_t* launches_by_class, double* flops_by_class,
+                    double* bytes_by_class);
+int gpk_timing_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPK_H */

@@ -1,0 +1,321 @@
+"""CPU oracle: a numpy/SciPy fp64 restatement of the reference's exact-GP likelihood path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the checker or
+as the timed CPU baseline.  The product package (``gaussianprocessfundamentals_amd``)
+never imports it and has no CPU fallback.
+
+Parity status: **parity unpinned by the reference itself.**  The reference
+(Bernsai/GaussianProcessFundamentals, ``gpbasics`` 2.0.0) ships no tests, fixtures or
+golden vectors, and it cannot be imported here (TensorFlow is absent: an ordinary
+``ModuleNotFoundError``, not a permission denial).  This restatement is therefore pinned
+by closed-form known answers (``known_answers()`` below, exercised in
+``tests/test_oracle.py``) and it generates the committed golden vectors under
+``tests/golden/`` (script: ``tests/golden/make_golden.py``).
+
+Every function follows the reference op-for-op; citations are
+``path:line`` relative to ``/root/reference/main/gpbasics``.  TensorFlow's own rounding
+(Eigen LLT blocking, reduction order) cannot be reproduced and is covered by tolerance.
+
+Kernel trees are given as nested tuples, independent of the product package:
+  ("SE",    {"ard": False})      SquaredExponentialKernel   hyp [l, (sg)]
+  ("PER",   {})                  PeriodicKernel              hyp [l, p, (sg)]
+  ("MAT32", {"ard": False})      MaternKernel3_2             hyp [l, (sg)]
+  ("MAT52", {"ard": False})      MaternKernel5_2             hyp [l, (sg)]
+  ("ADD", [child, child, ...])   AdditionOperator
+  ("MUL", [child, child, ...])   MultiplicationOperator
+``standard=True`` (MAT/PER) selects the build's well-posed multi-dimensional form: Euclidean
+distance for the Matern kernels, a per-dimension sum of sin^2 for PER.  Both equal the
+reference form when D == 1; for D > 1 the reference's L1 forms are not positive definite
+(e.g. min eigenvalue -0.94 for the C3 inputs, -29 for C5's PER), so its Cholesky fails there.
+``ard=True`` is the build's ARD extension (the reference has only scalar length scales,
+SURVEY Q4): the length-scale hyperparameter is a vector of D values and the kernel equals
+the reference kernel with l = 1 evaluated on inputs divided elementwise by that vector.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Sequence, Tuple
+
+import numpy as np
+import scipy.linalg as sla
+
+LOG_2PI = math.log(2.0 * math.pi)
+
+
+# ---------------------------------------------------------------- distances (A/Distances.py)
+def euclidian_distance(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Expanded-norm L2 distance, unclamped: A/Distances.py:4-7.
+
+    sqrt(rowsum(a*a) - 2 a b^T + rowsum(b*b)^T); a negative argument gives NaN exactly as in
+    the reference."""
+    na = np.sum(a * a, axis=-1, keepdims=True)
+    nb = np.sum(b * b, axis=-1, keepdims=True)
+    with np.errstate(invalid="ignore"):
+        return np.sqrt((na - 2.0 * (a @ np.swapaxes(b, -1, -2))) + np.swapaxes(nb, -1, -2))
+
+
+def manhattan_distance(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """L1 distance via broadcast: A/Distances.py:10-12."""
+    return np.sum(np.abs(a[..., :, None, :] - b[..., None, :, :]), axis=-1)
+
+
+def squared_l2_direct(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Build's default SE distance: sum_d (a_d - b_d)^2 (identical to the reference where the
+    reference is finite, up to rounding; never NaN).  Not in the reference."""
+    diff = a[..., :, None, :] - b[..., None, :, :]
+    return np.sum(diff * diff, axis=-1)
+
+
+# ---------------------------------------------------------------- base kernels (K/BaseKernels.py)
+def n_hyp(tree, scaled: bool, dim: int) -> int:
+    """Hyperparameter count in DFS order: K/Operators.py:28-32 and the per-kernel
+    get_number_of_hyper_parameter (K/BaseKernels.py:308-314, :475-481, :734-740, :894-900)."""
+    op, arg = tree
+    if op in ("ADD", "MUL"):
+        return sum(n_hyp(c, scaled, dim) for c in arg)
+    base = 2 if op == "PER" else 1
+    return base + (1 if scaled else 0)
+
+
+def _scale_inputs(x, ls):
+    return x / np.asarray(ls, dtype=np.float64)
+
+
+def eval_base(op: str, opts: dict, hyp: Sequence, x: np.ndarray, x_: np.ndarray,
+              scaled: bool, se_expanded: bool) -> np.ndarray:
+    ard = bool(opts.get("ard", False))
+    if op == "SE":
+        # K/BaseKernels.py:277-294
+        if ard:
+            x, x_ = _scale_inputs(x, hyp[0]), _scale_inputs(x_, hyp[0])
+            l = 1.0
+        else:
+            l = float(hyp[0])
+        if se_expanded:
+            dist = euclidian_distance(x, x_)
+            sq = dist * dist                                   # tf.square(dist)
+        else:
+            sq = squared_l2_direct(x, x_)
+        r = np.exp(-0.5 * (sq / (l * l)))
+        if scaled:
+            r = float(hyp[1]) * r                              # :289-290
+        return r
+    if op in ("MAT52", "MAT32"):
+        # K/BaseKernels.py:859-880 (MAT52), :702-720 (MAT32); L1 distance
+        if ard:
+            x, x_ = _scale_inputs(x, hyp[0]), _scale_inputs(x_, hyp[0])
+            l = 1.0
+        else:
+            l = abs(float(hyp[0]))
+        if opts.get("standard", False):
+            # build option: Euclidean distance (the textbook Matern; PD in any D).  Equal to the
+            # reference's L1 form when D == 1.
+            dist = np.sqrt(squared_l2_direct(x, x_))
+        else:
+            dist = manhattan_distance(x, x_)
+        if op == "MAT52":
+            frac = (math.sqrt(5.0) * dist) / l
+            third = (5.0 * (dist * dist)) / (3.0 * (l * l))
+            r = ((1.0 + frac) + third) * np.exp(-frac)
+        else:
+            frac = (math.sqrt(3.0) * dist) / l
+            r = (1.0 + frac) * np.exp(-frac)
+        if scaled:
+            r = float(hyp[1]) * r
+        return r
+    if op == "PER":
+        # K/BaseKernels.py:440-457; L1 distance, hyp [l, p, (sg)]
+        if ard:
+            raise ValueError("PER has no ARD form")
+        l, p = float(hyp[0]), float(hyp[1])
+        if opts.get("standard", False):
+            # build option: per-dimension form exp(-2 sum_d sin^2(pi |x_d - y_d| / p) / l^2),
+            # a product of 1-D periodic kernels (PD in any D); equal to the reference when D == 1.
+            dd = np.abs(x[..., :, None, :] - x_[..., None, :, :])
+            sd = np.sin(math.pi * (dd / p))
+            sine = np.sum(sd * sd, axis=-1)
+        else:
+            dist = manhattan_distance(x, x_)
+            sine = np.sin(math.pi * (dist / p))
+            sine = sine * sine
+        r = np.exp((-2.0 * sine) / (l * l))
+        if scaled:
+            r = float(hyp[2]) * r
+        return r
+    raise ValueError("unsupported kernel op %r" % op)
+
+
+def kernel_matrix(tree, hyp: List, x: np.ndarray, x_: np.ndarray, scaled: bool = False,
+                  se_expanded: bool = False, row_chunk: int = 1024) -> np.ndarray:
+    """Kernel.get_tf_tensor (K/Kernel.py:51-52) for a tree; ADD/MUL fold left over children
+    with DFS hyperparameter slicing exactly as K/Operators.py:207-225 / :306-326.
+    Rows are evaluated in chunks (elementwise identical; bounds the [rows, m, D] temporaries)."""
+    if x.ndim == 2 and x.shape[0] > row_chunk:
+        return np.concatenate([_kernel_matrix(tree, hyp, x[i:i + row_chunk], x_, scaled, se_expanded)
+                               for i in range(0, x.shape[0], row_chunk)], axis=0)
+    return _kernel_matrix(tree, hyp, x, x_, scaled, se_expanded)
+
+
+def _kernel_matrix(tree, hyp, x, x_, scaled, se_expanded):
+    op, arg = tree
+    if op in ("ADD", "MUL"):
+        idx = 0
+        result = None
+        dim = x.shape[-1]
+        for child in arg:
+            k = n_hyp(child, scaled, dim)
+            m = _kernel_matrix(child, hyp[idx:idx + k], x, x_, scaled, se_expanded)
+            idx += k
+            if result is None:
+                result = m
+            else:
+                result = result + m if op == "ADD" else result * m
+        return result
+    return eval_base(op, arg, hyp, x, x_, scaled, se_expanded)
+
+
+# ---------------------------------------------------------------- covariance + likelihood
+def k_noised(tree, hyp, noise, x, scaled=False, se_expanded=False):
+    """HolisticCovarianceMatrix.get_K_noised: S/CovarianceMatrix.py:197-206."""
+    K = kernel_matrix(tree, hyp, x, x, scaled, se_expanded)
+    n = x.shape[-2]
+    return K + noise * np.eye(n)
+
+
+def cholesky_lower(A):
+    """tf.linalg.cholesky (S/CovarianceMatrix.py:250): lower factor; raises
+    np.linalg.LinAlgError when not positive definite (TF raises InvalidArgumentError)."""
+    return sla.cholesky(A, lower=True, check_finite=False)
+
+
+def l_alpha(L, y):
+    """get_L_alpha: alpha = L^T \\ (L \\ y)  (S/CovarianceMatrix.py:256-265)."""
+    z = sla.solve_triangular(L, y, lower=True, check_finite=False)
+    return sla.solve_triangular(L.T, z, lower=False, check_finite=False)
+
+
+def nlml_components(tree, hyp, noise, x, y, scaled=False, se_expanded=False):
+    """One LogLikelihood.get_metric evaluation, CHOLESKY_BASED strategy
+    (M/LogLikelihood.py:30-65, M/Metrics.py:138-139 and :152-154).
+
+    Returns dict(nlml, fit, logdet, n) with nlml = -LML (minimise convention,
+    M/Metrics.py:27), fit = y^T alpha, logdet = 2 sum log diag L."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1, 1)
+    A = k_noised(tree, hyp, noise, x, scaled, se_expanded)
+    L = cholesky_lower(A)
+    alpha = l_alpha(L, y)
+    fit = float((y.T @ alpha)[0, 0])                               # :39
+    logdet = float(2.0 * np.sum(np.log(np.diag(L))))               # M/Metrics.py:153-154
+    n = x.shape[-2]
+    ll = (-0.5 * fit + -0.5 * logdet) + (-0.5 * (n * LOG_2PI))     # :41-49
+    return {"nlml": -ll, "fit": fit, "logdet": logdet, "n": n, "L": L, "alpha": alpha}
+
+
+def nlml(tree, hyp, noise, x, y, scaled=False, se_expanded=False) -> float:
+    return nlml_components(tree, hyp, noise, x, y, scaled, se_expanded)["nlml"]
+
+
+def batch_nlml(tree, hyp, noise, xb, yb, scaled=False, se_expanded=False) -> float:
+    """BatchDataInput mode: the data-fit term is averaged over the
+    batch by p_batch_metric_aggregator=reduce_mean (M/LogLikelihood.py:62-63) while the
+    Cholesky log-determinant is a reduce_sum with no axis (M/Metrics.py:153-154), i.e.
+    summed over the whole batch before being broadcast into every member."""
+    fits, logdets = [], []
+    for b in range(xb.shape[0]):
+        c = nlml_components(tree, hyp, noise, xb[b], yb[b], scaled, se_expanded)
+        fits.append(c["fit"])
+        logdets.append(c["logdet"])
+    n = xb.shape[-2]
+    logdet_total = float(np.sum(logdets))
+    lls = [(-0.5 * f + -0.5 * logdet_total) + (-0.5 * (n * LOG_2PI)) for f in fits]
+    return -float(np.mean(lls))
+
+
+def posterior(tree, hyp, noise, x, y, xs, scaled=False, se_expanded=False):
+    """get_posterior_mu / get_posterior_var (S/Auxiliary.py:57-93) with the explicit
+    inverse of L used by get_L_inv_K (S/CovarianceMatrix.py:267-275); K_ss carries no noise
+    (S/CovarianceMatrix.py:218-225).  Returns (mu [M], full covariance [M, M])."""
+    y = np.asarray(y, dtype=np.float64).reshape(-1, 1)
+    A = k_noised(tree, hyp, noise, x, scaled, se_expanded)
+    L = cholesky_lower(A)
+    alpha = l_alpha(L, y)
+    Ks = kernel_matrix(tree, hyp, x, xs, scaled, se_expanded)             # [N, M]
+    mu = (Ks.T @ alpha).reshape(-1)                                         # :75-77
+    Linv = np.linalg.inv(L)                                                 # :270
+    v = Linv @ Ks                                                           # :60-62
+    Kss = kernel_matrix(tree, hyp, xs, xs, scaled, se_expanded)
+    var = Kss - v.T @ v                                                     # :86-88
+    return mu, var
+
+
+# ---------------------------------------------------------------- synthetic configs
+def make_inputs(cfg: str, n: int = None, seed: int = None) -> Tuple[np.ndarray, np.ndarray]:
+    """Synthetic data generators of SURVEY §8(d) (numpy default_rng(seed))."""
+    if cfg in ("C1", "C2", "C4", "metric"):
+        d = 1
+        seed = {"C1": 0, "C2": 1, "C4": 3, "metric": 5}[cfg] if seed is None else seed
+        n = {"C1": 256, "C2": 4096, "C4": 4096, "metric": 8192}[cfg] if n is None else n
+        rng = np.random.default_rng(seed)
+        x = np.sort(rng.uniform(0.0, 1.0, n)).reshape(n, d)
+        y = np.sin(4.0 * math.pi * x[:, 0]) + 0.1 * rng.standard_normal(n)
+        return x, y
+    if cfg == "C3":
+        n = 8192 if n is None else n
+        rng = np.random.default_rng(2 if seed is None else seed)
+        x = rng.uniform(0.0, 1.0, (n, 4))
+        y = np.sum(np.sin(2.0 * math.pi * x), axis=1) + 0.1 * rng.standard_normal(n)
+        return x, y
+    if cfg == "C5":
+        n = 16384 if n is None else n
+        rng = np.random.default_rng(4 if seed is None else seed)
+        x = rng.uniform(0.0, 1.0, (n, 8))
+        y = np.sum(np.sin(2.0 * math.pi * x), axis=1) + 0.1 * rng.standard_normal(n)
+        return x, y
+    raise ValueError(cfg)
+
+
+def known_answers() -> List[Tuple[str, float, float]]:
+    """Closed-form checks.  Returns (name, oracle value, exact value)."""
+    out = []
+    se = ("SE", {"ard": False})
+    # N=1: NLL = y^2/(2(1+s2)) + log(1+s2)/2 + log(2pi)/2
+    for y0, s2 in ((0.7, 0.01), (-1.3, 0.5)):
+        got = nlml(se, [0.3], s2, np.array([[0.2]]), np.array([y0]))
+        exp = 0.5 * y0 * y0 / (1 + s2) + 0.5 * math.log(1 + s2) + 0.5 * LOG_2PI
+        out.append(("N1_y%.1f" % y0, got, exp))
+    # N=2: K = [[1+s2, k],[k, 1+s2]], det = (1+s2)^2 - k^2, inverse closed form
+    x = np.array([[0.1], [0.35]])
+    yv = np.array([0.4, -0.9])
+    l, s2 = 0.2, 0.05
+    kk = math.exp(-0.5 * (0.25 ** 2) / (l * l))
+    a = 1 + s2
+    det = a * a - kk * kk
+    quad = (a * yv[0] ** 2 - 2 * kk * yv[0] * yv[1] + a * yv[1] ** 2) / det
+    exp = 0.5 * quad + 0.5 * math.log(det) + LOG_2PI
+    out.append(("N2", nlml(se, [l], s2, x, yv), exp))
+    # far separated points: K ~ I
+    xf = np.arange(8, dtype=np.float64).reshape(-1, 1) * 100.0
+    yf = np.linspace(-1, 1, 8)
+    s2 = 0.1
+    exp = 0.5 * float(np.sum(yf ** 2)) / (1 + s2) + 0.5 * 8 * math.log(1 + s2) + 0.5 * 8 * LOG_2PI
+    out.append(("far", nlml(se, [0.5], s2, xf, yf), exp))
+    # k(x, x) = 1 for SE / MAT / PER
+    xp = np.array([[0.3, -1.2]])
+    for tree, hyp in ((se, [0.7]), (("MAT52", {}), [0.7]), (("MAT32", {}), [0.7]), (("PER", {}), [0.7, 0.4])):
+        out.append(("diag_" + tree[0], float(kernel_matrix(tree, hyp, xp, xp)[0, 0]), 1.0))
+    # PER at d = p gives 1
+    out.append(("per_d_eq_p", float(kernel_matrix(("PER", {}), [0.9, 0.5], np.array([[0.0]]), np.array([[0.5]]))[0, 0]), 1.0))
+    # MAT52 at d = l/sqrt(5): (1 + 1 + 1/3) e^-1
+    l = 0.8
+    got = float(kernel_matrix(("MAT52", {}), [l], np.array([[0.0]]), np.array([[l / math.sqrt(5.0)]]))[0, 0])
+    out.append(("mat52_unit", got, (2.0 + 1.0 / 3.0) * math.exp(-1.0)))
+    # ARD identity: k_ARD(x, y; ls) == k_ref(x/ls, y/ls; l=1)
+    rng = np.random.default_rng(7)
+    xa, xb = rng.uniform(size=(5, 3)), rng.uniform(size=(4, 3))
+    ls = [0.3, 0.6, 1.1]
+    for name in ("SE", "MAT52", "MAT32"):
+        k1 = kernel_matrix((name, {"ard": True}), [ls], xa, xb)
+        k2 = kernel_matrix((name, {"ard": False}), [1.0], xa / ls, xb / ls)
+        out.append(("ard_" + name, float(np.max(np.abs(k1 - k2))), 0.0))
+    return out

@@ -1,0 +1,39 @@
+"""Shared test helpers: build drop-in objects and the matching oracle tree."""
+import os
+
+import numpy as np
+import torch
+
+import gaussianprocessfundamentals_amd.global_parameters as gp
+from gaussianprocessfundamentals_amd.KernelBasics import BaseKernels as bk
+from gaussianprocessfundamentals_amd.KernelBasics import Operators as ops
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+_BASE = {"SE": bk.SquaredExponentialKernel, "PER": bk.PeriodicKernel,
+         "MAT32": bk.MaternKernel3_2, "MAT52": bk.MaternKernel5_2}
+
+
+def make_kernel(tree, dim):
+    """Product kernel object for an oracle-style tree."""
+    op, arg = tree
+    if op == "ADD":
+        return ops.AdditionOperator(dim, [make_kernel(c, dim) for c in arg])
+    if op == "MUL":
+        return ops.MultiplicationOperator(dim, [make_kernel(c, dim) for c in arg])
+    return _BASE[op](dim, ard=bool(arg.get("ard", False)), standard=bool(arg.get("standard", False)))
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"))
+
+
+def hyp_list(values):
+    """Reference-style hyperparameter list of fp64 tensors (vectors stay vectors)."""
+    return [torch.tensor(v, dtype=torch.float64) for v in values]
+
+
+def set_flags(scaled=False, expanded=False, dtype=torch.float64):
+    gp.p_scaled_base_kernel = scaled
+    gp.p_se_expanded_norm = expanded
+    gp.p_dtype = dtype

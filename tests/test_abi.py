@@ -1,0 +1,71 @@
+"""The C-ABI library loads and exports every function include/gpk.h declares (no GPU needed);
+gpk_plan (host-only) sizes the augmented layout."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from gaussianprocessfundamentals_amd import _build, _native
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "gpk.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gpk_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    _build.build()
+    return _native.load_library()
+
+
+def test_every_declared_symbol_is_exported(lib):
+    decl = declared_functions()
+    assert len(decl) >= 10
+    missing = [f for f in decl if not hasattr(lib, f)]
+    assert not missing, missing
+    assert sorted(_native.EXPORTS) == decl
+
+
+def test_abi_version(lib):
+    assert lib.gpk_abi_version() == _native.GPK_ABI_VERSION
+
+
+@pytest.mark.parametrize("n,m,batch", [(1, 0, 1), (128, 0, 1), (129, 0, 2), (8192, 0, 1), (4096, 512, 1), (300, 77, 3)])
+def test_plan_layout(lib, n, m, batch):
+    lay = _native.plan(_native.GPK_F64, batch, n, m, 2)
+    nb = lay.nb
+    assert lay.n_pad % nb == 0 and lay.n_pad >= n and lay.n_pad - n < nb
+    assert lay.y_row == lay.n_pad + m
+    assert lay.p % nb == 0 and lay.p > lay.y_row
+    assert lay.ld >= lay.p
+    assert lay.w_bytes == batch * lay.p * lay.ld * 8
+    assert lay.inv_bytes == batch * (lay.n_pad // nb) * nb * nb * 8
+
+
+def test_plan_rejects_bad_arguments(lib):
+    lay = _native.GpkLayout()
+    assert lib.gpk_plan(7, 1, 10, 0, 1, ctypes.byref(lay)) < 0
+    assert lib.gpk_plan(0, 0, 10, 0, 1, ctypes.byref(lay)) < 0
+    assert lib.gpk_plan(0, 1, 0, 0, 1, ctypes.byref(lay)) < 0
+    assert lib.gpk_plan(0, 1, 10, 0, 17, ctypes.byref(lay)) < 0
+    assert b"invalid argument" in lib.gpk_last_error()
+
+
+def test_struct_sizes_match_header(lib):
+    # gpk_node: 4 x int32; gpk_kdesc: 4 x int32 + 16 nodes; gpk_layout: 2 x int32 + 10 x int64 + 2 size_t
+    assert ctypes.sizeof(_native.GpkNode) == 16
+    assert ctypes.sizeof(_native.GpkKdesc) == 16 + 16 * 16
+    assert ctypes.sizeof(_native.GpkLayout) == 8 + 10 * 8 + 2 * 8
+
+
+def test_product_fails_loudly_without_gpu(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_native.NativeUnavailable):
+        _native.lib()

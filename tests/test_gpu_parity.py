@@ -1,0 +1,316 @@
+"""HIP path vs the CPU oracle and the golden vectors (needs the MI355X).
+
+Tolerances (fp64 unless stated):
+  kernel matrices       |dK| <= 1e-13 + 1e-12 |K|          (transcendental ulp differences)
+  NLL                   rel <= 1e-9 (C2-C5, noise >= 1e-2);  rel <= 1e-6 for C1 (noise 1e-8,
+                        cond(K) ~ 1e10)
+  posterior mu / var    max-abs <= 1e-8 (C2)
+  fp32 engine (C3)      rel <= 1e-3 vs the fp64 oracle; measured value printed
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gp_oracle as o
+from tests.helpers import golden, hyp_list, make_kernel, set_flags
+
+import gaussianprocessfundamentals_amd.global_parameters as gp
+from gaussianprocessfundamentals_amd import engine
+from gaussianprocessfundamentals_amd.DataHandling.DataInput import BatchDataInput, DataInput
+from gaussianprocessfundamentals_amd.Metrics.Auxiliary import get_metric_by_type
+from gaussianprocessfundamentals_amd.Metrics.Metrics import MetricType
+from gaussianprocessfundamentals_amd.MeanFunctionBasics.BaseMeanFunctions import ZeroMeanFunction
+from gaussianprocessfundamentals_amd.Statistics.GaussianProcess import GaussianProcess
+from gaussianprocessfundamentals_amd.sweep import HyperparameterSweep, native_batched_evaluator
+
+pytestmark = pytest.mark.gpu
+
+SE = ("SE", {"ard": False})
+
+
+def build_gp(tree, x, y, xs=None, ys=None):
+    d = x.shape[-1]
+    k = make_kernel(tree, d)
+    if x.ndim == 3:
+        di = BatchDataInput(x, y[..., None], xs, ys, test_ratio=0)
+    elif xs is None:
+        di = DataInput(x, y.reshape(-1, 1), x, y.reshape(-1, 1))
+    else:
+        di = DataInput(x, y.reshape(-1, 1), xs, (ys if ys is not None else np.zeros(len(xs))).reshape(-1, 1))
+    di.set_mean_function(ZeroMeanFunction(d))
+    g = GaussianProcess(k, ZeroMeanFunction(d))
+    g.set_data_input(di)
+    return g
+
+
+def gpu_nlml(tree, hyp, noise, x, y):
+    g = build_gp(tree, x, y)
+    m = get_metric_by_type(MetricType.LL, g)
+    return float(m.get_metric_checked(hyp_list(hyp), torch.tensor(noise, dtype=torch.float64)))
+
+
+def rel(a, b):
+    return abs(a - b) / max(abs(b), 1e-300)
+
+
+# ------------------------------------------------------------------------------ kernel matrices
+KERNEL_CASES = [
+    (SE, [0.3], 1),
+    (("PER", {}), [0.7, 0.45], 1),
+    (("MAT32", {}), [0.4], 2),
+    (("MAT52", {}), [0.35], 3),
+    (("SE", {"ard": True}), [[0.3, 0.7, 1.2]], 3),
+    (("MAT52", {"ard": True}), [[0.25, 0.5, 0.75, 1.0]], 4),
+    (("ADD", [SE, ("PER", {})]), [0.3, 0.8, 0.5], 1),
+    (("MUL", [("MAT32", {}), ("ADD", [SE, ("MAT52", {})])]), [0.5, 0.3, 0.9], 2),
+    (("MAT52", {"ard": True, "standard": True}), [[0.25, 0.5, 0.75, 1.0]], 4),
+    (("MAT32", {"standard": True}), [0.4], 3),
+    (("ADD", [("SE", {"ard": True}), ("PER", {"standard": True})]), [[0.4, 0.6, 0.8], 1.0, 0.5], 3),
+]
+
+
+@pytest.mark.parametrize("tree,hyp,d", KERNEL_CASES)
+@pytest.mark.parametrize("scaled", [False, True])
+def test_kernel_matrix_matches_oracle(tree, hyp, d, scaled):
+    set_flags(scaled=scaled)
+    rng = np.random.default_rng(3)
+    x, xs = rng.uniform(-1, 1, (130, d)), rng.uniform(-1, 1, (77, d))
+    if scaled:  # add one sg per base kernel, after its own hyperparameters
+        hyp = _with_sg(tree, hyp)
+    k = make_kernel(tree, d)
+    got = k.get_tf_tensor(hyp_list(hyp), x, xs).cpu().numpy()
+    exp = o.kernel_matrix(tree, hyp, x, xs, scaled=scaled)
+    assert got.shape == (130, 77)
+    np.testing.assert_allclose(got, exp, rtol=1e-12, atol=1e-13)
+
+
+def _with_sg(tree, hyp):
+    out, idx = [], 0
+
+    def walk(t):
+        nonlocal idx
+        op, arg = t
+        if op in ("ADD", "MUL"):
+            for c in arg:
+                walk(c)
+            return
+        cnt = 2 if op == "PER" else 1
+        out.extend(hyp[idx:idx + cnt])
+        out.append(0.5 + 0.25 * len(out))
+        idx += cnt
+    walk(tree)
+    return out
+
+
+def test_kernel_matrix_se_expanded_norm_quirk():
+    """p_se_expanded_norm reproduces Auxiliary/Distances.py:4-7 including its NaNs."""
+    set_flags(expanded=True)
+    rng = np.random.default_rng(5)
+    x = rng.uniform(0, 1, (200, 8))
+    k = make_kernel(SE, 8)
+    got = k.get_tf_tensor(hyp_list([0.7]), x, x).cpu().numpy()
+    exp = o.kernel_matrix(SE, [0.7], x, x, se_expanded=True)
+    # Which near-zero arguments round negative depends on the summation order (TensorFlow,
+    # numpy and the device all differ), so only the pattern's location is pinned: NaNs appear
+    # on both sides, and only where the true squared distance is at rounding level.
+    true_sq = np.sum((x[:, None, :] - x[None, :, :]) ** 2, axis=-1)
+    assert np.isnan(got).any() and np.isnan(exp).any()
+    assert np.all(true_sq[np.isnan(got)] < 1e-12) and np.all(true_sq[np.isnan(exp)] < 1e-12)
+    fin = np.isfinite(exp) & np.isfinite(got)
+    np.testing.assert_allclose(got[fin], exp[fin], rtol=1e-10, atol=1e-7)
+    set_flags(expanded=False)
+    direct = k.get_tf_tensor(hyp_list([0.7]), x, x).cpu().numpy()
+    assert np.all(np.isfinite(direct))
+    np.testing.assert_allclose(np.diag(direct), 1.0, rtol=0, atol=0)
+
+
+def test_kernel_matrix_fp32_output():
+    rng = np.random.default_rng(4)
+    x = rng.uniform(0, 1, (100, 2))
+    K = engine.kernel_matrix(make_kernel(("MAT52", {}), 2), hyp_list([0.3]), x, x, out_dtype=torch.float32)
+    assert K.dtype == torch.float32
+    np.testing.assert_allclose(K.cpu().numpy(), o.kernel_matrix(("MAT52", {}), [0.3], x, x), rtol=1e-6, atol=1e-7)
+
+
+# ------------------------------------------------------------------------------ likelihood
+@pytest.mark.parametrize("n", [1, 2, 5, 127, 128, 129, 300, 1000])
+def test_nlml_sizes_match_oracle(n):
+    x, y = o.make_inputs("C1", n=n, seed=n)
+    got = gpu_nlml(SE, [0.1], 1e-2, x, y)
+    exp = o.nlml(SE, [0.1], 1e-2, x, y)
+    assert rel(got, exp) < 1e-10, (got, exp)
+
+
+def test_known_answers_on_gpu():
+    for y0, s2 in ((0.7, 0.01), (-1.3, 0.5)):
+        got = gpu_nlml(SE, [0.3], s2, np.array([[0.2]]), np.array([y0]))
+        exp = 0.5 * y0 * y0 / (1 + s2) + 0.5 * math.log(1 + s2) + 0.5 * math.log(2 * math.pi)
+        assert rel(got, exp) < 1e-14
+    xf = np.arange(8, dtype=np.float64).reshape(-1, 1) * 100.0
+    yf = np.linspace(-1, 1, 8)
+    exp = 0.5 * float(np.sum(yf ** 2)) / 1.1 + 4 * math.log(1.1) + 4 * math.log(2 * math.pi)
+    assert rel(gpu_nlml(SE, [0.5], 0.1, xf, yf), exp) < 1e-13
+
+
+def test_golden_c1_n256_jitter():
+    g = golden("c1_se_n256")
+    got = gpu_nlml(SE, [0.1], 1e-8, g["x"], g["y"])
+    assert rel(got, float(g["nlml"])) < 1e-6, (got, float(g["nlml"]))
+
+
+def test_golden_c1_factor_and_alpha():
+    """At the reference's default jitter (1e-8, cond ~1e10) two correct Cholesky codes agree
+    only to ~cond * eps in L; the meaningful checks are the backward error of L and the
+    residual of alpha.  At noise 1e-2 L itself is compared elementwise."""
+    g = golden("c1_se_n256")
+    x, y = g["x"], g["y"]
+    gpr = build_gp(SE, x, y)
+    cm = gpr.covariance_matrix
+    L = cm.get_L_K(hyp_list([0.1]), torch.tensor(1e-8, dtype=torch.float64)).cpu().numpy()
+    K = o.k_noised(SE, [0.1], 1e-8, x)
+    assert np.max(np.abs(L @ L.T - K)) < 1e-13
+    assert np.max(np.abs(L - g["L"])) < 1e-5
+    a = cm.get_L_alpha(hyp_list([0.1]), torch.tensor(1e-8, dtype=torch.float64)).cpu().numpy().reshape(-1)
+    assert np.max(np.abs(L @ (L.T @ a) - y)) < 1e-6
+    cm.reset()
+    L2 = cm.get_L_K(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64)).cpu().numpy()
+    np.testing.assert_allclose(L2, o.cholesky_lower(o.k_noised(SE, [0.1], 1e-2, x)), rtol=0, atol=1e-13)
+
+
+def test_golden_c2_n4096_nlml_and_posterior():
+    g = golden("c2_se_n4096")
+    gpr = build_gp(SE, g["x"], g["y"], g["xs"])
+    m = get_metric_by_type(MetricType.LL, gpr)
+    got = float(m.get_metric_checked(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64)))
+    assert rel(got, float(g["nlml"])) < 1e-9
+    mu = gpr.aux.get_posterior_mu(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64)).cpu().numpy()
+    assert np.max(np.abs(mu - g["mu"])) < 1e-8
+    vd = gpr.aux.get_posterior_var_diag(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64)).cpu().numpy()
+    assert np.max(np.abs(vd - g["var_diag"])) < 1e-8
+    var = gpr.aux.get_posterior_var(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64)).cpu().numpy()
+    assert np.max(np.abs(var[:64, :64] - g["var_block"])) < 1e-8
+    full, mean_mu, post = gpr.predict(hyp_list([0.1]), noise=torch.tensor(1e-2, dtype=torch.float64))
+    assert np.max(np.abs(post.cpu().numpy() - g["mu"])) < 1e-8
+    assert float(torch.max(torch.abs(mean_mu))) == 0.0
+
+
+def test_golden_c3_mat52_ard_fp64_and_fp32():
+    g = golden("c3_mat52ard_n8192")
+    x, y = o.make_inputs("C3")
+    from tests.golden.make_golden import digest
+    assert digest(x) == str(g["x_sha256"]) and digest(y) == str(g["y_sha256"])
+    tree = ("MAT52", {"ard": True, "standard": True})
+    ls = list(g["ls"])
+    got64 = gpu_nlml(tree, [ls], 0.1, x, y)
+    assert rel(got64, float(g["nlml"])) < 1e-9
+    set_flags(dtype=torch.float32)
+    got32 = gpu_nlml(tree, [ls], 0.1, x, y)
+    print("C3 fp32 engine: nlml=%.6f fp64 oracle=%.6f rel=%.3e" % (got32, float(g["nlml"]), rel(got32, float(g["nlml"]))))
+    assert rel(got32, float(g["nlml"])) < 1e-3
+
+
+def test_golden_c4_sweep_argmin():
+    g = golden("c4_sweep128_n4096")
+    set_flags(scaled=True)
+    k = make_kernel(SE, 1)
+    ev = native_batched_evaluator(k, g["x"], g["y"], 1e-2, max_batch=64)
+    nlml, info, best = HyperparameterSweep(ev).run(torch.tensor(g["cands"]))
+    nl = nlml.cpu().numpy()
+    ok = np.isfinite(g["nlml"])
+    assert np.all(info.cpu().numpy()[ok] == 0)
+    assert np.max(np.abs(nl[ok] - g["nlml"][ok]) / np.abs(g["nlml"][ok])) < 1e-9
+    assert best == int(np.argmin(np.where(ok, g["nlml"], np.inf)))
+
+
+def test_golden_c5_sum_ard_n16384():
+    g = golden("c5_seard_per_n16384")
+    x, y = o.make_inputs("C5")
+    tree = ("ADD", [("SE", {"ard": True}), ("PER", {"standard": True})])
+    got = gpu_nlml(tree, [list(g["ls"]), float(g["per"][0]), float(g["per"][1])], 1e-2, x, y)
+    assert rel(got, float(g["nlml"])) < 1e-8
+
+
+def test_small_trees_scaled_expanded_batch():
+    g = golden("small_trees")
+    tree = ("MUL", [("ADD", [SE, ("MAT32", {})]), ("PER", {})])
+    set_flags(scaled=True)
+    assert rel(gpu_nlml(tree, list(g["hyp"]), 1e-3, g["x"], g["y"]), float(g["nlml_scaled_tree"])) < 1e-9
+    set_flags(scaled=False, expanded=True)
+    assert rel(gpu_nlml(SE, [0.3], 1e-3, g["x"], g["y"]), float(g["nlml_se_expanded"])) < 1e-9
+    set_flags(expanded=False)
+    gb = build_gp(SE, g["xb"], g["yb"])
+    m = get_metric_by_type(MetricType.LL, gb)
+    got = float(m.get_metric(hyp_list([0.2]), torch.tensor(1e-2, dtype=torch.float64)))
+    assert rel(got, float(g["nlml_batch"])) < 1e-10
+
+
+def test_reference_l1_forms_fail_like_the_reference_for_d_gt_1():
+    """The reference's L1 Matern is indefinite in D=4: both the oracle and the device report a
+    failed Cholesky (info != 0) instead of a number."""
+    x, y = o.make_inputs("C3", n=2000)
+    tree = ("MAT52", {"ard": True})
+    with pytest.raises(np.linalg.LinAlgError):
+        o.nlml(tree, [[0.25, 0.5, 0.75, 1.0]], 0.1, x, y)
+    from gaussianprocessfundamentals_amd.engine import CholeskyError
+    with pytest.raises(CholeskyError):
+        gpu_nlml(tree, [[0.25, 0.5, 0.75, 1.0]], 0.1, x, y)
+
+
+def test_metric_matches_oracle_at_metric_size():
+    """The bench workload (SE, D=1, N=8192, fp64) against the oracle, full size."""
+    x, y = o.make_inputs("metric")
+    got = gpu_nlml(SE, [0.1], 1e-2, x, y)
+    exp = o.nlml(SE, [0.1], 1e-2, x, y)
+    assert rel(got, exp) < 1e-9
+
+
+# ------------------------------------------------------------------------------ other plugin surface
+def test_inverses_and_noised_k():
+    x, y = o.make_inputs("C1", n=200, seed=9)
+    gpr = build_gp(SE, x, y)
+    cm = gpr.covariance_matrix
+    h, nz = hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64)
+    Kn = o.k_noised(SE, [0.1], 1e-2, x)
+    np.testing.assert_allclose(cm.get_K_noised(h, nz).cpu().numpy(), Kn, rtol=1e-12, atol=1e-13)
+    L = np.linalg.cholesky(Kn)
+    np.testing.assert_allclose(cm.get_L_inv_K(h, nz).cpu().numpy(), np.linalg.inv(L), rtol=1e-8, atol=1e-8)
+    np.testing.assert_allclose(cm.get_K_inv(h, nz).cpu().numpy(), np.linalg.inv(Kn), rtol=1e-7, atol=1e-7)
+
+
+def test_not_positive_definite_reports_info():
+    x = np.linspace(0, 1, 200).reshape(-1, 1)
+    y = np.sin(x[:, 0])
+    gpr = build_gp(SE, x, y)
+    m = get_metric_by_type(MetricType.LL, gpr)
+    from gaussianprocessfundamentals_amd.engine import CholeskyError
+    with pytest.raises(CholeskyError):
+        m.get_metric_checked(hyp_list([0.5]), torch.tensor(-1.0, dtype=torch.float64))
+    # batched: a failing candidate gets +inf and nonzero info; the others are unaffected
+    k = make_kernel(SE, 1)
+    ev = native_batched_evaluator(k, x, y, 1e-2)
+    out = ev(torch.tensor([[0.1], [float("nan")], [0.2]], dtype=torch.float64)).cpu().numpy()
+    assert out[1, 1] != 0 and math.isinf(out[1, 0])
+    assert out[0, 1] == 0 and out[2, 1] == 0
+    assert rel(out[0, 0], o.nlml(SE, [0.1], 1e-2, x, y)) < 1e-10
+
+
+def test_trsv_forward_backward():
+    x, y = o.make_inputs("C1", n=333, seed=2)
+    gpr = build_gp(SE, x, y)
+    f = gpr.covariance_matrix.factorization(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64))
+    L = np.linalg.cholesky(o.k_noised(SE, [0.1], 1e-2, x))
+    z = np.linalg.solve(L, y)
+    np.testing.assert_allclose(f.z(0).cpu().numpy(), z, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(f.alpha(0).cpu().numpy(), np.linalg.solve(L.T, z), rtol=1e-8, atol=1e-8)
+
+
+def test_sweep_matches_single_evaluations():
+    x, y = o.make_inputs("C1", n=500, seed=4)
+    k = make_kernel(SE, 1)
+    cands = torch.tensor([[v] for v in np.geomspace(0.02, 0.5, 10)], dtype=torch.float64)
+    nlml, info, best = HyperparameterSweep(native_batched_evaluator(k, x, y, 1e-2, max_batch=4)).run(cands)
+    exp = [o.nlml(SE, [float(c)], 1e-2, x, y) for c in cands[:, 0]]
+    assert np.max(np.abs(nlml.cpu().numpy() - exp) / np.abs(exp)) < 1e-10
+    assert best == int(np.argmin(exp))

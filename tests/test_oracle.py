@@ -1,0 +1,72 @@
+"""The CPU oracle against closed-form answers and its own committed golden vectors."""
+import numpy as np
+import pytest
+
+from oracle import gp_oracle as o
+from tests.helpers import golden
+
+SE = ("SE", {"ard": False})
+
+
+@pytest.mark.parametrize("name,got,exp", o.known_answers())
+def test_known_answer(name, got, exp):
+    assert abs(got - exp) <= 1e-12 * max(1.0, abs(exp)), name
+
+
+def test_expanded_norm_exact_on_1d_diagonal_and_nan_in_8d():
+    x = np.random.default_rng(0).uniform(0, 1, (500, 1))
+    d = o.euclidian_distance(x, x)
+    assert np.all(np.diag(d) == 0.0)
+    x8 = np.random.default_rng(1).uniform(0, 1, (500, 8))
+    assert np.isnan(np.diag(o.euclidian_distance(x8, x8))).any()
+
+
+def test_batch_quirk_logdet_summed_fit_averaged():
+    rng = np.random.default_rng(2)
+    xb = rng.uniform(0, 1, (3, 20, 1))
+    yb = rng.standard_normal((3, 20))
+    comps = [o.nlml_components(SE, [0.3], 0.1, xb[b], yb[b]) for b in range(3)]
+    ld = sum(c["logdet"] for c in comps)
+    exp = -np.mean([-0.5 * c["fit"] - 0.5 * ld - 10 * o.LOG_2PI for c in comps])
+    assert abs(o.batch_nlml(SE, [0.3], 0.1, xb, yb) - exp) < 1e-10
+
+
+def test_l1_forms_are_indefinite_beyond_1d():
+    x, y = o.make_inputs("C3", n=600)
+    K = o.kernel_matrix(("MAT52", {"ard": True}), [[0.25, 0.5, 0.75, 1.0]], x, x)
+    assert np.linalg.eigvalsh(K)[0] < -0.1
+    Ks = o.kernel_matrix(("MAT52", {"ard": True, "standard": True}), [[0.25, 0.5, 0.75, 1.0]], x, x)
+    assert np.linalg.eigvalsh(Ks)[0] > -1e-10
+    x1 = x[:, :1]
+    for op in ("MAT52", "MAT32", "PER"):
+        hyp = [0.3, 0.4] if op == "PER" else [0.3]
+        a = o.kernel_matrix((op, {}), hyp, x1, x1)
+        b = o.kernel_matrix((op, {"standard": True}), hyp, x1, x1)
+        np.testing.assert_allclose(a, b, rtol=1e-14, atol=1e-15)
+
+
+def test_golden_c1_recomputes():
+    g = golden("c1_se_n256")
+    c = o.nlml_components(SE, [0.1], 1e-8, g["x"], g["y"])
+    assert abs(c["nlml"] - float(g["nlml"])) <= 1e-9 * abs(float(g["nlml"]))
+    np.testing.assert_allclose(c["L"], g["L"], rtol=0, atol=1e-12)
+
+
+def test_golden_small_trees_recompute():
+    g = golden("small_trees")
+    tree = ("MUL", [("ADD", [SE, ("MAT32", {})]), ("PER", {})])
+    got = o.nlml(tree, list(g["hyp"]), 1e-3, g["x"], g["y"], scaled=True)
+    assert abs(got - float(g["nlml_scaled_tree"])) <= 1e-10 * abs(got)
+    assert abs(o.batch_nlml(SE, [0.2], 1e-2, g["xb"], g["yb"]) - float(g["nlml_batch"])) < 1e-9
+
+
+def test_golden_inputs_are_reproducible():
+    """The large configs regenerate their inputs from a seed: pin the generator."""
+    from tests.golden.make_golden import digest
+    for name, cfg in (("c3_mat52ard_n8192", "C3"), ("c5_seard_per_n16384", "C5")):
+        g = golden(name)
+        x, y = o.make_inputs(cfg)
+        assert digest(x) == str(g["x_sha256"]) and digest(y) == str(g["y_sha256"])
+    g = golden("c2_se_n4096")
+    x, y = o.make_inputs("C2")
+    np.testing.assert_array_equal(x, g["x"])
