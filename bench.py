@@ -28,6 +28,7 @@ sys.path.insert(0, HERE)
 
 PEAK = {"f64": 78.6, "f32": 157.3}   # TFLOP/s dense MFMA (AMD MI355X spec; microarch guide for f32)
 HBM_PEAK = 8000.0                      # GB/s spec
+DEFAULT_BATCH = 8                      # candidates per rank per step on the metric config
 
 CONFIGS = {
     # name: (kernel, d, n, noise, dtype, hyp)
@@ -45,6 +46,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     ap.add_argument("--n", type=int, default=None, help="override N")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="hyperparameter candidates factorised together per rank per step "
+                         "(default: %d for the metric config, 1 otherwise)" % DEFAULT_BATCH)
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events")
@@ -126,17 +130,24 @@ def main():
     flat_h = []
     for h in hyp:
         flat_h.extend(h if isinstance(h, list) else [h])
-    # weak scaling: every rank evaluates its own candidate (length scale offset by rank)
-    flat_h[0] = flat_h[0] * (1.0 + 0.01 * rank) if not isinstance(hyp[0], list) else flat_h[0]
-    H = torch.tensor(flat_h, dtype=torch.float64, device=dev)
+    batch = args.batch or (DEFAULT_BATCH if args.config == "metric" else 1)
+    # weak scaling: every rank evaluates its own `batch` candidates (a sweep over the first
+    # hyperparameter: candidate c of rank r scales it by 1 + 0.01 (r * batch + c))
+    rows = []
+    for c in range(batch):
+        h = list(flat_h)
+        if not isinstance(hyp[0], list):
+            h[0] = h[0] * (1.0 + 0.01 * (rank * batch + c))
+        rows.append(h)
+    H = torch.tensor(rows, dtype=torch.float64, device=dev).contiguous()
     NZ = torch.tensor([noise], dtype=torch.float64, device=dev)
-    fact = engine.AugmentedFactorization(n, d, 0, 1, dt)
-    gathered = torch.empty(2 * world, dtype=torch.float64, device=dev) if world > 1 else None
+    fact = engine.AugmentedFactorization(n, d, 0, batch, dt)
+    gathered = torch.empty(2 * batch * world, dtype=torch.float64, device=dev) if world > 1 else None
 
     def step():
-        fact.run(kd, H, 0, NZ, 0, X, 0, Y, 0)
+        fact.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
         if world > 1:
-            mine = torch.stack([fact.nlml()[0], fact.info[0].to(torch.float64)])
+            mine = torch.cat([fact.nlml(), fact.info.to(torch.float64)])
             dist.all_gather_into_tensor(gathered, mine)
 
     for _ in range(args.warmup):
@@ -163,10 +174,10 @@ def main():
         el = float(tt.item())
     timing = nat.timing_read() if use_events else None
     nl = float(fact.nlml()[0].item())
-    info = int(fact.info[0].item())
+    info = int(fact.info.abs().max().item())
 
     if rank == 0:
-        evals = args.steps * world
+        evals = args.steps * world * batch
         value = evals / el
         ms = el / args.steps * 1000.0
         lay = fact.layout
@@ -200,8 +211,9 @@ def main():
             "vs_baseline": None,
             "dtype": dtn,
             "data": "synthetic (SURVEY §8d generator, numpy default_rng seed 5), resident in HBM",
-            "config": {"workload": "%s GP -LML, kernel=%s, D=%d, N=%d, noise=%g; one evaluation per rank per step"
-                                   % (args.config, kname, d, n, noise),
+            "config": {"workload": "%s GP -LML, kernel=%s, D=%d, N=%d, noise=%g; %d candidate evaluations per rank per step (batched factorisation)"
+                                   % (args.config, kname, d, n, noise, batch),
+                       "candidates_per_rank_step": batch,
                        "n": n, "d": d, "kernel": kname, "panel": int(lay.nb), "parallelism": "dp%d (independent candidates)" % world},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -1,6 +1,7 @@
 // extern "C" entry points of libgpk.so (declared in include/gpk.h).
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -101,6 +102,24 @@ bool valid_kdesc(const gpk_kdesc* kd, int64_t d) {
 }
 
 size_t elem_size(int dtype) { return dtype == GPK_F64 ? 8 : 4; }
+
+// Launch-shape thresholds (environment overrides for tuning runs).
+struct Tune {
+  int64_t upd_t128_min;   // 128 x 128 update tiles when at least this many (else 64 x 64)
+  int64_t trsm_t128_min;  // 128-row panel-solve tiles when at least this many (else 64)
+  int64_t diag_dbg;       // timing-only ablation flags of the diagonal kernel (never set in production)
+};
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? (int64_t)atoll(v) : dflt;
+}
+
+const Tune& tune() {
+  static const Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
+                         env_i64("GPK_DIAG_DEBUG", 0)};
+  return t;
+}
 
 }  // namespace
 
@@ -204,43 +223,82 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
   const int dt = lay->dtype;
   const size_t es = elem_size(dt);
   const int64_t nblk = lay->n_pad / NB;
-  for (int64_t k = 0; k < nblk; ++k) {
-    const int64_t j0 = k * NB;
+
+  // diagonal block k: factor + invert
+  auto diag = [&](int64_t k) -> hipError_t {
     DiagArgs da;
     da.W = W;
     da.ld = lay->ld;
     da.w_bs = lay->w_batch_stride;
     da.Winv = Winv;
     da.inv_bs = lay->inv_batch_stride;
-    da.j0 = j0;
+    da.j0 = k * NB;
     da.kblk = k;
     da.info = info_dev;
-    GPK_HIP(timed(1, (double)lay->batch * NB * NB * NB / 3.0, 0.0, s,
-                  [&] { return launch_diag(da, dt, lay->batch, s); }),
-            "diag");
-    const int64_t row0 = j0 + NB;
-    const int32_t nt = (int32_t)((lay->p - row0) / NB);
-    if (nt <= 0) continue;
-    GemmArgs ga;
-    ga.W = W;
-    ga.ld = lay->ld;
-    ga.w_bs = lay->w_batch_stride;
+    da.dbg = (int32_t)tune().diag_dbg;
+    return timed(1, (double)lay->batch * NB * NB * NB / 3.0, 0.0, s,
+                 [&] { return launch_diag(da, dt, lay->batch, s); });
+  };
+  GemmArgs base;
+  memset(&base, 0, sizeof(base));
+  base.W = W;
+  base.ld = lay->ld;
+  base.w_bs = lay->w_batch_stride;
+  base.inv_bs = lay->inv_batch_stride;
+  // panel solve of block k: every row below the block (the y / test rows included)
+  auto trsm = [&](int64_t k) -> hipError_t {
+    GemmArgs ga = base;
     ga.Binv = static_cast<const char*>(Winv) + (size_t)k * NB * NB * es;
-    ga.inv_bs = lay->inv_batch_stride;
+    ga.j0 = k * NB;
+    ga.row0 = ga.j0 + NB;
+    const int64_t rows = lay->p - ga.row0;
+    if (rows <= 0) return hipSuccess;
+    const int tile = (rows / NB * lay->batch >= tune().trsm_t128_min) ? 128 : 64;
+    ga.nt = (int32_t)(rows / tile);
+    ga.kdepth = NB;
+    const double rK = (double)(lay->n_pad - ga.row0);  // algorithmic: K-part rows x nb^2
+    return timed(2, (double)lay->batch * rK * NB * NB, 0.0, s,
+                 [&] { return launch_gemm(ga, dt, GEMM_TRSM, tile, lay->batch, s); });
+  };
+  // trailing update from panel columns [j0, j0 + kdepth): rows/cols >= row0 = j0 + kdepth;
+  // ncols128 > 0 restricts the update to that many 128-column blocks (thin update)
+  auto update = [&](int64_t j0, int kdepth, int64_t ncols128) -> hipError_t {
+    GemmArgs ga = base;
     ga.j0 = j0;
-    ga.row0 = row0;
-    ga.nt = nt;
+    ga.row0 = j0 + kdepth;
+    ga.kdepth = kdepth;
+    const int64_t rows = lay->p - ga.row0;
+    if (rows <= 0) return hipSuccess;
+    const int64_t t128 = rows / NB;
+    const int64_t w128 = ncols128 > 0 ? ncols128 : t128;
+    const int64_t tiles128 = w128 * (w128 + 1) / 2 + (t128 - w128) * w128;
+    const int tile = (tiles128 * lay->batch >= tune().upd_t128_min) ? 128 : 64;
+    const int64_t scale = NB / tile;
+    ga.nt = (int32_t)(rows / tile);
     ga.c_lo = 0;
-    ga.c_hi = nt;
-    // algorithmic work: rows below the block of the K part times the panel (solve)
-    const double rK = (double)(lay->n_pad - row0);
-    GPK_HIP(timed(2, (double)lay->batch * rK * NB * NB, 0.0, s,
-                  [&] { return launch_gemm(ga, dt, GEMM_TRSM, lay->batch, s); }),
-            "trsm");
-    // algorithmic work of the trailing SYRK on the K part: 2 * nb * r(r+1)/2
-    GPK_HIP(timed(3, (double)lay->batch * NB * rK * (rK + 1.0), 0.0, s,
-                  [&] { return launch_gemm(ga, dt, GEMM_UPDATE, lay->batch, s); }),
-            "update");
+    ga.c_hi = (int32_t)(w128 * scale);
+    // algorithmic flops: 2 * kdepth * (lower-triangular elements of the K part updated)
+    const double rK = (double)(lay->n_pad - ga.row0);
+    const double wK = ncols128 > 0 ? (double)(ncols128 * NB) : rK;
+    const double elems = rK > 0 ? (wK * (wK + 1.0) / 2.0 + (rK - wK) * wK) : 0.0;
+    return timed(3, (double)lay->batch * 2.0 * kdepth * elems, 0.0, s,
+                 [&] { return launch_gemm(ga, dt, GEMM_UPDATE, tile, lay->batch, s); });
+  };
+
+  // Two 128-column panels per trailing update (K = 256): factor panel k, apply it to the next
+  // block column only, factor panel k+1, then update the rest of the trailing matrix with both
+  // panels at once.  Halves the read-modify-write passes over the trailing matrix.
+  for (int64_t k = 0; k < nblk; k += 2) {
+    GPK_HIP(diag(k), "diag");
+    GPK_HIP(trsm(k), "trsm");
+    if (k + 1 < nblk) {
+      GPK_HIP(update(k * NB, NB, 1), "update thin");
+      GPK_HIP(diag(k + 1), "diag");
+      GPK_HIP(trsm(k + 1), "trsm");
+      GPK_HIP(update(k * NB, 2 * NB, 0), "update");
+    } else {
+      GPK_HIP(update(k * NB, NB, 0), "update");
+    }
   }
   return 0;
 }

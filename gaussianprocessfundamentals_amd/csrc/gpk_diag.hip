@@ -1,0 +1,230 @@
+// Diagonal-block factorisation of the blocked Cholesky: one 512-thread workgroup per batch
+// member factors the 128 x 128 block at (j0, j0) of W in LDS and inverts the factor.
+//
+// The block is handled as 8 x 8 tiles of 16 x 16, every tile operation an f64 MFMA chain
+// (v_mfma_f64_16x16x4_f64, 4 MFMAs per 16-deep product):
+//   for kb = 0..7:
+//     wave 0   : potf2 of tile (kb, kb) in registers (lane r owns row r, pivots broadcast
+//                with v_readlane) and its inverse Dinv_kb
+//     waves    : panel tiles  X_i = A_{i,kb} Dinv_kb^T                  (i > kb)
+//     waves    : trailing     A_{i,j} -= X_i X_j^T                      (kb < j <= i)
+//   inverse by block rows (I = 0..7), one wave per tile column J < I:
+//     Linv_{I,J} = -Dinv_I (sum_{K=J}^{I-1} L_{I,K} Linv_{K,J}),   Linv_{I,I} = Dinv_I
+// The f64 C/D layout (col = lane & 15, row = (lane >> 4) + 4 reg) equals the B-operand layout
+// of k-step s = reg, so the inner product T stays in registers between the two MFMA chains.
+//
+// Writes L_kk to W (lower triangle) and L_kk^-1 (zeros above the diagonal) to Winv; the first
+// non-positive pivot (1-based global column) goes to info[b] (LAPACK convention, as the
+// InvalidArgumentError of tf.linalg.cholesky at gpbasics/Statistics/CovarianceMatrix.py:250).
+#include "gpk_internal.h"
+
+namespace gpk {
+namespace {
+
+constexpr int DB = 16;            // tile edge
+constexpr int NTL = NB / DB;      // tiles per block edge (8)
+constexpr int LDA = NB + 2;       // LDS row stride (doubles): 16 rows of one column on distinct banks
+constexpr int DT = 512;           // threads (8 waves)
+constexpr int LDS_A = NB * LDA;
+constexpr int LDS_DINV = NTL * DB * DB;
+constexpr size_t DIAG_LDS_BYTES = sizeof(double) * (LDS_A + LDS_DINV) + 16;
+
+__device__ __forceinline__ double rdlane(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// 1/sqrt(x) from the hardware estimate plus two Newton steps (~1 ulp); NaN for x < 0.
+__device__ __forceinline__ double rsqrt_refined(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  r = r * fma(-h * r, r, 1.5);
+  r = r * fma(-h * r, r, 1.5);
+  return r;
+}
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// potf2 + inverse of tile (kb, kb), one wave.  Lanes 16..63 mirror lanes 0..15 and never store.
+__device__ __forceinline__ void potf2_tile(double* A, double* Dk, int kb, int lane, int* flag,
+                                           int64_t col_base) {
+  const int r = lane & 15;
+  const int c0 = kb * DB;
+  double v[DB], rinv[DB];
+#pragma unroll
+  for (int c = 0; c < DB; ++c) v[c] = (c <= r) ? A[(c0 + r) * LDA + c0 + c] : 0.0;
+#pragma unroll
+  for (int j = 0; j < DB; ++j) {
+    const double piv = rdlane(v[j], j);
+    if (!(piv > 0.0) && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + j + 1);
+    const double ri = rsqrt_refined(piv);
+    rinv[j] = ri;
+    v[j] = (r == j) ? piv * ri : v[j] * ri;
+#pragma unroll
+    for (int c = j + 1; c < DB; ++c) v[c] = fma(-v[j], rdlane(v[j], c), v[c]);
+  }
+  // column r of the inverse: forward substitution, rows broadcast lane-uniformly
+  double x[DB];
+#pragma unroll
+  for (int rr = 0; rr < DB; ++rr) {
+    double s = (rr == r) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < rr; ++k) s = fma(-rdlane(v[k], rr), x[k], s);
+    x[rr] = s * rinv[rr];
+  }
+  if (lane < DB) {
+#pragma unroll
+    for (int c = 0; c < DB; ++c) A[(c0 + r) * LDA + c0 + c] = (c <= r) ? v[c] : 0.0;
+#pragma unroll
+    for (int rr = 0; rr < DB; ++rr) Dk[rr * DB + r] = x[rr];  // Dinv[rr][r]
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* A = sm;
+  double* Dinv = A + LDS_A;
+  int* flag = reinterpret_cast<int*>(Dinv + LDS_DINV);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int lr = lane & 15;       // MFMA operand row / C-D column
+  const int lk = lane >> 4;       // MFMA operand k within a 4-step / C-D row offset
+  const int b = blockIdx.x;
+  T* Wb = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs + a.j0 * a.ld + a.j0;
+  // 8 loads in flight per thread before the LDS stores (a plain loop serialises load/store)
+  constexpr int PER = NB * NB / DT;
+#pragma unroll
+  for (int g = 0; g < PER; g += 8) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + (g + q) * DT;
+      const int r = e >> 7, c = e & (NB - 1);
+      v[q] = (c <= r) ? (double)Wb[(int64_t)r * a.ld + c] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + (g + q) * DT;
+      A[(e >> 7) * LDA + (e & (NB - 1))] = v[q];
+    }
+  }
+  if (tid == 0) *flag = 0;
+  __syncthreads();
+
+  for (int kb = 0; kb < NTL; ++kb) {
+    double* Dk = Dinv + kb * DB * DB;
+    if (wave == 0 && !(a.dbg & 2)) potf2_tile(A, Dk, kb, lane, flag, a.j0);
+    if (a.dbg & 4) continue;
+    __syncthreads();
+    if (kb == NTL - 1) break;
+    // panel: X_i = A_{i,kb} * Dinv_kb^T   (B[k][c] = Dinv[c][k])
+    {
+      const int i = kb + 1 + wave;
+      if (i < NTL) {
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const double av = A[(i * DB + lr) * LDA + kb * DB + 4 * s + lk];
+          const double bv = Dk[lr * DB + 4 * s + lk];
+          acc = mfma64(av, bv, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + kb * DB + lr] = acc[q];
+      }
+    }
+    __syncthreads();
+    // trailing tiles (i, j), kb < j <= i: A_ij -= X_i X_j^T
+    {
+      const int m = NTL - 1 - kb;
+      const int ntri = m * (m + 1) / 2;
+      for (int t = wave; t < ntri; t += DT / 64) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+        const int tj = t - ti * (ti + 1) / 2;
+        const int i = kb + 1 + ti, j = kb + 1 + tj;
+        d4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = A[(i * DB + lk + 4 * q) * LDA + j * DB + lr];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const double av = -A[(i * DB + lr) * LDA + kb * DB + 4 * s + lk];
+          const double bv = A[(j * DB + lr) * LDA + kb * DB + 4 * s + lk];
+          acc = mfma64(av, bv, acc);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + j * DB + lr] = acc[q];
+      }
+    }
+    __syncthreads();
+  }
+
+  // L_kk back to W (lower triangle only)
+  for (int e = tid; e < NB * NB; e += DT) {
+    const int r = e >> 7, c = e & (NB - 1);
+    if (c <= r) Wb[(int64_t)r * a.ld + c] = (T)A[r * LDA + c];
+  }
+  if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
+
+  // inverse by 16-row blocks, in place (block rows < I of A hold Linv, row I still holds L)
+  for (int I = 0; I < ((a.dbg & 1) ? 0 : NTL); ++I) {
+    const int J = wave;
+    const bool active = J < I;
+    d4 out = {0.0, 0.0, 0.0, 0.0};
+    if (active) {
+      d4 tacc = {0.0, 0.0, 0.0, 0.0};
+      for (int K = J; K < I; ++K) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const double av = A[(I * DB + lr) * LDA + K * DB + 4 * s + lk];
+          const double bv = A[(K * DB + 4 * s + lk) * LDA + J * DB + lr];
+          tacc = mfma64(av, bv, tacc);
+        }
+      }
+      const double* Di = Dinv + I * DB * DB;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) out = mfma64(-Di[lr * DB + 4 * s + lk], tacc[s], out);
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) A[(I * DB + lk + 4 * q) * LDA + J * DB + lr] = out[q];
+    }
+    if (wave == NTL - 1) {
+      const double* Di = Dinv + I * DB * DB;
+      for (int e = lane; e < DB * DB; e += 64) A[(I * DB + e / DB) * LDA + I * DB + e % DB] = Di[e];
+    }
+    __syncthreads();
+  }
+  T* Ib = reinterpret_cast<T*>(a.Winv) + (int64_t)b * a.inv_bs + a.kblk * NB * NB;
+  for (int e = tid; e < NB * NB; e += DT) {
+    const int r = e >> 7, c = e & (NB - 1);
+    Ib[e] = (T)((c <= r) ? A[r * LDA + c] : 0.0);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s) {
+  static bool attr_done[2] = {false, false};
+  const void* fn = dtype == GPK_F64 ? reinterpret_cast<const void*>(diag_kernel<double>)
+                                    : reinterpret_cast<const void*>(diag_kernel<float>);
+  bool& done = attr_done[dtype == GPK_F64 ? 0 : 1];
+  if (!done) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DIAG_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    done = true;
+  }
+  if (dtype == GPK_F64)
+    hipLaunchKernelGGL(diag_kernel<double>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+  else
+    hipLaunchKernelGGL(diag_kernel<float>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gpk

@@ -50,6 +50,7 @@ struct GemmArgs {
   int64_t row0;      // first row (and column) of the trailing region
   int32_t nt;        // 128-tiles of the trailing region
   int32_t c_lo, c_hi;  // tile-column range handled by this launch (update)
+  int32_t kdepth;      // panel width summed over (multiple of 16): 128, or 256 for the deferred update
 };
 
 struct DiagArgs {
@@ -61,6 +62,7 @@ struct DiagArgs {
   int64_t j0;
   int64_t kblk;
   int32_t* info;
+  int32_t dbg;  // timing-only ablations (GPK_DIAG_DEBUG): 1 no inverse, 2 no potf2, 4 no tile ops
 };
 
 struct FinArgs {
@@ -91,7 +93,7 @@ struct TrsvArgs {
 hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
                            hipStream_t s);
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s);
-hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int32_t batch, hipStream_t s);
+hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s);
 hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_trsv_diag(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);

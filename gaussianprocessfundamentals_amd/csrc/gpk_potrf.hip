@@ -1,20 +1,20 @@
-// Blocked right-looking Cholesky of the augmented matrix W (see include/gpk.h), plus the
-// read-out and the triangular solves.
+// MFMA GEMM of the blocked Cholesky (panel solve + trailing update), the read-out, and the
+// triangular solves.  The diagonal-block factorisation lives in gpk_diag.hip.
 //
 // Replaces tf.linalg.cholesky / tf.linalg.triangular_solve of
 // gpbasics/Statistics/CovarianceMatrix.py:247-265 and the log-determinant / data-fit
 // assembly of gpbasics/Metrics/Metrics.py:152-154 and gpbasics/Metrics/LogLikelihood.py:30-65.
 //
 // Per panel step k (columns j0 = 128k .. j0+127):
-//   diag_kernel      one workgroup per batch member factors the 128 x 128 diagonal block in
-//                    LDS (inner 16-blocks: register potf2 by one wave + parallel panel solve and
-//                    rank-16 update), then inverts it (row-block recursion on the 16-block
-//                    inverses).  Writes L_kk to W and L_kk^-1 to Winv.
-//   gemm<TRSM>       rows below the block: W[R, j0:j0+128] <- W[R, j0:j0+128] * L_kk^-T
-//                    (an MFMA GEMM against the inverted block; every row of the augmented
-//                    matrix, so z = L^-1 y and V^T = Ks^T L^-T come out of the same launch)
-//   gemm<UPDATE>     lower tiles of the trailing matrix: C -= P P^T on f64 MFMA
-//                    (v_mfma_f64_16x16x4_f64) or f32 MFMA (v_mfma_f32_16x16x4_f32)
+//   gemm<TRSM>    rows below the block: W[R, j0:j0+128] <- W[R, j0:j0+128] * L_kk^-T, an MFMA
+//                 GEMM against the inverted diagonal block (upper zero blocks skipped); every
+//                 row of the augmented matrix, so z = L^-1 y and V^T = Ks^T L^-T come out of it
+//   gemm<UPDATE>  lower tiles of the trailing matrix: C -= P P^T, f64 MFMA
+//                 (v_mfma_f64_16x16x4_f64) or f32 MFMA (v_mfma_f32_16x16x4_f32)
+// Tiles are TM x TN (128 x 128 while the grid fills the chip, 64 x 64 on small trailing
+// matrices); a 256-thread workgroup = 2 x 2 waves, double-buffered LDS staging of 16-deep K
+// chunks through registers; block ids are remapped so that each XCD (blockIdx % 8) walks a
+// contiguous run of tiles, which share panel rows in its L2.
 #include <math.h>
 
 #include "gpk_internal.h"
@@ -22,206 +22,6 @@
 namespace gpk {
 namespace {
 
-constexpr int DB = 16;         // inner block of the diagonal factorisation
-constexpr int LDA = NB + 1;    // LDS row stride of the 128 x 128 diagonal block (doubles)
-
-__device__ __forceinline__ double rdlane(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
-
-// ================================================================================ diagonal block
-// LDS map (doubles): A[128][129] | Dinv[8][16][16] | T[16][112] | flag (int)
-constexpr int LDS_A = NB * LDA;
-constexpr int LDS_DINV = (NB / DB) * DB * DB;
-constexpr int LDS_T = DB * (NB - DB);
-constexpr int DT = 512;       // threads of the diagonal-block workgroup
-constexpr int DQ = 2048 / DT;  // per-thread items of the 16 x 128 phases
-constexpr size_t DIAG_LDS_BYTES = sizeof(double) * (LDS_A + LDS_DINV + LDS_T) + 16;
-
-// One wave factors the 16 x 16 block at (c0, c0) of A in registers (lane r & 15 owns row r)
-// and writes L_D back plus its inverse Dinv (lower, zeros above).
-__device__ __forceinline__ void potf2_16(double* A, int c0, double* Dv, int* flag, int lane,
-                                         int64_t col_base) {
-  const int r = lane & 15;
-  double v[DB];
-#pragma unroll
-  for (int c = 0; c < DB; ++c) v[c] = (c <= r) ? A[(c0 + r) * LDA + c0 + c] : 0.0;
-#pragma unroll
-  for (int j = 0; j < DB; ++j) {
-    const double piv = rdlane(v[j], j);
-    if (!(piv > 0.0) && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + j + 1);
-    const double dj = sqrt(piv);
-    const double rinv = 1.0 / dj;
-    v[j] = (r == j) ? dj : v[j] * rinv;
-#pragma unroll
-    for (int c = j + 1; c < DB; ++c) {
-      const double lcj = rdlane(v[j], c);
-      v[c] = fma(-v[j], lcj, v[c]);
-    }
-  }
-  // column (lane & 15) of the inverse: forward substitution with rows read lane-uniformly
-  double x[DB];
-#pragma unroll
-  for (int rr = 0; rr < DB; ++rr) {
-    double s = (rr == r) ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = 0; k < rr; ++k) s = fma(-rdlane(v[k], rr), x[k], s);
-    x[rr] = s / rdlane(v[rr], rr);
-  }
-  if (lane < DB) {
-#pragma unroll
-    for (int c = 0; c < DB; ++c)
-      if (c <= r) A[(c0 + r) * LDA + c0 + c] = v[c];
-#pragma unroll
-    for (int rr = 0; rr < DB; ++rr) Dv[rr * DB + r] = x[rr];  // Dinv[rr][r]
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* A = sm;
-  double* Dinv = A + LDS_A;
-  double* Tt = Dinv + LDS_DINV;
-  int* flag = reinterpret_cast<int*>(Tt + LDS_T);
-
-  const int tid = threadIdx.x;
-  const int b = blockIdx.x;
-  T* Wb = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs + a.j0 * a.ld + a.j0;
-  for (int e = tid; e < NB * NB; e += DT) {
-    const int r = e >> 7, c = e & (NB - 1);
-    A[r * LDA + c] = (c <= r) ? (double)Wb[(int64_t)r * a.ld + c] : 0.0;
-  }
-  if (tid == 0) *flag = 0;
-  __syncthreads();
-
-  for (int kb = 0; kb < NB / DB; ++kb) {
-    const int c0 = kb * DB;
-    double* Dk = Dinv + kb * DB * DB;
-    if (tid < 64) potf2_16(A, c0, Dk, flag, tid, a.j0);
-    __syncthreads();
-    const int nrow = NB - c0 - DB;
-    if (nrow == 0) break;
-    // panel below the 16-block: X = B * Dinv^T, via registers (in place)
-    double xv[DQ];
-#pragma unroll
-    for (int q = 0; q < DQ; ++q) {
-      const int idx = tid + q * DT;
-      xv[q] = 0.0;
-      if (idx < nrow * DB) {
-        const int r = c0 + DB + idx / DB, c = idx % DB;
-        double s = 0.0;
-        for (int k = 0; k <= c; ++k) s = fma(A[r * LDA + c0 + k], Dk[c * DB + k], s);
-        xv[q] = s;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < DQ; ++q) {
-      const int idx = tid + q * DT;
-      if (idx < nrow * DB) A[(c0 + DB + idx / DB) * LDA + c0 + idx % DB] = xv[q];
-    }
-    __syncthreads();
-    // trailing rank-16 update of the lower triangle, 4 x 4 micro-tiles
-    const int nt = nrow / 4;
-    const int ntri = nt * (nt + 1) / 2;
-    for (int t = tid; t < ntri; t += DT) {
-      int ti = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-      while (ti * (ti + 1) / 2 > t) --ti;
-      while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-      const int tj = t - ti * (ti + 1) / 2;
-      const int rb = c0 + DB + 4 * ti, cb = c0 + DB + 4 * tj;
-      double acc[4][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
-#pragma unroll 2
-      for (int k = 0; k < DB; ++k) {
-        double ar[4], ac[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ar[i] = A[(rb + i) * LDA + c0 + k];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ac[j] = A[(cb + j) * LDA + c0 + k];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = fma(ar[i], ac[j], acc[i][j]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (cb + j <= rb + i) A[(rb + i) * LDA + cb + j] -= acc[i][j];
-    }
-    __syncthreads();
-  }
-
-  // L_kk back to W (lower triangle only)
-  for (int e = tid; e < NB * NB; e += DT) {
-    const int r = e >> 7, c = e & (NB - 1);
-    if (c <= r) Wb[(int64_t)r * a.ld + c] = (T)A[r * LDA + c];
-  }
-  if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
-  __syncthreads();
-
-  // In-place inverse by 16-row blocks:
-  //   Linv[I, <I] = -Dinv_I * (L[I, <I] * Linv[<I, <I]),  Linv[I, I] = Dinv_I.
-  // Row blocks < I of A already hold Linv; row block I still holds L.
-  for (int I = 0; I < NB / DB; ++I) {
-    const int r0 = I * DB;
-    const int ncol = r0;  // strictly-lower columns of this row block
-    double tv[DQ];
-#pragma unroll
-    for (int q = 0; q < DQ; ++q) {
-      const int idx = tid + q * DT;
-      tv[q] = 0.0;
-      if (idx < DB * ncol) {
-        const int r = idx / ncol, c = idx % ncol;
-        double s = 0.0;
-        for (int k = c; k < r0; ++k) s = fma(A[(r0 + r) * LDA + k], A[k * LDA + c], s);
-        tv[q] = s;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < DQ; ++q) {
-      const int idx = tid + q * DT;
-      if (idx < DB * ncol) Tt[(idx / ncol) * (NB - DB) + idx % ncol] = tv[q];
-    }
-    __syncthreads();
-    const double* Di = Dinv + I * DB * DB;
-#pragma unroll
-    for (int q = 0; q < DQ; ++q) {
-      const int idx = tid + q * DT;
-      if (idx < DB * ncol) {
-        const int r = idx / ncol, c = idx % ncol;
-        double s = 0.0;
-        for (int k = 0; k <= r; ++k) s = fma(Di[r * DB + k], Tt[k * (NB - DB) + c], s);
-        tv[q] = -s;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < DQ; ++q) {
-      const int idx = tid + q * DT;
-      if (idx < DB * ncol) A[(r0 + idx / ncol) * LDA + idx % ncol] = tv[q];
-    }
-    if (tid < DB * DB) {
-      const int r = tid / DB, c = tid % DB;
-      A[(r0 + r) * LDA + r0 + c] = Di[r * DB + c];
-    }
-    __syncthreads();
-  }
-  T* Ib = reinterpret_cast<T*>(a.Winv) + (int64_t)b * a.inv_bs + a.kblk * NB * NB;
-  for (int e = tid; e < NB * NB; e += DT) {
-    const int r = e >> 7, c = e & (NB - 1);
-    Ib[e] = (T)((c <= r) ? A[r * LDA + c] : 0.0);
-  }
-}
-
-// ================================================================================ MFMA GEMM
 template <typename T>
 struct Mfma;
 template <>
@@ -243,30 +43,38 @@ struct Mfma<float> {
   static __device__ __forceinline__ int row(int lane, int reg) { return 4 * (lane >> 4) + reg; }
 };
 
+#ifndef GPK_SCHED_FENCE
+#define GPK_SCHED_FENCE 0  // fence the staging loads ahead of the MFMA block (A/B knob)
+#endif
+
 constexpr int GBK = 16;   // K depth staged per LDS buffer
-constexpr int SLD = 18;   // LDS row stride (elements): rows 0..15 at one k, and k+1, on distinct banks
+constexpr int SLD = 18;   // LDS row stride (elements): 16 rows at one k, and k+1, on distinct banks
 
-template <typename T>
-struct Stage {
-  static constexpr int EPC = 16 / (int)sizeof(T);  // elements per 16-B chunk
-  static constexpr int CPR = GBK / EPC;            // chunks per row
-  static constexpr int NCH = NB * CPR / 256;       // chunks per thread per operand
-};
+// bijective XCD-aware remap: consecutive logical tiles land on one XCD (blockIdx % 8 group)
+__device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk) {
+  const int64_t q = nblk / 8, r = nblk % 8;
+  const int64_t x = bid % 8, pos = bid / 8;
+  const int64_t base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + pos;
+}
 
-// One 256-thread workgroup computes one 128 x 128 tile: acc = A_rows(128 x 128) * B_rows(128 x 128)^T
-// over the 128-wide panel, 4 waves in a 2 x 2 grid, each 64 x 64 = 4 x 4 MFMA blocks.
-// A and B are row-major with the K index contiguous; double-buffered LDS, register-staged.
-template <typename T, int MODE>
+// One 256-thread workgroup computes a TM x TN tile: acc = A_rows(TM x 128) * B_rows(TN x 128)^T
+// over the 128-wide panel.  Waves 2 x 2, each (TM/2) x (TN/2) = MB x NBK blocks of 16 x 16.
+template <typename T, int MODE, int TM, int TN>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
-  typedef Stage<T> S;
+  constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B chunk
+  constexpr int CPR = GBK / EPC;             // chunks per row and K chunk
+  constexpr int NCA = TM * CPR / 256;        // A chunks per thread
+  constexpr int NCB = TN * CPR / 256;        // B chunks per thread
+  constexpr int MB = TM / 32, NBK = TN / 32; // 16 x 16 blocks per wave
   typedef typename Mfma<T>::acc_t acc_t;
-  __shared__ __attribute__((aligned(16))) T sA[2][NB * SLD];
-  __shared__ __attribute__((aligned(16))) T sB[2][NB * SLD];
+  __shared__ __attribute__((aligned(16))) T sA[2][TM * SLD];
+  __shared__ __attribute__((aligned(16))) T sB[2][TN * SLD];
 
   const int b = blockIdx.y;
-  int64_t ti, tj;
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
+  int64_t ti, tj;  // tile coordinates in units of TM (rows) and TN (cols)
   if (MODE == GEMM_UPDATE) {
-    const int64_t t = blockIdx.x;
     const int64_t w = a.c_hi - a.c_lo;
     const int64_t ttri = w * (w + 1) / 2;
     if (t < ttri) {
@@ -281,16 +89,16 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
       tj = a.c_lo + u % w;
     }
   } else {
-    ti = blockIdx.x;
+    ti = t;
     tj = 0;
   }
   T* W = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs;
-  const int64_t R = a.row0 + ti * NB;
+  const int64_t R = a.row0 + ti * TM;
   const T* Ag = W + R * a.ld + a.j0;
   const T* Bg;
   int64_t ldb;
   if (MODE == GEMM_UPDATE) {
-    Bg = W + (a.row0 + tj * NB) * a.ld + a.j0;
+    Bg = W + (a.row0 + tj * TN) * a.ld + a.j0;
     ldb = a.ld;
   } else {
     Bg = reinterpret_cast<const T*>(a.Binv) + (int64_t)b * a.inv_bs;
@@ -302,98 +110,118 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
   const int wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
 
-  uint4 ra[S::NCH], rb[S::NCH];
-  const T* pga[S::NCH];
-  const T* pgb[S::NCH];
-  int loff[S::NCH];
+  uint4 ra[NCA], rb[NCB];
+  const T* pga[NCA];
+  const T* pgb[NCB];
+  int la[NCA], lb[NCB];
 #pragma unroll
-  for (int u = 0; u < S::NCH; ++u) {
+  for (int u = 0; u < NCA; ++u) {
     const int q = tid + 256 * u;
-    const int row = q / S::CPR, ch = q % S::CPR;
-    pga[u] = Ag + (int64_t)row * a.ld + ch * S::EPC;
-    pgb[u] = Bg + (int64_t)row * ldb + ch * S::EPC;
-    loff[u] = row * SLD + ch * S::EPC;
+    pga[u] = Ag + (int64_t)(q / CPR) * a.ld + (q % CPR) * EPC;
+    la[u] = (q / CPR) * SLD + (q % CPR) * EPC;
   }
-#define GPK_GLOAD(kc)                                                           \
-  _Pragma("unroll") for (int u = 0; u < S::NCH; ++u) {                          \
-    ra[u] = *reinterpret_cast<const uint4*>(pga[u] + (kc) * GBK);               \
-    rb[u] = *reinterpret_cast<const uint4*>(pgb[u] + (kc) * GBK);               \
+#pragma unroll
+  for (int u = 0; u < NCB; ++u) {
+    const int q = tid + 256 * u;
+    pgb[u] = Bg + (int64_t)(q / CPR) * ldb + (q % CPR) * EPC;
+    lb[u] = (q / CPR) * SLD + (q % CPR) * EPC;
   }
-#define GPK_LSTORE(buf)                                                         \
-  _Pragma("unroll") for (int u = 0; u < S::NCH; ++u) {                          \
-    T* pa_ = &sA[buf][loff[u]];                                                 \
-    T* pb_ = &sB[buf][loff[u]];                                                 \
-    if (sizeof(T) == 8) {                                                       \
-      *reinterpret_cast<uint4*>(pa_) = ra[u];                                   \
-      *reinterpret_cast<uint4*>(pb_) = rb[u];                                   \
-    } else {                                                                    \
-      reinterpret_cast<uint2*>(pa_)[0] = make_uint2(ra[u].x, ra[u].y);          \
-      reinterpret_cast<uint2*>(pa_)[1] = make_uint2(ra[u].z, ra[u].w);          \
-      reinterpret_cast<uint2*>(pb_)[0] = make_uint2(rb[u].x, rb[u].y);          \
-      reinterpret_cast<uint2*>(pb_)[1] = make_uint2(rb[u].z, rb[u].w);          \
-    }                                                                           \
+#define GPK_GLOAD(kc)                                                                     \
+  {                                                                                       \
+    _Pragma("unroll") for (int u = 0; u < NCA; ++u) ra[u] =                               \
+        *reinterpret_cast<const uint4*>(pga[u] + (kc) * GBK);                             \
+    _Pragma("unroll") for (int u = 0; u < NCB; ++u) rb[u] =                               \
+        *reinterpret_cast<const uint4*>(pgb[u] + (kc) * GBK);                             \
+  }
+#define GPK_STORE16(dst, v)                                                               \
+  {                                                                                       \
+    if (sizeof(T) == 8) {                                                                 \
+      *reinterpret_cast<uint4*>(dst) = (v);                                               \
+    } else {                                                                              \
+      reinterpret_cast<uint2*>(dst)[0] = make_uint2((v).x, (v).y);                        \
+      reinterpret_cast<uint2*>(dst)[1] = make_uint2((v).z, (v).w);                        \
+    }                                                                                     \
+  }
+#define GPK_LSTORE(buf)                                                                   \
+  {                                                                                       \
+    _Pragma("unroll") for (int u = 0; u < NCA; ++u) GPK_STORE16(&sA[buf][la[u]], ra[u]);  \
+    _Pragma("unroll") for (int u = 0; u < NCB; ++u) GPK_STORE16(&sB[buf][lb[u]], rb[u]);  \
   }
 
-  acc_t acc[4][4];
+  acc_t acc[MB][NBK];
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int m = 0; m < MB; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = acc_t{0, 0, 0, 0};
+    for (int n = 0; n < NBK; ++n) acc[m][n] = acc_t{0, 0, 0, 0};
 
-  constexpr int NK = NB / GBK;
+  const int NK = (MODE == GEMM_TRSM) ? NB / GBK : a.kdepth / GBK;
   GPK_GLOAD(0);
   GPK_LSTORE(0);
   __syncthreads();
-  const int arow = (wr * 64 + (lane & 15)) * SLD + (lane >> 4);
-  const int brow = (wc * 64 + (lane & 15)) * SLD + (lane >> 4);
+  const int arow = (wr * (TM / 2) + (lane & 15)) * SLD + (lane >> 4);
+  const int brow = (wc * (TN / 2) + (lane & 15)) * SLD + (lane >> 4);
+  // Fragments are software-pipelined one 4-deep k-step ahead (two register sets), and the next
+  // chunk's first fragments are read right after the barrier, under the last step's MFMAs.
+  T fa0[MB], fb0[NBK], fa1[MB], fb1[NBK];
+#define GPK_FRAG(FA, FB, P, Q, S)                                                          \
+  {                                                                                        \
+    _Pragma("unroll") for (int m = 0; m < MB; ++m) FA[m] = (P)[arow + m * 16 * SLD + (S) * 4]; \
+    _Pragma("unroll") for (int n = 0; n < NBK; ++n) FB[n] = (Q)[brow + n * 16 * SLD + (S) * 4]; \
+  }
+  // TRSM against the lower-triangular inverse: K chunk KC feeds output columns >= 16 KC only
+#define GPK_MMA(FA, FB, KC)                                                                \
+  {                                                                                        \
+    _Pragma("unroll") for (int n = 0; n < NBK; ++n) {                                      \
+      if (MODE == GEMM_TRSM && (KC) > (wc * (TN / 2) + n * 16) / GBK) continue;            \
+      _Pragma("unroll") for (int m = 0; m < MB; ++m) acc[m][n] = Mfma<T>::op(FA[m], FB[n], acc[m][n]); \
+    }                                                                                      \
+  }
+  GPK_FRAG(fa0, fb0, sA[0], sB[0], 0);
   for (int kc = 0; kc < NK; ++kc) {
     const int buf = kc & 1;
-    if (kc + 1 < NK) { GPK_GLOAD(kc + 1); }
+    // branch-free staging (the last iteration re-stages its own chunk into the idle buffer):
+    // a conditional load/store pair makes hipcc spill the staging registers to scratch
+    const int knext = (kc + 1 < NK) ? kc + 1 : kc;
+    GPK_GLOAD(knext);
+    // keep the next chunk's loads in flight under this chunk's MFMAs: without the fence hipcc
+    // sinks every load to its ds_write and serialises them (load, vmcnt(0), write, load, ...)
+    if (GPK_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
     const T* pa = sA[buf];
     const T* pb = sB[buf];
-#pragma unroll
-    for (int s = 0; s < GBK / 4; ++s) {
-      T af[4], bf[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) af[m] = pa[arow + m * 16 * SLD + s * 4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bf[n] = pb[brow + n * 16 * SLD + s * 4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = Mfma<T>::op(af[m], bf[n], acc[m][n]);
-    }
-    if (kc + 1 < NK) { GPK_LSTORE(buf ^ 1); }
+    GPK_FRAG(fa1, fb1, pa, pb, 1);
+    GPK_MMA(fa0, fb0, kc);
+    GPK_FRAG(fa0, fb0, pa, pb, 2);
+    GPK_MMA(fa1, fb1, kc);
+    GPK_FRAG(fa1, fb1, pa, pb, 3);
+    GPK_MMA(fa0, fb0, kc);
+    if (GPK_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
+    GPK_LSTORE(buf ^ 1);
     __syncthreads();
+    GPK_FRAG(fa0, fb0, sA[buf ^ 1], sB[buf ^ 1], 0);
+    GPK_MMA(fa1, fb1, kc);
   }
+#undef GPK_FRAG
+#undef GPK_MMA
+#undef GPK_GLOAD
+#undef GPK_STORE16
+#undef GPK_LSTORE
 
   const int col = lane & 15;
-  if (MODE == GEMM_UPDATE) {
-    T* C = W + R * a.ld + a.row0 + tj * NB;
+  T* C = (MODE == GEMM_UPDATE) ? W + R * a.ld + a.row0 + tj * TN : W + R * a.ld + a.j0;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+  for (int m = 0; m < MB; ++m)
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NBK; ++n)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int rr = wr * 64 + m * 16 + Mfma<T>::row(lane, r);
-          const int cc = wc * 64 + n * 16 + col;
-          T* p = C + (int64_t)rr * a.ld + cc;
+      for (int r = 0; r < 4; ++r) {
+        const int rr = wr * (TM / 2) + m * 16 + Mfma<T>::row(lane, r);
+        const int cc = wc * (TN / 2) + n * 16 + col;
+        T* p = C + (int64_t)rr * a.ld + cc;
+        if (MODE == GEMM_UPDATE)
           *p = *p - acc[m][n][r];
-        }
-  } else {
-    T* C = W + R * a.ld + a.j0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int rr = wr * 64 + m * 16 + Mfma<T>::row(lane, r);
-          const int cc = wc * 64 + n * 16 + col;
-          C[(int64_t)rr * a.ld + cc] = acc[m][n][r];
-        }
-  }
+        else
+          *p = acc[m][n][r];
+      }
 }
 
 // ================================================================================ read-out
@@ -477,50 +305,36 @@ __global__ __launch_bounds__(256) void trsv_update_kernel(TrsvArgs a) {
   }
 }
 
-}  // namespace
-
-hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s) {
-  static bool attr_done[2] = {false, false};
-  if (dtype == GPK_F64) {
-    if (!attr_done[0]) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(diag_kernel<double>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)DIAG_LDS_BYTES);
-      attr_done[0] = true;
-    }
-    hipLaunchKernelGGL(diag_kernel<double>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
-  } else {
-    if (!attr_done[1]) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(diag_kernel<float>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)DIAG_LDS_BYTES);
-      attr_done[1] = true;
-    }
-    hipLaunchKernelGGL(diag_kernel<float>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int32_t batch, hipStream_t s) {
+template <typename T, int MODE, int TM, int TN>
+hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
+  // a.nt / c_lo / c_hi are in units of this launch's tile sizes
   unsigned nblk;
-  if (mode == GEMM_UPDATE) {
+  if (MODE == GEMM_UPDATE) {
     const int64_t w = a.c_hi - a.c_lo;
     nblk = (unsigned)(w * (w + 1) / 2 + (int64_t)(a.nt - a.c_hi) * w);
   } else {
     nblk = (unsigned)a.nt;
   }
   if (nblk == 0) return hipSuccess;
-  dim3 grid(nblk, batch);
+  hipLaunchKernelGGL((gemm_kernel<T, MODE, TM, TN>), dim3(nblk, batch), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s) {
   if (dtype == GPK_F64) {
     if (mode == GEMM_UPDATE)
-      hipLaunchKernelGGL((gemm_kernel<double, GEMM_UPDATE>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_kernel<double, GEMM_TRSM>), grid, dim3(256), 0, s, a);
-  } else {
-    if (mode == GEMM_UPDATE)
-      hipLaunchKernelGGL((gemm_kernel<float, GEMM_UPDATE>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_kernel<float, GEMM_TRSM>), grid, dim3(256), 0, s, a);
+      return tile == 128 ? launch_gemm_t<double, GEMM_UPDATE, 128, 128>(a, batch, s)
+                         : launch_gemm_t<double, GEMM_UPDATE, 64, 64>(a, batch, s);
+    return tile == 128 ? launch_gemm_t<double, GEMM_TRSM, 128, 128>(a, batch, s)
+                       : launch_gemm_t<double, GEMM_TRSM, 64, 128>(a, batch, s);
   }
-  return hipGetLastError();
+  if (mode == GEMM_UPDATE)
+    return tile == 128 ? launch_gemm_t<float, GEMM_UPDATE, 128, 128>(a, batch, s)
+                       : launch_gemm_t<float, GEMM_UPDATE, 64, 64>(a, batch, s);
+  return tile == 128 ? launch_gemm_t<float, GEMM_TRSM, 128, 128>(a, batch, s)
+                     : launch_gemm_t<float, GEMM_TRSM, 64, 128>(a, batch, s);
 }
 
 hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream_t s) {
