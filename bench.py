@@ -52,7 +52,21 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events")
+    ap.add_argument("--roofline-steps", type=int, default=3, help="steps of the look-ahead-off roofline pass")
     return ap.parse_args()
+
+
+def pmc_traffic(cfg, batch):
+    """HBM bytes per update launch from the committed PMC pass (profiles/pmc_traffic.json:
+    2 x FETCH_SIZE + WRITE_SIZE per the gfx950 corrections, averaged over the update dispatches of
+    `tools/pmc_pass.sh` on the same config); None when no pass for this config is on file."""
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get("%s_b%d" % (cfg, batch))
+    except (OSError, ValueError):
+        return None
+    return rec
 
 
 def build_kernel(name, d):
@@ -79,23 +93,37 @@ def cpu_baseline(cfg_name, n, budget_s):
     if hyp is None:
         hyp = [list(np.linspace(0.4, 1.1, d)), 1.0, 0.5]
     x, y = o.make_inputs("metric" if cfg_name == "metric" else cfg_name, n=n)
-    evals = 0
+    # median of >= 5 warm repetitions with the host threads, plus one 1-thread figure
+    times = []
     with threadpool_limits(limits=threads):
-        o.nlml(tree, hyp, noise, x[:512], y[:512])  # warm the BLAS pool
-        t0 = time.perf_counter()
-        while True:
+        o.nlml(tree, hyp, noise, x, y)  # warm (BLAS pool, page-in)
+        t_all = time.perf_counter()
+        while len(times) < 5 or (time.perf_counter() - t_all < budget_s and len(times) < 9):
+            t0 = time.perf_counter()
             o.nlml(tree, hyp, noise, x, y)
-            evals += 1
-            el = time.perf_counter() - t0
-            if el > budget_s or evals >= 8:
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_all > 3 * budget_s:
                 break
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        o.nlml(tree, hyp, noise, x, y)
+        t1 = time.perf_counter() - t0
+    med = sorted(times)[len(times) // 2]
     try:
         cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:  # noqa: BLE001
         cpu_model = "unknown"
-    return {"value": evals / el, "unit": "LML evals/s", "cores": threads, "kind": "port",
-            "sample": "%d full evaluations of the %s workload (N=%d, fp64) by the numpy/SciPy oracle "
-                      "(OpenBLAS dpotrf/dtrtrs), %d threads, %s, %.1f s" % (evals, cfg_name, n, threads, cpu_model, el)}
+    try:
+        from threadpoolctl import threadpool_info
+        blas = ",".join(sorted({"%s %s" % (i.get("internal_api"), i.get("version")) for i in threadpool_info()
+                                if i.get("user_api") == "blas"}))
+    except Exception:  # noqa: BLE001
+        blas = "unknown"
+    return {"value": 1.0 / med, "unit": "LML evals/s", "cores": threads, "kind": "port",
+            "value_1_thread": 1.0 / t1,
+            "sample": "median of %d warm full evaluations of the %s workload (N=%d, fp64: K build, dpotrf, "
+                      "2 x dtrtrs, read-out) by the numpy/SciPy oracle, %d threads (%s), %s; plus one "
+                      "1-thread evaluation (%.1f s)" % (len(times), cfg_name, n, threads, blas, cpu_model, t1)}
 
 
 def main():
@@ -173,6 +201,22 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     timing = nat.timing_read() if use_events else None
+    # Roofline pass: a few more steps with the look-ahead off, so that every kernel runs alone on
+    # the caller's stream and its HIP-event duration is its own (in the timed region above the
+    # bulk update shares the chip with the panel chain, which stretches each launch's span).
+    iso = None
+    if use_events:
+        old_la = nat.tune("lookahead", 0)
+        step()
+        torch.cuda.synchronize()
+        nat.timing_reset()
+        nat.timing_enable(True)
+        for _ in range(args.roofline_steps):
+            step()
+        torch.cuda.synchronize()
+        nat.timing_enable(False)
+        iso = nat.timing_read()
+        nat.tune("lookahead", old_la)
     nl = float(fact.nlml()[0].item())
     info = int(fact.info.abs().max().item())
 
@@ -185,16 +229,26 @@ def main():
         roof = None
         breakdown = None
         if timing:
-            up = timing["update"]
+            pmc = pmc_traffic(args.config, batch)
+            up = iso["update"]
             ach = up["flops"] / (up["ms"] * 1e-3) / 1e12 if up["ms"] > 0 else 0.0
+            ov = timing["update"]
             roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK[dtn], "unit": "TFLOP/s",
-                    "frac": round(ach / PEAK[dtn], 4), "traffic": None,
+                    "frac": round(ach / PEAK[dtn], 4), "traffic": (pmc.get("hbm_bytes_per_launch") if pmc else None),
+                    "traffic_source": (pmc.get("source") if pmc else None),
                     "kernel": "gemm_kernel<UPDATE> (trailing SYRK, %s MFMA 16x16x4)" % dtn,
-                    "launches_per_step": up["launches"] // args.steps,
-                    "avg_launch_us": round(up["ms"] * 1e3 / max(1, up["launches"]), 2)}
+                    "measured_in": "%d-step post-pass with the look-ahead off (kernels serialised on one "
+                                   "stream); the rocprof trace's last %d update dispatches" % (
+                                       args.roofline_steps, up["launches"]),
+                    "launches_per_step": up["launches"] // args.roofline_steps,
+                    "avg_launch_us": round(up["ms"] * 1e3 / max(1, up["launches"]), 2),
+                    "algorithmic_gflop_per_launch": round(up["flops"] / max(1, up["launches"]) / 1e9, 4),
+                    "algorithmic_bytes_per_launch": round(up["bytes"] / max(1, up["launches"])),
+                    "overlapped_achieved": round(ov["flops"] / (ov["ms"] * 1e-3) / 1e12, 3) if ov["ms"] > 0 else None}
             asm = timing["assemble"]
             breakdown = {k: round(v["ms"] / args.steps, 4) for k, v in timing.items()}
             breakdown["kbuild_GBps"] = round(asm["bytes"] / (asm["ms"] * 1e-3) / 1e9, 1) if asm["ms"] > 0 else None
+            breakdown["note"] = "sums of kernel spans per class; with the look-ahead the classes overlap"
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.config, n, args.cpu_seconds)

@@ -26,7 +26,7 @@ TIMING_CLASSES = ("assemble", "diag", "trsm", "update", "finalize", "trsv")
 EXPORTS = (
     "gpk_abi_version", "gpk_last_error", "gpk_plan", "gpk_assemble", "gpk_potrf_aug",
     "gpk_finalize", "gpk_nlml", "gpk_kernel_matrix", "gpk_trsv", "gpk_timing_enable",
-    "gpk_timing_read", "gpk_timing_reset",
+    "gpk_timing_read", "gpk_timing_reset", "gpk_tune",
 )
 
 
@@ -76,6 +76,7 @@ def _declare(lib):
         "gpk_timing_enable": (c_int, [c_int]),
         "gpk_timing_read": (c_int, [D, POINTER(c_int64), D, D]),
         "gpk_timing_reset": (c_int, []),
+        "gpk_tune": (c_int, [ctypes.c_char_p, c_int64, ctypes.POINTER(c_int64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -147,6 +148,13 @@ def dtype_code(torch_dtype) -> int:
 
 def timing_enable(on: bool = True):
     check(load_library().gpk_timing_enable(1 if on else 0), "gpk_timing_enable")
+
+
+def tune(key: str, value: int) -> int:
+    """Set a scheduling knob of libgpk (see gpk_tune in include/gpk.h); returns the old value."""
+    old = c_int64(0)
+    check(load_library().gpk_tune(key.encode(), int(value), ctypes.byref(old)), "gpk_tune")
+    return int(old.value)
 
 
 def timing_reset():

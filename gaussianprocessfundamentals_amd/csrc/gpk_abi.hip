@@ -4,6 +4,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <initializer_list>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -108,6 +110,8 @@ struct Tune {
   int64_t upd_t128_min;   // 128 x 128 update tiles when at least this many (else 64 x 64)
   int64_t trsm_t128_min;  // 128-row panel-solve tiles when at least this many (else 64)
   int64_t diag_dbg;       // timing-only ablation flags of the diagonal kernel (never set in production)
+  int64_t lookahead;      // 1: panel chain on a high-priority side stream (default), 0: one stream
+  int64_t reserve_cus;    // CUs kept free of the bulk trailing update for the panel chain
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -115,10 +119,46 @@ int64_t env_i64(const char* name, int64_t dflt) {
   return (v && *v) ? (int64_t)atoll(v) : dflt;
 }
 
-const Tune& tune() {
-  static const Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
-                         env_i64("GPK_DIAG_DEBUG", 0)};
+Tune& tune() {
+  static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
+                         env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
+                         env_i64("GPK_RESERVE_CUS", 8)};
   return t;
+}
+
+// Per host thread and device: the high-priority panel stream, the bulk-update stream (created
+// with a CU mask that leaves tune().reserve_cus CUs to the panel chain, so that the
+// diagonal-block kernel -- one workgroup of 150 KB LDS per batch member -- never waits for a CU
+// to drain) and the fork / join events of gpk_potrf_aug; created on first use.
+struct SideStream {
+  hipStream_t panel_s = nullptr, bulk_s = nullptr;
+  hipEvent_t fork = nullptr, panel = nullptr, bulk = nullptr, join_p = nullptr, join_b = nullptr;
+};
+
+SideStream* side_stream() {
+  thread_local std::vector<SideStream> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
+  if ((int)cache.size() <= dev) cache.resize(dev + 1);
+  SideStream& ss = cache[dev];
+  if (!ss.panel_s) {
+    int least = 0, greatest = 0, ncu = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithPriority(&ss.panel_s, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
+    const int64_t r = std::max<int64_t>(0, std::min<int64_t>(tune().reserve_cus, ncu / 2));
+    if (r > 0) {
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int c = (int)r; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
+      if (hipExtStreamCreateWithCUMask(&ss.bulk_s, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+        return nullptr;
+    } else if (hipStreamCreateWithFlags(&ss.bulk_s, hipStreamNonBlocking) != hipSuccess) {
+      return nullptr;
+    }
+    for (hipEvent_t* e : {&ss.fork, &ss.panel, &ss.bulk, &ss.join_p, &ss.join_b})
+      if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  }
+  return &ss;
 }
 
 }  // namespace
@@ -224,6 +264,20 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
   const size_t es = elem_size(dt);
   const int64_t nblk = lay->n_pad / NB;
 
+  const Tune& tn = tune();
+  // The panel chain (diag, panel solve, thin and look-ahead updates) runs on a high-priority
+  // stream, the bulk of each trailing update on a CU-masked stream concurrently with the next
+  // panel pair's chain; both fork from and join back into the caller's stream.
+  // GPK_LOOKAHEAD=0 puts everything on the caller's stream.
+  const bool la = tn.lookahead != 0;
+  SideStream* ss = nullptr;
+  if (la) {
+    ss = side_stream();
+    if (!ss) return fail_hip(hipErrorInvalidValue, "side stream");
+  }
+  hipStream_t sp = la ? ss->panel_s : s;
+  hipStream_t sb = la ? ss->bulk_s : s;
+
   // diagonal block k: factor + invert
   auto diag = [&](int64_t k) -> hipError_t {
     DiagArgs da;
@@ -235,9 +289,9 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
     da.j0 = k * NB;
     da.kblk = k;
     da.info = info_dev;
-    da.dbg = (int32_t)tune().diag_dbg;
-    return timed(1, (double)lay->batch * NB * NB * NB / 3.0, 0.0, s,
-                 [&] { return launch_diag(da, dt, lay->batch, s); });
+    da.dbg = (int32_t)tn.diag_dbg;
+    return timed(1, (double)lay->batch * NB * NB * NB / 3.0, 0.0, sp,
+                 [&] { return launch_diag(da, dt, lay->batch, sp); });
   };
   GemmArgs base;
   memset(&base, 0, sizeof(base));
@@ -253,16 +307,16 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
     ga.row0 = ga.j0 + NB;
     const int64_t rows = lay->p - ga.row0;
     if (rows <= 0) return hipSuccess;
-    const int tile = (rows / NB * lay->batch >= tune().trsm_t128_min) ? 128 : 64;
+    const int tile = (rows / NB * lay->batch >= tn.trsm_t128_min) ? 128 : 64;
     ga.nt = (int32_t)(rows / tile);
     ga.kdepth = NB;
     const double rK = (double)(lay->n_pad - ga.row0);  // algorithmic: K-part rows x nb^2
-    return timed(2, (double)lay->batch * rK * NB * NB, 0.0, s,
-                 [&] { return launch_gemm(ga, dt, GEMM_TRSM, tile, lay->batch, s); });
+    return timed(2, (double)lay->batch * rK * NB * NB, 0.0, sp,
+                 [&] { return launch_gemm(ga, dt, GEMM_TRSM, tile, lay->batch, sp); });
   };
-  // trailing update from panel columns [j0, j0 + kdepth): rows/cols >= row0 = j0 + kdepth;
-  // ncols128 > 0 restricts the update to that many 128-column blocks (thin update)
-  auto update = [&](int64_t j0, int kdepth, int64_t ncols128) -> hipError_t {
+  // trailing update from panel columns [j0, j0 + kdepth) of the lower tiles whose 128-column
+  // block lies in [c_lo, c_hi) (relative to row0 = j0 + kdepth; c_hi < 0: to the end)
+  auto update = [&](int64_t j0, int kdepth, int64_t c_lo, int64_t c_hi, hipStream_t st) -> hipError_t {
     GemmArgs ga = base;
     ga.j0 = j0;
     ga.row0 = j0 + kdepth;
@@ -270,35 +324,65 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
     const int64_t rows = lay->p - ga.row0;
     if (rows <= 0) return hipSuccess;
     const int64_t t128 = rows / NB;
-    const int64_t w128 = ncols128 > 0 ? ncols128 : t128;
-    const int64_t tiles128 = w128 * (w128 + 1) / 2 + (t128 - w128) * w128;
-    const int tile = (tiles128 * lay->batch >= tune().upd_t128_min) ? 128 : 64;
+    if (c_hi < 0 || c_hi > t128) c_hi = t128;
+    if (c_lo >= c_hi) return hipSuccess;
+    const int64_t w128 = c_hi - c_lo;
+    const int64_t tiles128 = w128 * (w128 + 1) / 2 + (t128 - c_hi) * w128;
+    const int tile = (tiles128 * lay->batch >= tn.upd_t128_min) ? 128 : 64;
     const int64_t scale = NB / tile;
     ga.nt = (int32_t)(rows / tile);
-    ga.c_lo = 0;
-    ga.c_hi = (int32_t)(w128 * scale);
-    // algorithmic flops: 2 * kdepth * (lower-triangular elements of the K part updated)
+    ga.c_lo = (int32_t)(c_lo * scale);
+    ga.c_hi = (int32_t)(c_hi * scale);
+    // algorithmic flops: 2 kdepth x (lower-triangle elements of the K part in the column range)
     const double rK = (double)(lay->n_pad - ga.row0);
-    const double wK = ncols128 > 0 ? (double)(ncols128 * NB) : rK;
-    const double elems = rK > 0 ? (wK * (wK + 1.0) / 2.0 + (rK - wK) * wK) : 0.0;
-    return timed(3, (double)lay->batch * 2.0 * kdepth * elems, 0.0, s,
-                 [&] { return launch_gemm(ga, dt, GEMM_UPDATE, tile, lay->batch, s); });
+    const double cl = std::min(rK, (double)(c_lo * NB)), ch = std::min(rK, (double)(c_hi * NB));
+    const double elems = (ch - cl) * rK - (cl + ch - 1.0) * (ch - cl) / 2.0;
+    // algorithmic bytes: the updated tiles' elements read + written once (y / test rows too)
+    // and the panel rows read once
+    const double rA = (double)rows;
+    const double ca = (double)(c_lo * NB), cb = (double)(c_hi * NB);
+    const double elems_all = (cb - ca) * rA - (ca + cb - 1.0) * (cb - ca) / 2.0;
+    const double bytes = (double)lay->batch * (double)es * (2.0 * elems_all + rA * kdepth);
+    return timed(3, (double)lay->batch * 2.0 * kdepth * std::max(0.0, elems), bytes, st,
+                 [&] { return launch_gemm(ga, dt, GEMM_UPDATE, tile, lay->batch, st); });
   };
 
   // Two 128-column panels per trailing update (K = 256): factor panel k, apply it to the next
-  // block column only, factor panel k+1, then update the rest of the trailing matrix with both
-  // panels at once.  Halves the read-modify-write passes over the trailing matrix.
+  // block column only (thin), factor panel k+1, then update the trailing matrix with both panels
+  // at once -- its first two block columns (look-ahead, on the panel stream: the next pair's
+  // panels) and the rest (bulk stream, overlapping the next pair's panel chain).
+  if (la) {
+    GPK_HIP(hipEventRecord(ss->fork, s), "event");
+    GPK_HIP(hipStreamWaitEvent(sp, ss->fork, 0), "event");
+    GPK_HIP(hipStreamWaitEvent(sb, ss->fork, 0), "event");
+  }
+  bool bulk_pending = false;
   for (int64_t k = 0; k < nblk; k += 2) {
     GPK_HIP(diag(k), "diag");
     GPK_HIP(trsm(k), "trsm");
+    const int kd = (k + 1 < nblk) ? 2 * NB : NB;
     if (k + 1 < nblk) {
-      GPK_HIP(update(k * NB, NB, 1), "update thin");
+      GPK_HIP(update(k * NB, NB, 0, 1, sp), "update thin");
       GPK_HIP(diag(k + 1), "diag");
       GPK_HIP(trsm(k + 1), "trsm");
-      GPK_HIP(update(k * NB, 2 * NB, 0), "update");
-    } else {
-      GPK_HIP(update(k * NB, NB, 0), "update");
     }
+    if (!la) {
+      GPK_HIP(update(k * NB, kd, 0, -1, s), "update");
+      continue;
+    }
+    GPK_HIP(hipEventRecord(ss->panel, sp), "event");      // panels k, k+1 solved
+    if (bulk_pending) GPK_HIP(hipStreamWaitEvent(sp, ss->bulk, 0), "event");
+    GPK_HIP(update(k * NB, kd, 0, 2, sp), "update look-ahead");
+    GPK_HIP(hipStreamWaitEvent(sb, ss->panel, 0), "event");
+    GPK_HIP(update(k * NB, kd, 2, -1, sb), "update bulk");
+    GPK_HIP(hipEventRecord(ss->bulk, sb), "event");
+    bulk_pending = true;
+  }
+  if (la) {
+    GPK_HIP(hipEventRecord(ss->join_p, sp), "event");
+    GPK_HIP(hipEventRecord(ss->join_b, sb), "event");
+    GPK_HIP(hipStreamWaitEvent(s, ss->join_p, 0), "event");
+    GPK_HIP(hipStreamWaitEvent(s, ss->join_b, 0), "event");
   }
   return 0;
 }
@@ -412,6 +496,21 @@ int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, 
 int gpk_timing_enable(int on) {
   std::lock_guard<std::mutex> lk(g_timing.mu);
   g_timing.on = on != 0;
+  return 0;
+}
+
+int gpk_tune(const char* key, int64_t value, int64_t* old) {
+  if (!key) return fail_arg(1, "key");
+  Tune& t = tune();
+  int64_t* slot = nullptr;
+  if (!strcmp(key, "lookahead")) slot = &t.lookahead;
+  else if (!strcmp(key, "reserve_cus")) slot = &t.reserve_cus;
+  else if (!strcmp(key, "upd_t128_min")) slot = &t.upd_t128_min;
+  else if (!strcmp(key, "trsm_t128_min")) slot = &t.trsm_t128_min;
+  else if (!strcmp(key, "diag_debug")) slot = &t.diag_dbg;
+  if (!slot) return fail_arg(1, "key (unknown tuning knob)");
+  if (old) *old = *slot;
+  *slot = value;
   return 0;
 }
 

@@ -43,12 +43,9 @@ struct Mfma<float> {
   static __device__ __forceinline__ int row(int lane, int reg) { return 4 * (lane >> 4) + reg; }
 };
 
-#ifndef GPK_SCHED_FENCE
-#define GPK_SCHED_FENCE 0  // fence the staging loads ahead of the MFMA block (A/B knob)
-#endif
+typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int GBK = 16;   // K depth staged per LDS buffer
-constexpr int SLD = 18;   // LDS row stride (elements): 16 rows at one k, and k+1, on distinct banks
+constexpr int ROWB = 128;  // bytes of one row of a staged K chunk (8 pieces of 16 B)
 
 // bijective XCD-aware remap: consecutive logical tiles land on one XCD (blockIdx % 8 group)
 __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk) {
@@ -58,18 +55,37 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk) {
   return base + pos;
 }
 
-// One 256-thread workgroup computes a TM x TN tile: acc = A_rows(TM x 128) * B_rows(TN x 128)^T
-// over the 128-wide panel.  Waves 2 x 2, each (TM/2) x (TN/2) = MB x NBK blocks of 16 x 16.
+// LDS image of a staged K chunk: one 128-B row per operand row, 16-B piece c of row r stored at
+// piece c ^ ((r >> 1) & 7).  The 16 rows a quarter-wave ds_read_b128 touches then fill all 16
+// slots of a 256-B bank row (conflict-free), while every global_load_lds wave-instruction still
+// writes its 1 KiB lane-linearly (8 rows): the swizzle is applied to the per-lane SOURCE address.
+__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// 16 B per lane global -> LDS (wave-uniform LDS base + 16 lane).  The gfx950 builtins sit in
+// __device__ helpers so that the host pass still emits the kernels' launch stubs.
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_base, 16, 0, 0);
+}
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// One 256-thread workgroup computes a TM x TN tile: acc = A_rows(TM x K) * B_rows(TN x K)^T,
+// K = the panel depth.  Waves 2 x 2, each (TM/2) x (TN/2) = MB x NBK blocks of 16 x 16.
+// Staging: global_load_lds (16 B per lane, no VGPR round trip) into two LDS stages; the chunk
+// kc+1 load is issued before chunk kc's fragment reads and MFMAs and retired by the barrier that
+// ends chunk kc.  K is permuted identically for both operands so that one ds_read_b128 yields
+// the operands of EPC consecutive MFMA k-steps: in k-step s, lane group q = lane >> 4 uses
+// logical piece q + 4 (s / EPC), element s % EPC.
 template <typename T, int MODE, int TM, int TN>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
-  constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B chunk
-  constexpr int CPR = GBK / EPC;             // chunks per row and K chunk
-  constexpr int NCA = TM * CPR / 256;        // A chunks per thread
-  constexpr int NCB = TN * CPR / 256;        // B chunks per thread
+  constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B piece
+  constexpr int GBK = ROWB / (int)sizeof(T); // K depth per stage (16 f64, 32 f32)
+  constexpr int KS = GBK / 4;                // MFMA k-steps per stage
   constexpr int MB = TM / 32, NBK = TN / 32; // 16 x 16 blocks per wave
+  constexpr int STAGE = (TM + TN) * ROWB;    // bytes per stage
+  constexpr int PW = (TM + TN) / 32;         // glds wave-instructions (8 rows each) per wave
   typedef typename Mfma<T>::acc_t acc_t;
-  __shared__ __attribute__((aligned(16))) T sA[2][TM * SLD];
-  __shared__ __attribute__((aligned(16))) T sB[2][TN * SLD];
+  typedef T vec_t __attribute__((ext_vector_type(EPC)));
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   const int b = blockIdx.y;
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
@@ -107,45 +123,24 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wid = tid >> 6;
+  const int wid = wave_uniform(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
 
-  uint4 ra[NCA], rb[NCB];
-  const T* pga[NCA];
-  const T* pgb[NCB];
-  int la[NCA], lb[NCB];
+  // per-lane source of each of this wave's glds instructions: rows [0, TM) are A, [TM, TM+TN) B
+  const T* src[PW];
 #pragma unroll
-  for (int u = 0; u < NCA; ++u) {
-    const int q = tid + 256 * u;
-    pga[u] = Ag + (int64_t)(q / CPR) * a.ld + (q % CPR) * EPC;
-    la[u] = (q / CPR) * SLD + (q % CPR) * EPC;
+  for (int i = 0; i < PW; ++i) {
+    const int g0 = (wid * PW + i) * 8;
+    const int r = g0 + (lane >> 3);
+    if (g0 < TM)
+      src[i] = Ag + (int64_t)r * a.ld + swz(r, lane & 7) * EPC;
+    else
+      src[i] = Bg + (int64_t)(r - TM) * ldb + swz(r - TM, lane & 7) * EPC;
   }
-#pragma unroll
-  for (int u = 0; u < NCB; ++u) {
-    const int q = tid + 256 * u;
-    pgb[u] = Bg + (int64_t)(q / CPR) * ldb + (q % CPR) * EPC;
-    lb[u] = (q / CPR) * SLD + (q % CPR) * EPC;
-  }
-#define GPK_GLOAD(kc)                                                                     \
-  {                                                                                       \
-    _Pragma("unroll") for (int u = 0; u < NCA; ++u) ra[u] =                               \
-        *reinterpret_cast<const uint4*>(pga[u] + (kc) * GBK);                             \
-    _Pragma("unroll") for (int u = 0; u < NCB; ++u) rb[u] =                               \
-        *reinterpret_cast<const uint4*>(pgb[u] + (kc) * GBK);                             \
-  }
-#define GPK_STORE16(dst, v)                                                               \
-  {                                                                                       \
-    if (sizeof(T) == 8) {                                                                 \
-      *reinterpret_cast<uint4*>(dst) = (v);                                               \
-    } else {                                                                              \
-      reinterpret_cast<uint2*>(dst)[0] = make_uint2((v).x, (v).y);                        \
-      reinterpret_cast<uint2*>(dst)[1] = make_uint2((v).z, (v).w);                        \
-    }                                                                                     \
-  }
-#define GPK_LSTORE(buf)                                                                   \
-  {                                                                                       \
-    _Pragma("unroll") for (int u = 0; u < NCA; ++u) GPK_STORE16(&sA[buf][la[u]], ra[u]);  \
-    _Pragma("unroll") for (int u = 0; u < NCB; ++u) GPK_STORE16(&sB[buf][lb[u]], rb[u]);  \
+#define GPK_GLDS(stage, kc)                                                                   \
+  {                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < PW; ++i)                                            \
+        glds16(src[i] + (int64_t)(kc) * GBK, smem + (stage) * STAGE + (wid * PW + i) * 1024);   \
   }
 
   acc_t acc[MB][NBK];
@@ -154,74 +149,72 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int n = 0; n < NBK; ++n) acc[m][n] = acc_t{0, 0, 0, 0};
 
+  const int q = lane >> 4, lr = lane & 15;
+  const int aoff = (wr * (TM / 2) + lr) * ROWB;
+  const int boff = (TM + wc * (TN / 2) + lr) * ROWB;
+  const int p0 = swz(lr, q) * 16, p1 = swz(lr, q + 4) * 16;
+
   const int NK = (MODE == GEMM_TRSM) ? NB / GBK : a.kdepth / GBK;
-  GPK_GLOAD(0);
-  GPK_LSTORE(0);
-  __syncthreads();
-  const int arow = (wr * (TM / 2) + (lane & 15)) * SLD + (lane >> 4);
-  const int brow = (wc * (TN / 2) + (lane & 15)) * SLD + (lane >> 4);
-  // Fragments are software-pipelined one 4-deep k-step ahead (two register sets), and the next
-  // chunk's first fragments are read right after the barrier, under the last step's MFMAs.
-  T fa0[MB], fb0[NBK], fa1[MB], fb1[NBK];
-#define GPK_FRAG(FA, FB, P, Q, S)                                                          \
-  {                                                                                        \
-    _Pragma("unroll") for (int m = 0; m < MB; ++m) FA[m] = (P)[arow + m * 16 * SLD + (S) * 4]; \
-    _Pragma("unroll") for (int n = 0; n < NBK; ++n) FB[n] = (Q)[brow + n * 16 * SLD + (S) * 4]; \
-  }
-  // TRSM against the lower-triangular inverse: K chunk KC feeds output columns >= 16 KC only
-#define GPK_MMA(FA, FB, KC)                                                                \
-  {                                                                                        \
-    _Pragma("unroll") for (int n = 0; n < NBK; ++n) {                                      \
-      if (MODE == GEMM_TRSM && (KC) > (wc * (TN / 2) + n * 16) / GBK) continue;            \
-      _Pragma("unroll") for (int m = 0; m < MB; ++m) acc[m][n] = Mfma<T>::op(FA[m], FB[n], acc[m][n]); \
-    }                                                                                      \
-  }
-  GPK_FRAG(fa0, fb0, sA[0], sB[0], 0);
+  GPK_GLDS(0, 0);
   for (int kc = 0; kc < NK; ++kc) {
-    const int buf = kc & 1;
-    // branch-free staging (the last iteration re-stages its own chunk into the idle buffer):
-    // a conditional load/store pair makes hipcc spill the staging registers to scratch
-    const int knext = (kc + 1 < NK) ? kc + 1 : kc;
-    GPK_GLOAD(knext);
-    // keep the next chunk's loads in flight under this chunk's MFMAs: without the fence hipcc
-    // sinks every load to its ds_write and serialises them (load, vmcnt(0), write, load, ...)
-    if (GPK_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
-    const T* pa = sA[buf];
-    const T* pb = sB[buf];
-    GPK_FRAG(fa1, fb1, pa, pb, 1);
-    GPK_MMA(fa0, fb0, kc);
-    GPK_FRAG(fa0, fb0, pa, pb, 2);
-    GPK_MMA(fa1, fb1, kc);
-    GPK_FRAG(fa1, fb1, pa, pb, 3);
-    GPK_MMA(fa0, fb0, kc);
-    if (GPK_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
-    GPK_LSTORE(buf ^ 1);
+    const int st = kc & 1;
+    // one barrier per chunk, at the top: it retires the chunk kc glds (vmcnt(0), issued a whole
+    // MFMA phase earlier) and frees stage st ^ 1, read during chunk kc - 1.  (At the bottom
+    // hipcc hoists it above the MFMAs, exposing the load latency.)
     __syncthreads();
-    GPK_FRAG(fa0, fb0, sA[buf ^ 1], sB[buf ^ 1], 0);
-    GPK_MMA(fa1, fb1, kc);
+    if (kc + 1 < NK) GPK_GLDS(st ^ 1, kc + 1);
+    const char* sb = smem + st * STAGE;
+    vec_t fa[MB][2], fb[NBK][2];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      fa[m][0] = *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + p0);
+      fa[m][1] = *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + p1);
+    }
+#pragma unroll
+    for (int n = 0; n < NBK; ++n) {
+      fb[n][0] = *reinterpret_cast<const vec_t*>(sb + boff + n * 16 * ROWB + p0);
+      fb[n][1] = *reinterpret_cast<const vec_t*>(sb + boff + n * 16 * ROWB + p1);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int n = 0; n < NBK; ++n) {
+        // TRSM against the lower-triangular inverse: K chunk kc feeds output columns >= kc GBK only
+        if (MODE == GEMM_TRSM && kc * GBK > wc * (TN / 2) + n * 16 + 15) continue;
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+          acc[m][n] = Mfma<T>::op(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]);
+      }
   }
-#undef GPK_FRAG
-#undef GPK_MMA
-#undef GPK_GLOAD
-#undef GPK_STORE16
-#undef GPK_LSTORE
+#undef GPK_GLDS
 
   const int col = lane & 15;
   T* C = (MODE == GEMM_UPDATE) ? W + R * a.ld + a.row0 + tj * TN : W + R * a.ld + a.j0;
+  T* cp[MB][NBK];
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < NBK; ++n)
+      cp[m][n] = C + (int64_t)(wr * (TM / 2) + m * 16 + Mfma<T>::row(lane, 0)) * a.ld +
+                 wc * (TN / 2) + n * 16 + col;
+  // rows of the C/D layout: row(lane, r) = row(lane, 0) + r * RSTEP
+  constexpr int RSTEP = sizeof(T) == 8 ? 4 : 1;
+  if (MODE == GEMM_UPDATE) {
+    // every C value is loaded before the first store: interleaved load/store pairs may alias,
+    // so hipcc would wait for each load in turn (64 dependent HBM round trips per tile)
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int n = 0; n < NBK; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[m][n][r] = cp[m][n][(int64_t)r * RSTEP * a.ld] - acc[m][n][r];
+  }
 #pragma unroll
   for (int m = 0; m < MB; ++m)
 #pragma unroll
     for (int n = 0; n < NBK; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rr = wr * (TM / 2) + m * 16 + Mfma<T>::row(lane, r);
-        const int cc = wc * (TN / 2) + n * 16 + col;
-        T* p = C + (int64_t)rr * a.ld + cc;
-        if (MODE == GEMM_UPDATE)
-          *p = *p - acc[m][n][r];
-        else
-          *p = acc[m][n][r];
-      }
+      for (int r = 0; r < 4; ++r) cp[m][n][(int64_t)r * RSTEP * a.ld] = acc[m][n][r];
 }
 
 // ================================================================================ read-out
