@@ -135,12 +135,42 @@ struct SideStream {
   hipEvent_t fork = nullptr, panel = nullptr, bulk = nullptr, join_p = nullptr, join_b = nullptr;
 };
 
+// Every side stream ever created, destroyed by an atexit handler: registered after the HIP
+// runtime's own start-up, it runs before the runtime tears down, and a CU-masked queue still
+// alive at that point crashes rocprofv3's finalisation.
+std::mutex g_side_mu;
+std::vector<SideStream*> g_side_all;
+
+void release_side_streams() {
+  std::lock_guard<std::mutex> lk(g_side_mu);
+  for (SideStream* ss : g_side_all) {
+    if (ss->panel_s) hipStreamSynchronize(ss->panel_s);
+    if (ss->bulk_s) hipStreamSynchronize(ss->bulk_s);
+    for (hipEvent_t e : {ss->fork, ss->panel, ss->bulk, ss->join_p, ss->join_b})
+      if (e) hipEventDestroy(e);
+    if (ss->panel_s) hipStreamDestroy(ss->panel_s);
+    if (ss->bulk_s) hipStreamDestroy(ss->bulk_s);
+    *ss = SideStream();
+  }
+  g_side_all.clear();
+}
+
 SideStream* side_stream() {
-  thread_local std::vector<SideStream> cache;
+  thread_local std::vector<SideStream*> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
-  if ((int)cache.size() <= dev) cache.resize(dev + 1);
-  SideStream& ss = cache[dev];
+  if ((int)cache.size() <= dev) cache.resize(dev + 1, nullptr);
+  if (!cache[dev]) {
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    static bool registered = false;
+    if (!registered) {
+      std::atexit(release_side_streams);
+      registered = true;
+    }
+    cache[dev] = new SideStream();  // owned by g_side_all (released at exit)
+    g_side_all.push_back(cache[dev]);
+  }
+  SideStream& ss = *cache[dev];
   if (!ss.panel_s) {
     int least = 0, greatest = 0, ncu = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
