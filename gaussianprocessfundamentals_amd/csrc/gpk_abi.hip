@@ -112,6 +112,7 @@ struct Tune {
   int64_t diag_dbg;       // timing-only ablation flags of the diagonal kernel (never set in production)
   int64_t lookahead;      // 1: panel chain on a high-priority side stream (default), 0: one stream
   int64_t reserve_cus;    // CUs kept free of the bulk trailing update for the panel chain
+  int64_t group;          // panels per trailing update (K = 128 group)
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -122,7 +123,7 @@ int64_t env_i64(const char* name, int64_t dflt) {
 Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
-                         env_i64("GPK_RESERVE_CUS", 8)};
+                         env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 4)};
   return t;
 }
 
@@ -377,34 +378,36 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
                  [&] { return launch_gemm(ga, dt, GEMM_UPDATE, tile, lay->batch, st); });
   };
 
-  // Two 128-column panels per trailing update (K = 256): factor panel k, apply it to the next
-  // block column only (thin), factor panel k+1, then update the trailing matrix with both panels
-  // at once -- its first two block columns (look-ahead, on the panel stream: the next pair's
-  // panels) and the rest (bulk stream, overlapping the next pair's panel chain).
+  // Groups of G 128-column panels per trailing update (K = 128 G): factor panel k of the group and
+  // apply it to the group's remaining block columns only (thin), ..., then update the trailing
+  // matrix with all G panels at once -- its first G block columns (look-ahead, on the panel
+  // stream: the next group's panels) and the rest (bulk stream, overlapping the next group's
+  // panel chain).  A deeper K halves the read-modify-write passes over the trailing matrix per
+  // doubling of G.
+  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tn.group, 8));
   if (la) {
     GPK_HIP(hipEventRecord(ss->fork, s), "event");
     GPK_HIP(hipStreamWaitEvent(sp, ss->fork, 0), "event");
     GPK_HIP(hipStreamWaitEvent(sb, ss->fork, 0), "event");
   }
   bool bulk_pending = false;
-  for (int64_t k = 0; k < nblk; k += 2) {
-    GPK_HIP(diag(k), "diag");
-    GPK_HIP(trsm(k), "trsm");
-    const int kd = (k + 1 < nblk) ? 2 * NB : NB;
-    if (k + 1 < nblk) {
-      GPK_HIP(update(k * NB, NB, 0, 1, sp), "update thin");
-      GPK_HIP(diag(k + 1), "diag");
-      GPK_HIP(trsm(k + 1), "trsm");
+  for (int64_t g0 = 0; g0 < nblk; g0 += G) {
+    const int64_t gend = std::min(g0 + G, nblk);
+    for (int64_t k = g0; k < gend; ++k) {
+      GPK_HIP(diag(k), "diag");
+      GPK_HIP(trsm(k), "trsm");
+      if (k + 1 < gend) GPK_HIP(update(k * NB, NB, 0, gend - k - 1, sp), "update thin");
     }
+    const int kd = (int)((gend - g0) * NB);
     if (!la) {
-      GPK_HIP(update(k * NB, kd, 0, -1, s), "update");
+      GPK_HIP(update(g0 * NB, kd, 0, -1, s), "update");
       continue;
     }
-    GPK_HIP(hipEventRecord(ss->panel, sp), "event");      // panels k, k+1 solved
+    GPK_HIP(hipEventRecord(ss->panel, sp), "event");      // panels g0 .. gend-1 solved
     if (bulk_pending) GPK_HIP(hipStreamWaitEvent(sp, ss->bulk, 0), "event");
-    GPK_HIP(update(k * NB, kd, 0, 2, sp), "update look-ahead");
+    GPK_HIP(update(g0 * NB, kd, 0, G, sp), "update look-ahead");
     GPK_HIP(hipStreamWaitEvent(sb, ss->panel, 0), "event");
-    GPK_HIP(update(k * NB, kd, 2, -1, sb), "update bulk");
+    GPK_HIP(update(g0 * NB, kd, G, -1, sb), "update bulk");
     GPK_HIP(hipEventRecord(ss->bulk, sb), "event");
     bulk_pending = true;
   }
@@ -538,6 +541,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "upd_t128_min")) slot = &t.upd_t128_min;
   else if (!strcmp(key, "trsm_t128_min")) slot = &t.trsm_t128_min;
   else if (!strcmp(key, "diag_debug")) slot = &t.diag_dbg;
+  else if (!strcmp(key, "group")) slot = &t.group;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -154,7 +154,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
   const int boff = (TM + wc * (TN / 2) + lr) * ROWB;
   const int p0 = swz(lr, q) * 16, p1 = swz(lr, q + 4) * 16;
 
-  const int NK = (MODE == GEMM_TRSM) ? NB / GBK : a.kdepth / GBK;
+#ifndef GPK_ABLATE
+#define GPK_ABLATE 0  // timing-only ablations (wrong results): 1 no C read, 2 no epilogue, 3 K loop x2
+#endif
+  const int NK0 = (MODE == GEMM_TRSM) ? NB / GBK : a.kdepth / GBK;
+  const int NK = (GPK_ABLATE == 3 && MODE == GEMM_UPDATE) ? 2 * NK0 : NK0;
   GPK_GLDS(0, 0);
   for (int kc = 0; kc < NK; ++kc) {
     const int st = kc & 1;
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
     // MFMA phase earlier) and frees stage st ^ 1, read during chunk kc - 1.  (At the bottom
     // hipcc hoists it above the MFMAs, exposing the load latency.)
     __syncthreads();
-    if (kc + 1 < NK) GPK_GLDS(st ^ 1, kc + 1);
+    if (kc + 1 < NK) GPK_GLDS(st ^ 1, (kc + 1) % NK0);
     const char* sb = smem + st * STAGE;
     vec_t fa[MB][2], fb[NBK][2];
 #pragma unroll
@@ -199,7 +203,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
                  wc * (TN / 2) + n * 16 + col;
   // rows of the C/D layout: row(lane, r) = row(lane, 0) + r * RSTEP
   constexpr int RSTEP = sizeof(T) == 8 ? 4 : 1;
-  if (MODE == GEMM_UPDATE) {
+  if (GPK_ABLATE == 2 && acc[0][0][0] != (T)12345.678) return;
+  if (MODE == GEMM_UPDATE && GPK_ABLATE != 1) {
     // every C value is loaded before the first store: interleaved load/store pairs may alias,
     // so hipcc would wait for each load in turn (64 dependent HBM round trips per tile)
 #pragma unroll

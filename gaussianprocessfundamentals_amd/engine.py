@@ -133,6 +133,19 @@ def kernel_matrix(kernel, hyper_parameter, x, x_, diag_add: float = 0.0, lower: 
 
 
 # ----------------------------------------------------------------------------- factorisation
+def _check_operand(name: str, t: torch.Tensor, bstride: int, per_member: int, batch: int,
+                   dev: torch.device) -> None:
+    if t is None:
+        raise ValueError("%s is required" % name)
+    if t.dtype != torch.float64 or not t.is_contiguous() or t.device != dev:
+        raise ValueError("%s must be a contiguous float64 tensor on %s (got %s, %s, contiguous=%s)"
+                         % (name, dev, t.dtype, t.device, t.is_contiguous()))
+    need = (batch - 1) * int(bstride) + int(per_member) if batch > 0 else 0
+    if int(bstride) < 0 or t.numel() < need:
+        raise ValueError("%s holds %d elements, the layout reads %d (batch %d, stride %d, %d per member)"
+                         % (name, t.numel(), need, batch, bstride, per_member))
+
+
 class AugmentedFactorization:
     """One factorisation of the augmented matrix W (include/gpk.h) for ``batch`` problems.
 
@@ -166,6 +179,20 @@ class AugmentedFactorization:
             Xs: Optional[torch.Tensor] = None, xs_bstride: int = 0,
             E: Optional[torch.Tensor] = None, e_bstride: int = 0):
         lay = self.layout
+        B, n, m, d = self.batch, self.n, self.m, self.d
+        # the device reads these extents blindly: check them here (an undersized operand would
+        # be read out of bounds, not reported)
+        _check_operand("hyper_parameter", hyp, hyp_stride, kd.n_hyp, B, self.W.device)
+        _check_operand("noise", noise, noise_stride, 1, B, self.W.device)
+        _check_operand("X", X, x_bstride, n * d, B, self.W.device)
+        _check_operand("y", y, y_bstride, n, B, self.W.device)
+        if m:
+            if E is not None:
+                _check_operand("E", E, e_bstride, m * n, B, self.W.device)
+            elif Xs is not None:
+                _check_operand("X_test", Xs, xs_bstride, m * d, B, self.W.device)
+            else:
+                raise ValueError("m = %d extra rows need X_test or E" % m)
         s = nat.stream_handle(self.W.device)
         L = self.L
         self.info.zero_()
