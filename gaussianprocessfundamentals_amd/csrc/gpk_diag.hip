@@ -4,8 +4,8 @@
 // The block is handled as 8 x 8 tiles of 16 x 16, every tile operation an f64 MFMA chain
 // (v_mfma_f64_16x16x4_f64, 4 MFMAs per 16-deep product):
 //   for kb = 0..7:
-//     wave 0   : potf2 of tile (kb, kb) in registers (lane r owns row r, pivots broadcast
-//                with v_readlane) and its inverse Dinv_kb
+//     wave 0   : potf2 of tile (kb, kb) in registers (lane r owns row r, columns broadcast
+//                through LDS) and its inverse Dinv_kb
 //     waves    : panel tiles  X_i = A_{i,kb} Dinv_kb^T                  (i > kb)
 //     waves    : trailing     A_{i,j} -= X_i X_j^T                      (kb < j <= i)
 //   inverse by block rows (I = 0..7), one wave per tile column J < I:
@@ -27,13 +27,8 @@ constexpr int LDA = NB + 2;       // LDS row stride (doubles): 16 rows of one co
 constexpr int DT = 512;           // threads (8 waves)
 constexpr int LDS_A = NB * LDA;
 constexpr int LDS_DINV = NTL * DB * DB;
-constexpr size_t DIAG_LDS_BYTES = sizeof(double) * (LDS_A + LDS_DINV) + 16;
-
-__device__ __forceinline__ double rdlane(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
+constexpr int LDS_COL = 2 * DB;  // potf2 column broadcast, double-buffered
+constexpr size_t DIAG_LDS_BYTES = sizeof(double) * (LDS_A + LDS_DINV + LDS_COL) + 16;
 
 // 1/sqrt(x) from the hardware estimate plus two Newton steps (~1 ulp); NaN for x < 0.
 __device__ __forceinline__ double rsqrt_refined(double x) {
@@ -48,38 +43,62 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// potf2 + inverse of tile (kb, kb), one wave.  Lanes 16..63 mirror lanes 0..15 and never store.
-__device__ __forceinline__ void potf2_tile(double* A, double* Dk, int kb, int lane, int* flag,
-                                           int64_t col_base) {
+// potf2 + inverse of tile (kb, kb), one wave.  Lanes 0..15 hold row r = lane of the tile and
+// factor it (right-looking); lanes 16..31 hold column r = lane - 16 of the identity and turn it
+// into column r of L^-1 (column-oriented forward substitution).  Both run the SAME update per
+// pivot j with w = their 16 values:   a = w[j] / L[j][j];  w[j] = a;  w[c] -= a L[c][j] (c > j)
+// (for a row of A, a = L[r][j]; for a column of the inverse, a = (L^-1)[j][r]).  Column j of L is
+// broadcast through LDS: written by lanes 0..15, read back by every lane with 8 broadcast
+// ds_read_b128.  Lanes 32..63 mirror 0..31 and never store.  (The earlier form -- one readlane
+// per element and a separate substitution -- took 2 x 480 readlanes and spilled SGPRs.)
+__device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf, int kb, int lane,
+                                           int* flag, int64_t col_base) {
+  typedef double dbl2 __attribute__((ext_vector_type(2)));
   const int r = lane & 15;
+  const bool inv = (lane & 16) != 0;
   const int c0 = kb * DB;
-  double v[DB], rinv[DB];
+  // rows: entries above the diagonal are never used (only c <= r is stored, and column j is
+  // read from rows c >= j only), so the tile row is loaded whole
+  double w[DB];
 #pragma unroll
-  for (int c = 0; c < DB; ++c) v[c] = (c <= r) ? A[(c0 + r) * LDA + c0 + c] : 0.0;
+  for (int c = 0; c < DB; c += 2) {
+    const dbl2 t = *reinterpret_cast<const dbl2*>(A + (c0 + r) * LDA + c0 + c);
+    w[c] = inv ? ((c == r) ? 1.0 : 0.0) : t.x;
+    w[c + 1] = inv ? ((c + 1 == r) ? 1.0 : 0.0) : t.y;
+  }
+  int bad = 0;  // first non-positive pivot of this tile (1-based in the tile), wave-uniform
 #pragma unroll
   for (int j = 0; j < DB; ++j) {
-    const double piv = rdlane(v[j], j);
-    if (!(piv > 0.0) && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + j + 1);
-    const double ri = rsqrt_refined(piv);
-    rinv[j] = ri;
-    v[j] = (r == j) ? piv * ri : v[j] * ri;
+    double* cb = colbuf + (j & 1) * DB;
+    if (lane < DB) cb[lane] = w[j];            // column j: entry (r, j) of row r
+    // Other lanes' stores are invisible to the per-thread memory model: without a fence hipcc
+    // may serve the reads below from the loads of step j - 2 (same buffer).  The wave's LDS
+    // operations retire in order, so a wave-scope fence is all the hardware needs.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double u[DB];
 #pragma unroll
-    for (int c = j + 1; c < DB; ++c) v[c] = fma(-v[j], rdlane(v[j], c), v[c]);
+    for (int c = j & ~1; c < DB; c += 2) {
+      const dbl2 t = *reinterpret_cast<const dbl2*>(cb + c);
+      u[c] = t.x;
+      u[c + 1] = t.y;
+    }
+    const double piv = u[j];
+    bad = (bad == 0 && !(piv > 0.0)) ? j + 1 : bad;
+    const double ri = rsqrt_refined(piv);      // 1 / L[j][j]
+    const double aj = w[j] * ri;
+    w[j] = aj;
+#pragma unroll
+    for (int c = j + 1; c < DB; ++c) w[c] = fma(-aj, u[c] * ri, w[c]);
   }
-  // column r of the inverse: forward substitution, rows broadcast lane-uniformly
-  double x[DB];
-#pragma unroll
-  for (int rr = 0; rr < DB; ++rr) {
-    double s = (rr == r) ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = 0; k < rr; ++k) s = fma(-rdlane(v[k], rr), x[k], s);
-    x[rr] = s * rinv[rr];
-  }
+  if (bad != 0 && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + bad);
   if (lane < DB) {
 #pragma unroll
-    for (int c = 0; c < DB; ++c) A[(c0 + r) * LDA + c0 + c] = (c <= r) ? v[c] : 0.0;
+    for (int c = 0; c < DB; ++c) A[(c0 + r) * LDA + c0 + c] = (c <= r) ? w[c] : 0.0;
+  } else if (lane < 2 * DB) {
 #pragma unroll
-    for (int rr = 0; rr < DB; ++rr) Dk[rr * DB + r] = x[rr];  // Dinv[rr][r]
+    for (int rr = 0; rr < DB; ++rr) Dk[rr * DB + r] = w[rr];  // Dinv[rr][r]
   }
 }
 
@@ -88,7 +107,8 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* A = sm;
   double* Dinv = A + LDS_A;
-  int* flag = reinterpret_cast<int*>(Dinv + LDS_DINV);
+  double* colbuf = Dinv + LDS_DINV;
+  int* flag = reinterpret_cast<int*>(colbuf + LDS_COL);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -97,29 +117,36 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
   const int lk = lane >> 4;       // MFMA operand k within a 4-step / C-D row offset
   const int b = blockIdx.x;
   T* Wb = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs + a.j0 * a.ld + a.j0;
-  // 8 loads in flight per thread before the LDS stores (a plain loop serialises load/store)
   constexpr int PER = NB * NB / DT;
+#ifndef GPK_DIAG_LOAD_BATCH
+#define GPK_DIAG_LOAD_BATCH 16
+#endif
+  {
+    // GPK_DIAG_LOAD_BATCH loads in flight per thread before their LDS stores (a plain loop
+    // serialises load / store; all 32 at once costs more registers than the kernel has)
+    constexpr int LB = GPK_DIAG_LOAD_BATCH;
+    const T* src = Wb + (int64_t)(tid >> 7) * a.ld + (tid & (NB - 1));
+    const int64_t step = (int64_t)(DT / NB) * a.ld;  // rows advanced per q
+    const int c = tid & (NB - 1);
 #pragma unroll
-  for (int g = 0; g < PER; g += 8) {
-    double v[8];
+    for (int g = 0; g < PER; g += LB) {
+      double v[LB];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + (g + q) * DT;
-      const int r = e >> 7, c = e & (NB - 1);
-      v[q] = (c <= r) ? (double)Wb[(int64_t)r * a.ld + c] : 0.0;
-    }
+      for (int q = 0; q < LB; ++q) v[q] = (double)src[(g + q) * step];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = tid + (g + q) * DT;
-      A[(e >> 7) * LDA + (e & (NB - 1))] = v[q];
+      for (int q = 0; q < LB; ++q) {
+        const int r = (tid >> 7) + (g + q) * (DT / NB);
+        A[r * LDA + c] = (c <= r) ? v[q] : 0.0;
+      }
     }
   }
   if (tid == 0) *flag = 0;
   __syncthreads();
 
+#pragma unroll 1
   for (int kb = 0; kb < NTL; ++kb) {
     double* Dk = Dinv + kb * DB * DB;
-    if (wave == 0 && !(a.dbg & 2)) potf2_tile(A, Dk, kb, lane, flag, a.j0);
+    if (wave == 0 && !(a.dbg & 2)) potf2_tile(A, Dk, colbuf, kb, lane, flag, a.j0);
     if (a.dbg & 4) continue;
     __syncthreads();
     if (kb == NTL - 1) break;
