@@ -35,6 +35,9 @@ CONFIGS = {
     "metric": ("SE", 1, 8192, 1e-2, "f64", [0.1]),
     "C2": ("SE", 1, 4096, 1e-2, "f64", [0.1]),
     "C3": ("MAT52-ARD", 4, 8192, 1e-1, "f32", [[0.25, 0.5, 0.75, 1.0]]),
+    # C4: the 128-candidate (lengthscale, signal variance) sweep, sharded over the ranks (strong
+    # scaling: one step = the whole sweep, every rank factorises its slice as one batch)
+    "C4": ("SE-SCALED", 1, 4096, 1e-2, "f64", None),
     "C5": ("SE-ARD+PER", 8, 16384, 1e-2, "f64", None),
 }
 
@@ -69,10 +72,17 @@ def pmc_traffic(cfg, batch):
     return rec
 
 
+def c4_candidates():
+    """lengthscale geomspace(0.02, 0.5, 16) x signal variance geomspace(0.25, 4, 8)
+    (the grid of tests/golden/make_golden.py)."""
+    import numpy as np
+    return [[float(a), float(b)] for a in np.geomspace(0.02, 0.5, 16) for b in np.geomspace(0.25, 4.0, 8)]
+
+
 def build_kernel(name, d):
     from gaussianprocessfundamentals_amd.KernelBasics import BaseKernels as bk
     from gaussianprocessfundamentals_amd.KernelBasics import Operators as ops
-    if name == "SE":
+    if name in ("SE", "SE-SCALED"):
         return bk.SquaredExponentialKernel(d)
     if name == "MAT52-ARD":
         return bk.MaternKernel5_2(d, ard=True, standard=True)
@@ -88,25 +98,28 @@ def cpu_baseline(cfg_name, n, budget_s):
     from oracle import gp_oracle as o
     threads = int(os.environ.get("GPK_CPU_THREADS", min(16, os.cpu_count() or 1)))
     kname, d, _, noise, _, hyp = CONFIGS[cfg_name]
-    tree = {"SE": ("SE", {}), "MAT52-ARD": ("MAT52", {"ard": True, "standard": True}),
+    tree = {"SE": ("SE", {}), "SE-SCALED": ("SE", {}), "MAT52-ARD": ("MAT52", {"ard": True, "standard": True}),
             "SE-ARD+PER": ("ADD", [("SE", {"ard": True}), ("PER", {"standard": True})])}[kname]
-    if hyp is None:
+    scaled = kname == "SE-SCALED"
+    if scaled:
+        hyp = list(c4_candidates()[0])  # one candidate of the sweep per evaluation
+    elif hyp is None:
         hyp = [list(np.linspace(0.4, 1.1, d)), 1.0, 0.5]
     x, y = o.make_inputs("metric" if cfg_name == "metric" else cfg_name, n=n)
     # median of >= 5 warm repetitions with the host threads, plus one 1-thread figure
     times = []
     with threadpool_limits(limits=threads):
-        o.nlml(tree, hyp, noise, x, y)  # warm (BLAS pool, page-in)
+        o.nlml(tree, hyp, noise, x, y, scaled=scaled)  # warm (BLAS pool, page-in)
         t_all = time.perf_counter()
         while len(times) < 5 or (time.perf_counter() - t_all < budget_s and len(times) < 9):
             t0 = time.perf_counter()
-            o.nlml(tree, hyp, noise, x, y)
+            o.nlml(tree, hyp, noise, x, y, scaled=scaled)
             times.append(time.perf_counter() - t0)
             if time.perf_counter() - t_all > 3 * budget_s:
                 break
     with threadpool_limits(limits=1):
         t0 = time.perf_counter()
-        o.nlml(tree, hyp, noise, x, y)
+        o.nlml(tree, hyp, noise, x, y, scaled=scaled)
         t1 = time.perf_counter() - t0
     med = sorted(times)[len(times) // 2]
     try:
@@ -140,13 +153,17 @@ def main():
 
     import gaussianprocessfundamentals_amd.global_parameters as gp
     gp.init(0)
+    if CONFIGS[args.config][0] == "SE-SCALED":
+        gp.p_scaled_base_kernel = True  # hyp = [lengthscale, signal variance]
     from gaussianprocessfundamentals_amd import _native as nat
     from gaussianprocessfundamentals_amd import engine
     from oracle import gp_oracle as o  # input generator only (same seeds as the golden vectors)
 
     kname, d, n, noise, dtn, hyp = CONFIGS[args.config]
     n = args.n or n
-    if hyp is None:
+    if kname == "SE-SCALED":
+        hyp = c4_candidates()[0]
+    elif hyp is None:
         hyp = [[0.4 + 0.1 * i for i in range(d)], 1.0, 0.5]
     dt = torch.float64 if dtn == "f64" else torch.float32
     x, y = o.make_inputs("metric" if args.config == "metric" else args.config, n=n)
@@ -158,24 +175,37 @@ def main():
     flat_h = []
     for h in hyp:
         flat_h.extend(h if isinstance(h, list) else [h])
-    batch = args.batch or (DEFAULT_BATCH if args.config == "metric" else 1)
-    # weak scaling: every rank evaluates its own `batch` candidates (a sweep over the first
-    # hyperparameter: candidate c of rank r scales it by 1 + 0.01 (r * batch + c))
-    rows = []
-    for c in range(batch):
-        h = list(flat_h)
-        if not isinstance(hyp[0], list):
-            h[0] = h[0] * (1.0 + 0.01 * (rank * batch + c))
-        rows.append(h)
+    sweep = kname == "SE-SCALED"
+    if sweep:
+        # C4 (strong scaling): the 128 candidates are split contiguously over the ranks
+        from gaussianprocessfundamentals_amd.sweep import shard_range
+        cands = c4_candidates()
+        s0, s1 = shard_range(len(cands), rank, world)
+        rows = cands[s0:s1]
+        batch = len(rows)
+        chunk = -(-len(cands) // world)
+    else:
+        batch = args.batch or (DEFAULT_BATCH if args.config == "metric" else 1)
+        chunk = batch
+        # weak scaling: every rank evaluates its own `batch` candidates (a sweep over the first
+        # hyperparameter: candidate c of rank r scales it by 1 + 0.01 (r * batch + c))
+        rows = []
+        for c in range(batch):
+            h = list(flat_h)
+            if not isinstance(hyp[0], list):
+                h[0] = h[0] * (1.0 + 0.01 * (rank * batch + c))
+            rows.append(h)
     H = torch.tensor(rows, dtype=torch.float64, device=dev).contiguous()
     NZ = torch.tensor([noise], dtype=torch.float64, device=dev)
     fact = engine.AugmentedFactorization(n, d, 0, batch, dt)
-    gathered = torch.empty(2 * batch * world, dtype=torch.float64, device=dev) if world > 1 else None
+    gathered = torch.empty(2 * chunk * world, dtype=torch.float64, device=dev) if world > 1 else None
+    mine = torch.full((2 * chunk,), float("nan"), dtype=torch.float64, device=dev)
 
     def step():
         fact.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
         if world > 1:
-            mine = torch.cat([fact.nlml(), fact.info.to(torch.float64)])
+            mine[:batch] = fact.nlml()
+            mine[chunk:chunk + batch] = fact.info.to(torch.float64)
             dist.all_gather_into_tensor(gathered, mine)
 
     for _ in range(args.warmup):
@@ -221,7 +251,7 @@ def main():
     info = int(fact.info.abs().max().item())
 
     if rank == 0:
-        evals = args.steps * world * batch
+        evals = args.steps * (len(c4_candidates()) if sweep else world * batch)
         value = evals / el
         ms = el / args.steps * 1000.0
         lay = fact.layout
@@ -261,12 +291,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sweep else "weak",
             "vs_baseline": None,
             "dtype": dtn,
             "data": "synthetic (SURVEY §8d generator, numpy default_rng seed 5), resident in HBM",
-            "config": {"workload": "%s GP -LML, kernel=%s, D=%d, N=%d, noise=%g; %d candidate evaluations per rank per step (batched factorisation)"
-                                   % (args.config, kname, d, n, noise, batch),
+            "config": {"workload": ("%s GP -LML sweep, kernel=SE (scaled), D=%d, N=%d, noise=%g; one step = all %d "
+                                    "(lengthscale, variance) candidates, %d per rank as one batched factorisation"
+                                    % (args.config, d, n, noise, len(c4_candidates()), batch)) if sweep else
+                                   ("%s GP -LML, kernel=%s, D=%d, N=%d, noise=%g; %d candidate evaluations per rank per step (batched factorisation)"
+                                    % (args.config, kname, d, n, noise, batch)),
                        "candidates_per_rank_step": batch,
                        "n": n, "d": d, "kernel": kname, "panel": int(lay.nb), "parallelism": "dp%d (independent candidates)" % world},
             "roofline": roof,
