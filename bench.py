@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="nlml", choices=["nlml", "grad"],
+                    help="nlml: -LML only (the headline metric); grad: -LML + its gradient w.r.t. every "
+                         "hyperparameter and the noise (identity-augmented factorisation + gradient pass)")
     ap.add_argument("--n", type=int, default=None, help="override N")
     ap.add_argument("--batch", type=int, default=None,
                     help="hyperparameter candidates factorised together per rank per step "
@@ -89,6 +92,31 @@ def build_kernel(name, d):
     if name == "SE-ARD+PER":
         return ops.AdditionOperator(d, [bk.SquaredExponentialKernel(d, ard=True), bk.PeriodicKernel(d, standard=True)])
     raise ValueError(name)
+
+
+def cpu_baseline_grad(cfg_name, n):
+    """-LML + gradient by the autodiff oracle (torch CPU reverse mode through Cholesky), one warm
+    evaluation on this host's threads."""
+    import numpy as np
+    import torch
+    from oracle import gp_autodiff as ad
+    from oracle import gp_oracle as o
+    threads = int(os.environ.get("GPK_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(threads)
+    kname, d, _, noise, _, hyp = CONFIGS[cfg_name]
+    tree = {"SE": ("SE", {}), "SE-SCALED": ("SE", {})}.get(kname)
+    if tree is None or hyp is None:
+        return None
+    x, y = o.make_inputs("metric" if cfg_name == "metric" else cfg_name, n=n)
+    ad.nlml_and_grad(tree, hyp, noise, x[:512], y[:512])  # warm
+    t0 = time.perf_counter()
+    ad.nlml_and_grad(tree, hyp, noise, x, y)
+    t1 = time.perf_counter() - t0
+    return {"value": 1.0 / t1, "unit": "LML+gradient evals/s", "cores": threads, "kind": "port",
+            "sample": "one warm -LML + gradient evaluation of the %s workload (N=%d, fp64) by the autodiff "
+                      "oracle (oracle/gp_autodiff.py: torch CPU reverse mode through cholesky / "
+                      "triangular_solve, as tf.GradientTape in the reference), %d threads (%.1f s)"
+                      % (cfg_name, n, threads, t1)}
 
 
 def cpu_baseline(cfg_name, n, budget_s):
@@ -197,12 +225,19 @@ def main():
             rows.append(h)
     H = torch.tensor(rows, dtype=torch.float64, device=dev).contiguous()
     NZ = torch.tensor([noise], dtype=torch.float64, device=dev)
-    fact = engine.AugmentedFactorization(n, d, 0, batch, dt)
+    grad_mode = args.mode == "grad"
+    if grad_mode:
+        fact = engine.InverseFactorization(n, d, batch, dt)
+    else:
+        fact = engine.AugmentedFactorization(n, d, 0, batch, dt)
     gathered = torch.empty(2 * chunk * world, dtype=torch.float64, device=dev) if world > 1 else None
     mine = torch.full((2 * chunk,), float("nan"), dtype=torch.float64, device=dev)
 
     def step():
-        fact.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
+        if grad_mode:
+            fact.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0, gradient=True)
+        else:
+            fact.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
         if world > 1:
             mine[:batch] = fact.nlml()
             mine[chunk:chunk + batch] = fact.info.to(torch.float64)
@@ -255,11 +290,13 @@ def main():
         value = evals / el
         ms = el / args.steps * 1000.0
         lay = fact.layout
-        f_lml = n ** 3 / 3.0 + 2.0 * n * n
+        # algorithmic flops per evaluation: potrf + 2 trsv; with the gradient, potrf + trtri + lauum
+        # (n^3: the inverse from the identity-augmented factorisation) + the O(n^2) gradient pass
+        f_lml = float(n) ** 3 if grad_mode else n ** 3 / 3.0 + 2.0 * n * n
         roof = None
         breakdown = None
         if timing:
-            pmc = pmc_traffic(args.config, batch)
+            pmc = pmc_traffic(args.config + ("_grad" if grad_mode else ""), batch)
             up = iso["update"]
             ach = up["flops"] / (up["ms"] * 1e-3) / 1e12 if up["ms"] > 0 else 0.0
             ov = timing["update"]
@@ -281,11 +318,12 @@ def main():
             breakdown["note"] = "sums of kernel spans per class; with the look-ahead the classes overlap"
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.config, n, args.cpu_seconds)
+            cpu = cpu_baseline_grad(args.config, n) if grad_mode else cpu_baseline(args.config, n, args.cpu_seconds)
         line = {
-            "metric": "log-marginal-likelihood evals/sec at N=%d %s" % (n, "fp64" if dtn == "f64" else "fp32"),
+            "metric": ("log-marginal-likelihood%s evals/sec at N=%d %s"
+                       % (" + gradient" if grad_mode else "", n, "fp64" if dtn == "f64" else "fp32")),
             "value": round(value, 3),
-            "unit": "LML evals/s",
+            "unit": "LML+gradient evals/s" if grad_mode else "LML evals/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,

@@ -44,6 +44,10 @@ class LogLikelihood(AbstractLogLikelihood):
         if reset:
             self.covariance_matrix.reset()
             self.last_covariance_matrix = None
+        if _wants_grad(hyper_parameter, noise):
+            # differentiable form: what the reference's tf.GradientTape sees through get_metric
+            # (Optimizer/Fitter.py:104-158); backward() uses the analytic device gradient
+            return _NegLogLikelihood.apply(self, _as_tensor(noise), *[_as_tensor(h) for h in hyper_parameter])
         f = self.covariance_matrix.factorization(hyper_parameter, noise)
         if self.data_input.data_x_train.dim() == 3:
             n = float(self.data_input.n_train)
@@ -54,12 +58,70 @@ class LogLikelihood(AbstractLogLikelihood):
             return -agg(ll)
         return f.nlml().reshape(1, 1)
 
+    def get_metric_and_gradient(self, hyper_parameter: List, noise, reset: bool = True):
+        """(-LML [1, 1], [d(-LML)/d h for h in hyper_parameter] (each shaped like h), d(-LML)/d noise).
+
+        One device factorisation with identity extra rows yields K^-1 and alpha; one fused pass
+        over the lower triangle evaluates 1/2 sum_ij ((K^-1)_ij - alpha_i alpha_j) dK_ij/d theta
+        for every hyperparameter (gpk_nlml_grad).  This is the gradient the reference obtains by
+        tf.GradientTape through get_metric (Optimizer/Fitter.py:104-158).  Gradients are NaN when
+        K + noise I is not positive definite (the metric is +inf)."""
+        if reset:
+            self.covariance_matrix.reset()
+            self.last_covariance_matrix = None
+        if self.data_input.data_x_train.dim() == 3:
+            raise NotImplementedError("gradients of the BatchDataInput aggregate (Q7) are not provided")
+        f = self.covariance_matrix.inverse_factorization(hyper_parameter, noise, gradient=True)
+        g = f.gradient()[0]
+        return f.nlml().reshape(1, 1), _split_like(g[:-1], hyper_parameter), g[-1]
+
     def get_metric_checked(self, hyper_parameter: List, noise, reset: bool = True) -> torch.Tensor:
         """get_metric that raises CholeskyError when K + noise I is not positive definite
         (the reference's TensorFlow raises from tf.linalg.cholesky); synchronises."""
         out = self.get_metric(hyper_parameter, noise, reset=reset)
         self.covariance_matrix.factorization(hyper_parameter, noise).check_info()
         return out
+
+
+def _as_tensor(h) -> torch.Tensor:
+    return h if isinstance(h, torch.Tensor) else torch.as_tensor(h, dtype=torch.float64)
+
+
+def _wants_grad(hyper_parameter, noise) -> bool:
+    if not torch.is_grad_enabled():
+        return False
+    return any(isinstance(h, torch.Tensor) and h.requires_grad for h in list(hyper_parameter) + [noise])
+
+
+def _split_like(flat: torch.Tensor, hyper_parameter) -> List[torch.Tensor]:
+    """Split a flat DFS-ordered vector into pieces shaped like the hyperparameter entries."""
+    out, i = [], 0
+    for h in hyper_parameter:
+        t = _as_tensor(h)
+        k = max(1, t.numel())
+        out.append(flat[i:i + k].reshape(t.shape))
+        i += k
+    return out
+
+
+class _NegLogLikelihood(torch.autograd.Function):
+    """-LML as an autograd node whose backward is the analytic device gradient."""
+
+    @staticmethod
+    def forward(ctx, metric, noise, *hyper_parameter):
+        nl, grads, gnoise = metric.get_metric_and_gradient(list(hyper_parameter), noise, reset=False)
+        ctx.save_for_backward(gnoise, *grads)
+        ctx.meta = [(h.device, h.dtype) for h in (noise,) + hyper_parameter]
+        return nl.clone()
+
+    @staticmethod
+    def backward(ctx, gout):
+        saved = ctx.saved_tensors
+        s = gout.reshape(())
+        res = [None]
+        for g, (dev, dt) in zip(saved, ctx.meta):
+            res.append((g * s).to(device=dev, dtype=dt))
+        return tuple(res)
 
 
 class BlockwiseLogLikelihood(AbstractMetric):

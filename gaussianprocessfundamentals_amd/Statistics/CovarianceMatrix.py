@@ -173,28 +173,41 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
         if self.data_input.data_x_train.dim() == 3:
             raise NotImplementedError("explicit inverses are not provided for BatchDataInput")
         if self._inv_fact is None:
-            x, _ = self._xy()
-            _, n, d = self._shape(x)
-            f = engine.AugmentedFactorization(n, d, n, 1, global_param.p_dtype)
-            eye = torch.eye(n, dtype=torch.float64, device=engine.device())
-            self._run(f, hyper_parameter, noise, E=eye)
-            f.check_info()
-            self._inv_fact = f
+            self._inv_fact = self.inverse_factorization(hyper_parameter, noise, gradient=False)
+            self._inv_fact.check_info()
         return self._inv_fact
+
+    def inverse_factorization(self, hyper_parameter, noise, gradient: bool = True):
+        """One factorisation with identity extra rows (engine.InverseFactorization): -LML, K^-1,
+        L^-1, alpha and (gradient=True) d(-LML)/d(hyperparameters, noise) for every member of a
+        DataInput (batch 1) or BatchDataInput (one member per batch entry).  Not memoised."""
+        self._require_data()
+        if not _is_scalar(noise):
+            raise Exception("No Data Input given or Noise unspecified")
+        x, y = self._xy()
+        batch, n, d = self._shape(x)
+        kd = engine.kernel_descriptor(self.kernel, d)
+        hyp = engine.pack_hyper_parameter(hyper_parameter, kd.n_hyp)
+        f = engine.InverseFactorization(n, d, batch, global_param.p_dtype)
+        yv = y.reshape(batch, n).to(torch.float64).contiguous()
+        f.run(kd, hyp, 0, noise_vector(noise), 0, x.contiguous(), n * d if batch > 1 else 0, yv,
+              n if batch > 1 else 0, gradient=gradient)
+        self.kernel._record_hyper_parameter(list(hyper_parameter))
+        return f
 
     def get_L_inv_K(self, hyper_parameter: List, noise) -> torch.Tensor:
         """inv(L) (CovarianceMatrix.py:267-275), without an explicit inverse: the identity rows of
         the augmented matrix come out as L^-T."""
         if self.L_inv_K is None:
             f = self._inverse_factorization(hyper_parameter, noise)
-            self.L_inv_K = f.extra_rows(0).to(torch.float64).transpose(0, 1).contiguous()
+            self.L_inv_K = f.l_inv(0).to(torch.float64).contiguous()
         return self.L_inv_K
 
     def get_K_inv(self, hyper_parameter: List, noise) -> torch.Tensor:
         """inv(K + noise I) (CovarianceMatrix.py:208-216) from the Schur complement corner."""
         if self.K_inv is None:
             f = self._inverse_factorization(hyper_parameter, noise)
-            self.K_inv = -f.corner(0).to(torch.float64)
+            self.K_inv = f.k_inv(0).to(torch.float64)
         return self.K_inv
 
     def get_K_s(self, hyper_parameter: List) -> torch.Tensor:

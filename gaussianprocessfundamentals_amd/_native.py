@@ -14,19 +14,21 @@ import torch  # noqa: F401  (must be loaded first: libgpk binds to torch's HIP r
 
 from . import _build
 
-GPK_ABI_VERSION = 1
+GPK_ABI_VERSION = 2
 GPK_F64, GPK_F32 = 0, 1
 OP_PER, OP_SE, OP_MAT32, OP_MAT52, OP_ADD, OP_MUL = 104, 105, 107, 108, 201, 202
 NODE_SCALED, NODE_ARD, NODE_SE_EXPANDED, NODE_STANDARD = 1, 2, 4, 8
 MAX_NODES, MAX_DIM, MAX_ARD, MAX_HYP = 16, 16, 2, 64
-NUM_CLASSES = 6
-TIMING_CLASSES = ("assemble", "diag", "trsm", "update", "finalize", "trsv")
+NUM_CLASSES = 7
+TIMING_CLASSES = ("assemble", "diag", "trsm", "update", "finalize", "trsv", "grad")
+AUG_EXTRA_IDENTITY = 1
 
 # every function include/gpk.h declares (checked by tests/test_abi.py against the header)
 EXPORTS = (
     "gpk_abi_version", "gpk_last_error", "gpk_plan", "gpk_assemble", "gpk_potrf_aug",
     "gpk_finalize", "gpk_nlml", "gpk_kernel_matrix", "gpk_trsv", "gpk_timing_enable",
-    "gpk_timing_read", "gpk_timing_reset", "gpk_tune",
+    "gpk_timing_read", "gpk_timing_reset", "gpk_tune", "gpk_potrf_aug_ex", "gpk_assemble_inverse",
+    "gpk_grad_workspace_bytes", "gpk_nlml_grad",
 )
 
 
@@ -77,6 +79,12 @@ def _declare(lib):
         "gpk_timing_read": (c_int, [D, POINTER(c_int64), D, D]),
         "gpk_timing_reset": (c_int, []),
         "gpk_tune": (c_int, [ctypes.c_char_p, c_int64, ctypes.POINTER(c_int64)]),
+        "gpk_potrf_aug_ex": (c_int, [POINTER(GpkLayout), P, P, P, c_int32, P]),
+        "gpk_assemble_inverse": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64,
+                                         P, c_int64, P, c_int64, P, P]),
+        "gpk_grad_workspace_bytes": (c_size_t, [POINTER(GpkKdesc), POINTER(GpkLayout)]),
+        "gpk_nlml_grad": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64, P,
+                                  c_int64, P, c_int64, P, P, P, P, P, P, c_size_t, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

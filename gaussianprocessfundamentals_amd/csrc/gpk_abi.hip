@@ -105,6 +105,31 @@ bool valid_kdesc(const gpk_kdesc* kd, int64_t d) {
 
 size_t elem_size(int dtype) { return dtype == GPK_F64 ? 8 : 4; }
 
+// For every base node of the postfix program: the nodes (subtree roots) whose values multiply
+// its value on the way to the root -- the siblings under each MUL ancestor.  d K / d k_node is
+// the product of those values (ADD ancestors pass the adjoint through unchanged).
+void adjoint_masks(const gpk_kdesc& kd, uint32_t* mask) {
+  int left[GPK_MAX_NODES], right[GPK_MAX_NODES], stk[GPK_MAX_NODES];
+  int sp = 0;
+  for (int q = 0; q < kd.n_nodes; ++q) {
+    left[q] = right[q] = -1;
+    mask[q] = 0u;
+    if (kd.nodes[q].op == GPK_OP_ADD || kd.nodes[q].op == GPK_OP_MUL) {
+      right[q] = stk[--sp];
+      left[q] = stk[--sp];
+    }
+    stk[sp++] = q;
+  }
+  for (int q = kd.n_nodes; q < GPK_MAX_NODES; ++q) mask[q] = 0u;
+  // top-down: the root is the last node; children inherit the parent's mask (+ sibling at MUL)
+  for (int q = kd.n_nodes - 1; q >= 0; --q) {
+    if (left[q] < 0) continue;
+    const bool mul = kd.nodes[q].op == GPK_OP_MUL;
+    mask[left[q]] = mask[q] | (mul ? (1u << right[q]) : 0u);
+    mask[right[q]] = mask[q] | (mul ? (1u << left[q]) : 0u);
+  }
+}
+
 // Launch-shape thresholds (environment overrides for tuning runs).
 struct Tune {
   int64_t upd_t128_min;   // 128 x 128 update tiles when at least this many (else 64 x 64)
@@ -236,17 +261,18 @@ static int check_layout(const gpk_layout* lay) {
   return 0;
 }
 
-int gpk_assemble(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
-                 int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
-                 const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
-                 const double* E, int64_t e_bstride, const double* y, int64_t y_bstride,
-                 void* W, void* stream) {
+static int assemble_impl(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+                         int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+                         const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
+                         const double* E, int64_t e_bstride, const double* y, int64_t y_bstride,
+                         void* W, bool eye, void* stream) {
   if (int e = check_layout(lay)) return e;
   if (!valid_kdesc(kd, lay->d)) return fail_arg(1, "kernel descriptor");
   if (!hyp_dev && kd->n_hyp > 0) return fail_arg(3, "hyp_dev");
   if (!noise_dev) return fail_arg(5, "noise_dev");
   if (!X) return fail_arg(7, "X");
-  if (lay->m > 0 && !Xs && !E) return fail_arg(9, "Xs or E");
+  if (eye && lay->m != lay->n) return fail_arg(2, "identity extra rows need a layout planned with m = n");
+  if (lay->m > 0 && !Xs && !E && !eye) return fail_arg(9, "Xs or E");
   if (!y) return fail_arg(13, "y");
   if (!W) return fail_arg(15, "W");
   AsmArgs a;
@@ -274,6 +300,7 @@ int gpk_assemble(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_d
   a.d = (int32_t)lay->d;
   a.dp = (lay->d % 2 == 0) ? (int32_t)lay->d + 1 : (int32_t)lay->d;
   a.plain = 0;
+  a.eye = eye ? 1 : 0;
   a.ntile = lay->p / ATILE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const double es = (double)elem_size(lay->dtype);
@@ -285,11 +312,32 @@ int gpk_assemble(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_d
   return 0;
 }
 
-int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, void* stream) {
+int gpk_assemble(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+                 int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+                 const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
+                 const double* E, int64_t e_bstride, const double* y, int64_t y_bstride,
+                 void* W, void* stream) {
+  return assemble_impl(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, Xs,
+                       xs_bstride, E, e_bstride, y, y_bstride, W, false, stream);
+}
+
+int gpk_assemble_inverse(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+                         int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+                         const double* X, int64_t x_bstride, const double* y, int64_t y_bstride,
+                         void* W, void* stream) {
+  return assemble_impl(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, nullptr,
+                       0, nullptr, 0, y, y_bstride, W, true, stream);
+}
+
+int gpk_potrf_aug_ex(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, int32_t flags,
+                     void* stream) {
   if (int e = check_layout(lay)) return e;
   if (!W) return fail_arg(2, "W");
   if (!Winv) return fail_arg(3, "Winv");
   if (!info_dev) return fail_arg(4, "info_dev");
+  if (flags & ~GPK_AUG_EXTRA_IDENTITY) return fail_arg(5, "flags");
+  const bool eye = (flags & GPK_AUG_EXTRA_IDENTITY) != 0;
+  if (eye && lay->m != lay->n) return fail_arg(1, "identity extra rows need a layout planned with m = n");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int dt = lay->dtype;
   const size_t es = elem_size(dt);
@@ -341,6 +389,10 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
     const int tile = (rows / NB * lay->batch >= tn.trsm_t128_min) ? 128 : 64;
     ga.nt = (int32_t)(rows / tile);
     ga.kdepth = NB;
+    if (eye) {  // identity rows t >= j0 + nb are still zero in this panel
+      ga.zlo = lay->n_pad + ga.j0 + NB;
+      ga.zhi = lay->y_row;
+    }
     const double rK = (double)(lay->n_pad - ga.row0);  // algorithmic: K-part rows x nb^2
     return timed(2, (double)lay->batch * rK * NB * NB, 0.0, sp,
                  [&] { return launch_gemm(ga, dt, GEMM_TRSM, tile, lay->batch, sp); });
@@ -364,6 +416,10 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
     ga.nt = (int32_t)(rows / tile);
     ga.c_lo = (int32_t)(c_lo * scale);
     ga.c_hi = (int32_t)(c_hi * scale);
+    if (eye) {  // identity rows t >= j0 + kdepth are zero in the panel columns
+      ga.zlo = lay->n_pad + j0 + kdepth;
+      ga.zhi = lay->y_row;
+    }
     // algorithmic flops: 2 kdepth x (lower-triangle elements of the K part in the column range)
     const double rK = (double)(lay->n_pad - ga.row0);
     const double cl = std::min(rK, (double)(c_lo * NB)), ch = std::min(rK, (double)(c_hi * NB));
@@ -420,6 +476,10 @@ int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
   return 0;
 }
 
+int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, void* stream) {
+  return gpk_potrf_aug_ex(lay, W, Winv, info_dev, 0, stream);
+}
+
 int gpk_finalize(const gpk_layout* lay, const void* W, const int32_t* info_dev, double* out_dev,
                  double* mu_dev, double* var_dev, void* stream) {
   if (int e = check_layout(lay)) return e;
@@ -459,6 +519,56 @@ int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, 
   e = gpk_potrf_aug(lay, W, Winv, info_dev, stream);
   if (e) return e;
   return gpk_finalize(lay, W, info_dev, out_dev, nullptr, nullptr, stream);
+}
+
+size_t gpk_grad_workspace_bytes(const gpk_kdesc* kd, const gpk_layout* lay) {
+  if (!kd || !lay || lay->n <= 0 || lay->batch <= 0) return 0;
+  const int64_t nt = (lay->n + ATILE - 1) / ATILE;
+  return (size_t)lay->batch * (size_t)(nt * (nt + 1) / 2) * (size_t)(kd->n_hyp + 1) * sizeof(double);
+}
+
+int gpk_nlml_grad(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, int64_t hyp_stride,
+                  const double* noise_dev, int64_t noise_stride, const double* X, int64_t x_bstride,
+                  const double* y, int64_t y_bstride, void* W, void* Winv, int32_t* info_dev,
+                  double* out_dev, double* grad_dev, void* work, size_t work_bytes, void* stream) {
+  if (int e = check_layout(lay)) return e;
+  if (lay->m != lay->n) return fail_arg(2, "gpk_nlml_grad needs a layout planned with m = n");
+  if (!valid_kdesc(kd, lay->d)) return fail_arg(1, "kernel descriptor");
+  if (!info_dev) return fail_arg(13, "info_dev");
+  if (!out_dev) return fail_arg(14, "out_dev");
+  if (grad_dev && (!work || work_bytes < gpk_grad_workspace_bytes(kd, lay)))
+    return fail_arg(16, "work (see gpk_grad_workspace_bytes)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(hipMemsetAsync(info_dev, 0, sizeof(int32_t) * lay->batch, s), "memset info");
+  int e = gpk_assemble_inverse(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, y,
+                               y_bstride, W, stream);
+  if (e) return e;
+  e = gpk_potrf_aug_ex(lay, W, Winv, info_dev, GPK_AUG_EXTRA_IDENTITY, stream);
+  if (e) return e;
+  e = gpk_finalize(lay, W, info_dev, out_dev, nullptr, nullptr, stream);
+  if (e) return e;
+  if (!grad_dev) return 0;
+  GradArgs g;
+  memset(&g, 0, sizeof(g));
+  g.W = W;
+  g.ld = lay->ld;
+  g.w_bs = lay->w_batch_stride;
+  g.n = lay->n;
+  g.n_pad = lay->n_pad;
+  g.y_row = lay->y_row;
+  g.hyp = hyp_dev;
+  g.hyp_stride = hyp_stride;
+  g.X = X;
+  g.x_bs = x_bstride;
+  g.d = (int32_t)lay->d;
+  g.dp = (lay->d % 2 == 0) ? (int32_t)lay->d + 1 : (int32_t)lay->d;
+  g.ntile = (lay->n + ATILE - 1) / ATILE;
+  g.part = static_cast<double*>(work);
+  g.grad = grad_dev;
+  g.info = info_dev;
+  adjoint_masks(*kd, g.adj_mask);
+  GPK_HIP(timed(6, 0.0, 0.0, s, [&] { return launch_grad(*kd, g, lay->dtype, lay->batch, s); }), "grad");
+  return 0;
 }
 
 int gpk_kernel_matrix(const gpk_kdesc* kd, const double* hyp_dev, int dtype, int uplo,

@@ -17,6 +17,8 @@
 //   Auxiliary/Distances.py:4-7 (GPK_NODE_SE_EXPANDED) or the direct sum of squares.
 //   noise on the training diagonal only: Statistics/CovarianceMatrix.py:197-206; K_ss has none
 //   (:218-225); K_s = k(X, X_test) (:277-286).
+#include <string.h>
+
 #include "gpk_internal.h"
 
 namespace gpk {
@@ -161,7 +163,7 @@ __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs&
     } else {
       const int c = classify(a, g);
       if (c == CLS_TRAIN) v = a.X[(int64_t)b * a.x_bs + g * a.d + k];
-      else if (c == CLS_TEST && a.E == nullptr) v = a.Xs[(int64_t)b * a.xs_bs + (g - a.n_pad) * a.d + k];
+      else if (c == CLS_TEST && a.E == nullptr && !a.eye) v = a.Xs[(int64_t)b * a.xs_bs + (g - a.n_pad) * a.d + k];
     }
     dst[pt * a.dp + k] = v;
     // ARD copies: u = x / ls (the reference kernel with l = 1 on rescaled inputs)
@@ -229,6 +231,8 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
     double v = 0.0;
     if (rcls == CLS_PAD || ccls == CLS_PAD) {
       v = (gi == gj) ? 1.0 : 0.0;
+    } else if (a.eye && rcls == CLS_TEST) {
+      v = (ccls == CLS_TRAIN && gj == gi - a.n_pad) ? 1.0 : 0.0;
     } else if (a.E != nullptr && rcls == CLS_TEST) {
       v = (ccls == CLS_TRAIN) ? a.E[(int64_t)b * a.e_bs + (gi - a.n_pad) * a.n + gj] : 0.0;
     } else if ((rcls == CLS_TRAIN || rcls == CLS_TEST) && (ccls == CLS_TRAIN || ccls == CLS_TEST)) {
@@ -241,7 +245,315 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   }
 }
 
+// ================================================================================ LML gradient
+// d(-LML)/d theta_p = 1/2 sum_ij (K^-1 - alpha alpha^T)_ij dK_ij/d theta_p: the reverse-mode
+// derivative TensorFlow's GradientTape takes through LogLikelihood.get_metric for
+// VariationalSgdFitter (gpbasics/Optimizer/Fitter.py:104-158).  K^-1 and alpha come out of ONE
+// factorisation of the augmented matrix with identity extra rows: its corner holds -K^-1 (lower
+// triangle) and its y row -alpha^T.  Every workgroup takes one 64 x 64 lower tile of the n x n
+// training block, re-evaluates the kernel tree there (values of every node, so the adjoint of a
+// base node is the product of the node values its ancestors multiply it by -- a host-built mask)
+// and reduces the weighted partial derivatives of each base node's hyperparameters; partial sums
+// per tile go to a workspace reduced in a fixed order by grad_reduce_kernel (deterministic).
+
+// values of every node of the postfix program (node q's value = its subtree's value) into the
+// thread's LDS column v[q * 256]
+__device__ __forceinline__ void eval_nodes(const gpk_kdesc& kd, const double* hyp, const double* pa,
+                                           const double* pb, int slot_stride, int d, double* v) {
+  Stack st;
+  st.s0 = 0.0;
+  int sp = 0;
+#pragma unroll 1
+  for (int q = 0; q < kd.n_nodes; ++q) {
+    const gpk_node nd = kd.nodes[q];
+    if (nd.op == GPK_OP_ADD || nd.op == GPK_OP_MUL) {
+      const double top = st.get(sp - 1);
+      const double below = st.get(sp - 2);
+      st.set(sp - 2, nd.op == GPK_OP_ADD ? below + top : below * top);
+      sp -= 1;
+    } else {
+      const int off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
+      st.set(sp, base_value(nd, hyp, pa + off, pb + off, d));
+      sp += 1;
+    }
+    v[q * 256] = st.get(sp - 1);
+  }
+}
+
+constexpr int GNP = GPK_MAX_DIM + 1;  // hyperparameters of one base node, at most (ARD l + sg)
+
+// acc[k] += coef * d k_node / d h[k] for the node's hyperparameters h (reference formulas, see the
+// citations at the top of this file; |l| of the Matern kernels differentiates to sign(l)).
+__device__ __forceinline__ void base_partials(const gpk_node& nd, const double* __restrict__ hyp,
+                                              const double* a, const double* b, int d, double coef,
+                                              double (&acc)[GNP]) {
+  const int fl = nd.flags;
+  const bool ard = (fl & GPK_NODE_ARD) != 0;
+  const bool scaled = (fl & GPK_NODE_SCALED) != 0;
+  const double* h = hyp + nd.hyp_offset;
+  if (nd.op == GPK_OP_SE) {
+    double s = 0.0;
+    if (fl & GPK_NODE_SE_EXPANDED) {
+      double na = 0.0, nb = 0.0, ab = 0.0;
+      for (int k = 0; k < d; ++k) {
+        na += a[k] * a[k];
+        nb += b[k] * b[k];
+        ab += a[k] * b[k];
+      }
+      const double dist = sqrt((na - 2.0 * ab) + nb);
+      s = dist * dist;
+    } else {
+      for (int k = 0; k < d; ++k) {
+        const double t = a[k] - b[k];
+        s += t * t;
+      }
+    }
+    const int sg_at = ard ? d : 1;
+    const double sg = scaled ? h[sg_at] : 1.0;
+    if (ard) {
+      const double r = exp(-0.5 * s);
+#pragma unroll
+      for (int k = 0; k < GPK_MAX_DIM; ++k)
+        if (k < d) {
+          const double t = a[k] - b[k];  // (x_k - y_k) / l_k
+          acc[k] += coef * sg * r * (t * t) / h[k];
+        }
+      if (scaled) acc[GPK_MAX_DIM] += coef * r;
+    } else {
+      const double l = h[0];
+      const double r = exp(-0.5 * (s / (l * l)));
+      acc[0] += coef * sg * r * s / (l * l * l);
+      if (scaled) acc[1] += coef * r;
+    }
+    return;
+  }
+  if (nd.op == GPK_OP_PER) {
+    const double l = h[0], per = h[1];
+    double sn, tw;  // sum sin^2(theta), sum theta sin(2 theta)
+    if (fl & GPK_NODE_STANDARD) {
+      sn = 0.0;
+      tw = 0.0;
+      for (int k = 0; k < d; ++k) {
+        const double th = PI * (fabs(a[k] - b[k]) / per);
+        const double t = sin(th);
+        sn += t * t;
+        tw += th * sin(2.0 * th);
+      }
+    } else {
+      double dist = 0.0;
+      for (int k = 0; k < d; ++k) dist += fabs(a[k] - b[k]);
+      const double th = PI * (dist / per);
+      const double t = sin(th);
+      sn = t * t;
+      tw = th * sin(2.0 * th);
+    }
+    const double r = exp((-2.0 * sn) / (l * l));
+    const double sg = scaled ? h[2] : 1.0;
+    acc[0] += coef * sg * r * 4.0 * sn / (l * l * l);
+    acc[1] += coef * sg * r * 2.0 * tw / (l * l * per);
+    if (scaled) acc[2] += coef * r;
+    return;
+  }
+  // MAT32 / MAT52
+  const bool std_form = (fl & GPK_NODE_STANDARD) != 0;
+  double dist = 0.0;
+  if (std_form) {
+    for (int k = 0; k < d; ++k) {
+      const double t = a[k] - b[k];
+      dist += t * t;
+    }
+    dist = sqrt(dist);
+  } else {
+    for (int k = 0; k < d; ++k) dist += fabs(a[k] - b[k]);
+  }
+  const double c = (nd.op == GPK_OP_MAT52) ? SQRT5 : SQRT3;
+  const int sg_at = ard ? d : 1;
+  const double sg = scaled ? h[sg_at] : 1.0;
+  const double l = ard ? 1.0 : h[0];
+  const double f = (c * dist) / fabs(l);
+  const double e = exp(-f);
+  double r, drdf;  // value and d value / d f
+  if (nd.op == GPK_OP_MAT52) {
+    r = ((1.0 + f) + f * f / 3.0) * e;
+    drdf = -(f / 3.0) * (1.0 + f) * e;
+  } else {
+    r = (1.0 + f) * e;
+    drdf = -f * e;
+  }
+  if (ard) {
+    // f = c dist(u, v), u = x / l: d dist / d l_k = -|u_k - v_k| / l_k (L1) or
+    // -(u_k - v_k)^2 / (l_k dist) (Euclidean)
+#pragma unroll
+    for (int k = 0; k < GPK_MAX_DIM; ++k)
+      if (k < d) {
+        const double t = a[k] - b[k];
+        double dd;
+        if (std_form) dd = dist > 0.0 ? -(t * t) / (h[k] * dist) : 0.0;
+        else dd = -fabs(t) / h[k];
+        acc[k] += coef * sg * drdf * c * dd;
+      }
+    if (scaled) acc[GPK_MAX_DIM] += coef * r;
+  } else {
+    acc[0] += coef * sg * drdf * (-f / l);  // d f / d l = -f / l  (f uses |l|)
+    if (scaled) acc[1] += coef * r;
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void grad_kernel(gpk_kdesc kd, AsmArgs a, GradArgs g) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int slot_stride = ATILE * a.dp;
+  double* hyp_s = smem;                                  // GPK_MAX_HYP
+  double* al_r = hyp_s + GPK_MAX_HYP;                    // alpha of the tile rows / columns
+  double* al_c = al_r + ATILE;
+  double* red = al_c + ATILE;                            // [4 waves][GNP + 1]
+  double* prow = red + 4 * (GNP + 1);
+  double* pcol = prow + (1 + kd.n_ard) * slot_stride;
+  double* vals = pcol + (1 + kd.n_ard) * slot_stride;   // [n_nodes][256] node values (MUL trees)
+
+  const int b = blockIdx.y;
+  const int64_t t = blockIdx.x;
+  int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while (r * (r + 1) / 2 > t) --r;
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  const int64_t ti = r, tj = t - r * (r + 1) / 2;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int np1 = kd.n_hyp + 1;
+  double* part = g.part + ((int64_t)b * gridDim.x + t) * np1;
+
+  const double* hyp_g = g.hyp + (int64_t)b * g.hyp_stride;
+  for (int e = tid; e < kd.n_hyp; e += 256) hyp_s[e] = hyp_g[e];
+  const T* W = reinterpret_cast<const T*>(g.W) + (int64_t)b * g.w_bs;
+  const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
+  if (tid < 2 * ATILE) {
+    const int64_t gg = (tid < ATILE ? gi0 : gj0) + (tid & (ATILE - 1));
+    // y row of the corner: -alpha^T
+    const double v = gg < g.n ? -(double)W[g.y_row * g.ld + g.n_pad + gg] : 0.0;
+    (tid < ATILE ? al_r : al_c)[tid & (ATILE - 1)] = v;
+  }
+  __syncthreads();
+  stage_points(kd, a, hyp_s, prow, gi0, b, true, slot_stride);
+  stage_points(kd, a, hyp_s, pcol, gj0, b, false, slot_stride);
+  __syncthreads();
+
+  const int c = lane;
+  const int64_t gj = gj0 + c;
+  // weighted (K^-1 - alpha alpha^T)_ij of this thread's 16 elements: weight 2 off the diagonal
+  // (the strictly lower triangle stands for both halves), 1 on it; the corner holds -K^-1
+  auto qval = [&](int rr) -> double {
+    const int64_t gi = gi0 + rr;
+    if (gi >= g.n || gj > gi) return 0.0;
+    const double qq = -(double)W[(g.n_pad + gi) * g.ld + g.n_pad + gj] - al_r[rr] * al_c[c];
+    return gi == gj ? qq : 2.0 * qq;
+  };
+  double noise_acc = 0.0;  // d K / d noise = I: the diagonal of the weighted matrix
+  if (ti == tj && (c & 3) == wave) noise_acc = qval(c);
+
+  for (int qn = 0; qn < kd.n_nodes; ++qn) {
+    const gpk_node nd = kd.nodes[qn];
+    if (nd.op == GPK_OP_ADD || nd.op == GPK_OP_MUL) continue;
+    const uint32_t mask = g.adj_mask[qn];
+    const int off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
+    double acc[GNP];
+#pragma unroll
+    for (int k = 0; k < GNP; ++k) acc[k] = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < ATILE / 4; ++k) {
+      const int rr = wave + 4 * k;
+      const double qk = qval(rr);
+      if (qk == 0.0) continue;
+      double adj = 1.0;
+      if (mask != 0u) {
+        eval_nodes(kd, hyp_s, prow + rr * a.dp, pcol + c * a.dp, slot_stride, a.d, vals + tid);
+#pragma unroll 1
+        for (int q = 0; q < kd.n_nodes; ++q)
+          if (mask & (1u << q)) adj *= vals[q * 256 + tid];
+      }
+      base_partials(nd, hyp_s, prow + off + rr * a.dp, pcol + off + c * a.dp, a.d, qk * adj, acc);
+    }
+    // hyperparameter slots of this node: ARD l_0..l_{d-1} then sg (stored at acc[GPK_MAX_DIM])
+    const bool ard = (nd.flags & GPK_NODE_ARD) != 0;
+    const int nshape = ard ? a.d : (nd.op == GPK_OP_PER ? 2 : 1);
+    const bool scaled = (nd.flags & GPK_NODE_SCALED) != 0;
+    const bool sg_moved = ard && scaled;
+    const int np = nshape + (scaled ? 1 : 0);
+#pragma unroll
+    for (int k = 0; k < GNP; ++k) {
+      if (k < np) {
+        const double sres = wave_sum((sg_moved && k == a.d) ? acc[GPK_MAX_DIM] : acc[k]);
+        if (lane == 0) red[wave * (GNP + 1) + k] = sres;
+      }
+    }
+    __syncthreads();
+    if (tid < np)
+      part[nd.hyp_offset + tid] = red[tid] + red[(GNP + 1) + tid] + red[2 * (GNP + 1) + tid] +
+                                  red[3 * (GNP + 1) + tid];
+    __syncthreads();
+  }
+  const double ns = wave_sum(noise_acc);
+  if (lane == 0) red[wave * (GNP + 1) + GNP] = ns;
+  __syncthreads();
+  if (tid == 0)
+    part[kd.n_hyp] = red[GNP] + red[(GNP + 1) + GNP] + red[2 * (GNP + 1) + GNP] + red[3 * (GNP + 1) + GNP];
+}
+
+// grad[b][p] = 1/2 sum over tiles (fixed order); NaN where the factorisation failed
+__global__ __launch_bounds__(256) void grad_reduce_kernel(GradArgs g, int64_t ntri, int np1) {
+  __shared__ double red[256];
+  const int p = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const double* part = g.part + (int64_t)b * ntri * np1 + p;
+  double s = 0.0;
+  for (int64_t t = tid; t < ntri; t += 256) s += part[t * np1];
+  red[tid] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) g.grad[(int64_t)b * np1 + p] = g.info[b] != 0 ? NAN : 0.5 * red[0];
+}
+
 }  // namespace
+
+hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_t batch, hipStream_t s) {
+  // the staging helpers read the points through an augmented-layout AsmArgs
+  AsmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.hyp = g.hyp;
+  a.hyp_stride = g.hyp_stride;
+  a.X = g.X;
+  a.x_bs = g.x_bs;
+  a.n = g.n;
+  a.m = g.n;
+  a.n_pad = g.n_pad;
+  a.y_row = g.y_row;
+  a.d = g.d;
+  a.dp = g.dp;
+  a.eye = 1;
+  const int64_t ntri = g.ntile * (g.ntile + 1) / 2;
+  bool has_mul = false;
+  for (int q = 0; q < kd.n_nodes; ++q) has_mul |= g.adj_mask[q] != 0u;
+  const size_t lds = sizeof(double) * (GPK_MAX_HYP + 2 * ATILE + 4 * (GNP + 1) +
+                                       2 * (size_t)(1 + kd.n_ard) * ATILE * a.dp +
+                                       (has_mul ? (size_t)kd.n_nodes * 256 : 0));
+  dim3 grid((unsigned)ntri, (unsigned)batch, 1);
+  if (dtype == GPK_F64)
+    hipLaunchKernelGGL(grad_kernel<double>, grid, dim3(256), lds, s, kd, a, g);
+  else
+    hipLaunchKernelGGL(grad_kernel<float>, grid, dim3(256), lds, s, kd, a, g);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((unsigned)(kd.n_hyp + 1), (unsigned)batch), dim3(256), 0, s,
+                     g, ntri, kd.n_hyp + 1);
+  return hipGetLastError();
+}
 
 hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
                            hipStream_t s) {

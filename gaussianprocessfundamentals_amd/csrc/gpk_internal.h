@@ -38,6 +38,7 @@ struct AsmArgs {
   int32_t uplo;      // plain mode: 1 = write j <= i only
   int64_t ntile;     // augmented: 64-tiles per dimension
   double diag_add;   // plain mode
+  int32_t eye;       // augmented: the m extra rows are the identity (E = I, m == n), zero corner
 };
 
 struct GemmArgs {
@@ -51,6 +52,9 @@ struct GemmArgs {
   int32_t nt;        // 128-tiles of the trailing region
   int32_t c_lo, c_hi;  // tile-column range handled by this launch (update)
   int32_t kdepth;      // panel width summed over (multiple of 16): 128, or 256 for the deferred update
+  // rows [zlo, zhi) are structurally zero in the panel columns [j0, j0 + kdepth) (identity extra
+  // rows: row n_pad + t of E L^-T is zero left of column t); tiles inside the range are skipped
+  int64_t zlo, zhi;
 };
 
 struct DiagArgs {
@@ -76,6 +80,24 @@ struct FinArgs {
   double* var;
 };
 
+struct GradArgs {
+  const void* W;       // factored augmented matrix with identity extra rows (m == n)
+  int64_t ld;
+  int64_t w_bs;
+  int64_t n, n_pad, y_row;
+  const double* hyp;
+  int64_t hyp_stride;
+  const double* X;
+  int64_t x_bs;
+  int32_t d;
+  int32_t dp;
+  int64_t ntile;       // 64-tiles per edge of the n x n training block
+  double* part;        // [batch][ntile (ntile + 1) / 2][n_hyp + 1] per-tile partial sums
+  double* grad;        // [batch][n_hyp + 1]
+  const int32_t* info;
+  uint32_t adj_mask[GPK_MAX_NODES];  // per node: nodes whose values multiply its adjoint
+};
+
 struct TrsvArgs {
   const void* W;
   int64_t ld;
@@ -95,6 +117,7 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s);
 hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream_t s);
+hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_trsv_diag(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
 

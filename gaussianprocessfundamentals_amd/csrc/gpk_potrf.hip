@@ -110,6 +110,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
   }
   T* W = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs;
   const int64_t R = a.row0 + ti * TM;
+  // structurally zero operand rows: the product (and so the update / solve) of the tile is zero
+  if (R >= a.zlo && R + TM <= a.zhi) return;
+  if (MODE == GEMM_UPDATE) {
+    const int64_t Rb = a.row0 + tj * TN;
+    if (Rb >= a.zlo && Rb + TN <= a.zhi) return;
+  }
   const T* Ag = W + R * a.ld + a.j0;
   const T* Bg;
   int64_t ldb;

@@ -266,3 +266,67 @@ class AugmentedFactorization:
         bad = torch.nonzero(info).flatten()
         if bad.numel():
             raise CholeskyError(int(info[bad[0]]))
+
+
+class InverseFactorization(AugmentedFactorization):
+    """Factorisation of the augmented matrix with identity extra rows (m = n), optionally followed
+    by the -LML gradient (``gpk_nlml_grad``).
+
+    After :meth:`run` the extra rows hold L^-T, the corner -K^-1 and the corner's y row -alpha^T
+    (include/gpk.h); tiles of structurally zero identity rows are skipped, so the factorisation
+    costs n^3 flops -- the work of potrf + trtri + lauum, i.e. of the reference's explicit
+    tf.linalg.inv(L) / inv(K) (gpbasics/Statistics/CovarianceMatrix.py:267-275).
+    ``gradient()[b]`` = d(-LML)/d(hyperparameters in DFS order) followed by d(-LML)/d(noise).
+    """
+
+    def __init__(self, n: int, d: int, batch: int = 1, dtype=None):
+        super().__init__(n, d, n, batch, dtype)
+        self.grad = None
+        self.work = None
+
+    def run(self, kd: nat.GpkKdesc, hyp: torch.Tensor, hyp_stride: int, noise: torch.Tensor,
+            noise_stride: int, X: torch.Tensor, x_bstride: int, y: torch.Tensor, y_bstride: int,
+            gradient: bool = True, **unused):
+        lay = self.layout
+        B, n, d = self.batch, self.n, self.d
+        dev = self.W.device
+        _check_operand("hyper_parameter", hyp, hyp_stride, kd.n_hyp, B, dev)
+        _check_operand("noise", noise, noise_stride, 1, B, dev)
+        _check_operand("X", X, x_bstride, n * d, B, dev)
+        _check_operand("y", y, y_bstride, n, B, dev)
+        L = self.L
+        grad_ptr = work_ptr = None
+        work_bytes = 0
+        if gradient:
+            work_bytes = int(L.gpk_grad_workspace_bytes(ctypes.byref(kd), ctypes.byref(lay)))
+            if self.work is None or self.work.numel() * 8 < work_bytes:
+                self.work = torch.empty(max(1, work_bytes // 8), dtype=torch.float64, device=dev)
+            self.grad = torch.empty((B, kd.n_hyp + 1), dtype=torch.float64, device=dev)
+            grad_ptr, work_ptr = nat.ptr(self.grad), nat.ptr(self.work)
+        else:
+            self.grad = None
+        nat.check(L.gpk_nlml_grad(ctypes.byref(kd), ctypes.byref(lay), nat.ptr(hyp), hyp_stride,
+                                  nat.ptr(noise), noise_stride, nat.ptr(X), x_bstride, nat.ptr(y), y_bstride,
+                                  nat.ptr(self.W), nat.ptr(self.Winv), nat.ptr(self.info), nat.ptr(self.out),
+                                  grad_ptr, work_ptr, work_bytes, nat.stream_handle(dev)), "gpk_nlml_grad")
+        self.kd = kd
+        self.done = True
+        return self
+
+    def gradient(self) -> torch.Tensor:
+        """[batch, n_hyp + 1] fp64: d(-LML)/d hyp (DFS order), then d(-LML)/d noise."""
+        if self.grad is None:
+            raise RuntimeError("run(..., gradient=True) first")
+        return self.grad
+
+    def k_inv(self, b: int = 0) -> torch.Tensor:
+        """(K + noise I)^-1, symmetrised from the corner's lower triangle."""
+        return -self.corner(b)
+
+    def l_inv(self, b: int = 0) -> torch.Tensor:
+        """L^-1 (lower): the transpose of the extra rows, which hold L^-T."""
+        return torch.triu(self.extra_rows(b)).transpose(0, 1)
+
+    def alpha(self, b: int = 0) -> torch.Tensor:
+        lay = self.layout
+        return -self.w(b)[lay.y_row, lay.n_pad:lay.n_pad + self.n].to(torch.float64)

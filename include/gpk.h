@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GPK_ABI_VERSION 1
+#define GPK_ABI_VERSION 2
 
 /* arithmetic types of the factorisation */
 enum { GPK_F64 = 0, GPK_F32 = 1 };
@@ -141,6 +141,21 @@ int gpk_assemble(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_d
  * info_dev[batch] must be zeroed by the caller before the call. */
 int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, void* stream);
 
+/* gpk_potrf_aug with flags: GPK_AUG_EXTRA_IDENTITY declares that the m (= n) extra rows were
+ * assembled as the identity (gpk_assemble_inverse); row n_pad + t of E L^-T is then zero left of
+ * column t, so every panel-solve and trailing-update tile made of such zero rows is skipped and the
+ * factorisation costs n^3 flops instead of 7 n^3 / 3 (potrf + trtri + lauum, the work of
+ * tf.linalg.inv(L) and L^-T L^-1 in get_L_inv_K / get_K_inv, Statistics/CovarianceMatrix.py:267-275). */
+#define GPK_AUG_EXTRA_IDENTITY 1
+int gpk_potrf_aug_ex(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, int32_t flags,
+                     void* stream);
+/* gpk_assemble with E = I (layout planned with m = n) without materialising E: after
+ * gpk_potrf_aug_ex(.., GPK_AUG_EXTRA_IDENTITY, ..) the extra rows hold L^-T (upper triangle),
+ * the corner -K^-1 (lower triangle) and the corner's y row -alpha^T. */
+int gpk_assemble_inverse(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+                         int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+                         const double* X, int64_t x_bstride, const double* y, int64_t y_bstride,
+                         void* W, void* stream);
 /* Read the results out of a factored W.  out_dev[b*4 + {0,1,2,3}] =
  * {nlml, fit = y^T alpha, logdet = 2 sum log L_ii, n}; nlml = +inf where info != 0.
  * mu_dev[b*m + t] = posterior mean (may be NULL), var_dev[b*m + t] = posterior variance
@@ -154,6 +169,19 @@ int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
              const double* X, int64_t x_bstride, const double* y, int64_t y_bstride,
              void* W, void* Winv, int32_t* info_dev, double* out_dev, void* stream);
 
+/* -LML and its gradient for every batch member (layout planned with m = n):
+ *   gpk_assemble_inverse + gpk_potrf_aug_ex(GPK_AUG_EXTRA_IDENTITY) + gpk_finalize, then
+ *   grad_dev[b*(n_hyp+1) + p] = d(-LML)/d hyp[p] (p < n_hyp, DFS order of the kernel tree) and
+ *   grad_dev[b*(n_hyp+1) + n_hyp] = d(-LML)/d noise, from
+ *   1/2 sum_ij ((K^-1)_ij - alpha_i alpha_j) dK_ij/d theta  -- the derivative the reference takes by
+ *   tf.GradientTape through LogLikelihood.get_metric (Optimizer/Fitter.py:104-158).
+ * grad_dev may be NULL (then only -LML and the inverse, e.g. for get_K_inv); NaN where info != 0.
+ * work: device scratch of gpk_grad_workspace_bytes(kd, lay) bytes. */
+size_t gpk_grad_workspace_bytes(const gpk_kdesc* kd, const gpk_layout* lay);
+int gpk_nlml_grad(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, int64_t hyp_stride,
+                  const double* noise_dev, int64_t noise_stride, const double* X, int64_t x_bstride,
+                  const double* y, int64_t y_bstride, void* W, void* Winv, int32_t* info_dev,
+                  double* out_dev, double* grad_dev, void* work, size_t work_bytes, void* stream);
 /* Plain kernel matrix K[i*ldk + j] = k(X_i, Y_j) (+ diag_add where i == j) for i < n, j < m.
  * uplo: 0 = full, 1 = lower triangle only.  dtype selects the stored element type. */
 int gpk_kernel_matrix(const gpk_kdesc* kd, const double* hyp_dev, int dtype, int uplo,
@@ -167,8 +195,8 @@ int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, 
              void* stream);
 
 /* Per-kernel-class timing with HIP events recorded on the launch stream.
- * class: 0 assemble, 1 diag, 2 trsm, 3 update, 4 finalize, 5 trsv */
-#define GPK_NUM_CLASSES 6
+ * class: 0 assemble, 1 diag, 2 trsm, 3 update, 4 finalize, 5 trsv, 6 grad */
+#define GPK_NUM_CLASSES 7
 int gpk_timing_enable(int on);
 /* synchronises the recorded events; returns totals since the last reset */
 int gpk_timing_read(double* ms_by_class, int64_t* launches_by_class, double* flops_by_class,

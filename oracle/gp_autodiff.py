@@ -1,0 +1,145 @@
+"""CPU gradient oracle: reverse-mode autodiff (torch, fp64, CPU) of the reference's -LML op sequence.
+
+TEST INFRASTRUCTURE ONLY (same rules as ``gp_oracle``: imported by ``tests/`` and nothing in
+the product package).
+
+The reference differentiates ``LogLikelihood.get_metric`` with ``tf.GradientTape`` inside
+``VariationalSgdFitter.fit`` (gpbasics/Optimizer/Fitter.py:104-158; TensorFlow's autodiff through
+``tf.linalg.cholesky`` / ``triangular_solve``).  TensorFlow cannot run here, so this module
+restates the same forward op sequence as ``gp_oracle`` -- kernel formulas
+(K/BaseKernels.py:277-294, :440-457, :702-720, :859-880), ADD/MUL folding with DFS
+hyperparameter slicing (K/Operators.py:207-225, :306-326), noise on the diagonal
+(S/CovarianceMatrix.py:197-206), Cholesky + two triangular solves (:247-265), log-determinant and
+-LML assembly (M/Metrics.py:152-154, M/LogLikelihood.py:30-65) -- in torch and lets torch's
+reverse mode produce the gradient, which is what GradientTape computes (including the
+derivative of |l| as sign(l) in the Matern kernels).  Pinned in tests/test_oracle.py by (a) its
+forward value == gp_oracle.nlml and (b) central finite differences of gp_oracle.nlml.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Sequence, Tuple
+
+import numpy as np
+import torch
+
+F64 = torch.float64
+LOG_2PI = math.log(2.0 * math.pi)
+
+
+def _n_hyp(tree, scaled: bool) -> int:
+    op, arg = tree
+    if op in ("ADD", "MUL"):
+        return sum(_n_hyp(c, scaled) for c in arg)
+    return (2 if op == "PER" else 1) + (1 if scaled else 0)
+
+
+def _l1(a, b):
+    return torch.sum(torch.abs(a[:, None, :] - b[None, :, :]), dim=-1)
+
+
+def _sq(a, b):
+    d = a[:, None, :] - b[None, :, :]
+    return torch.sum(d * d, dim=-1)
+
+
+def _base(op, opts, hyp, x, x_, scaled, se_expanded):
+    ard = bool(opts.get("ard", False))
+    if op == "SE":
+        if ard:
+            x, x_, l = x / hyp[0], x_ / hyp[0], None
+        else:
+            l = hyp[0]
+        if se_expanded:
+            na = torch.sum(x * x, -1, keepdim=True)
+            nb = torch.sum(x_ * x_, -1, keepdim=True)
+            dist = torch.sqrt((na - 2.0 * (x @ x_.T)) + nb.T)
+            s = dist * dist
+        else:
+            s = _sq(x, x_)
+        r = torch.exp(-0.5 * s) if l is None else torch.exp(-0.5 * (s / (l * l)))
+        return hyp[1] * r if scaled else r
+    if op in ("MAT32", "MAT52"):
+        if ard:
+            x, x_, l = x / hyp[0], x_ / hyp[0], None
+        else:
+            l = torch.abs(hyp[0])
+        if opts.get("standard", False):
+            s = _sq(x, x_)
+            # sqrt at 0 has an infinite derivative; the distance itself does not depend on
+            # the hyperparameters unless ARD, where d sqrt(s)/d l is finite away from s = 0
+            dist = torch.sqrt(torch.clamp(s, min=1e-300)) * (s > 0)
+        else:
+            dist = _l1(x, x_)
+        c = math.sqrt(5.0) if op == "MAT52" else math.sqrt(3.0)
+        frac = (c * dist) if l is None else (c * dist) / l
+        if op == "MAT52":
+            third = (5.0 * (dist * dist)) / 3.0 if l is None else (5.0 * (dist * dist)) / (3.0 * (l * l))
+            r = ((1.0 + frac) + third) * torch.exp(-frac)
+        else:
+            r = (1.0 + frac) * torch.exp(-frac)
+        return hyp[1] * r if scaled else r
+    if op == "PER":
+        l, p = hyp[0], hyp[1]
+        if opts.get("standard", False):
+            dd = torch.abs(x[:, None, :] - x_[None, :, :])
+            sd = torch.sin(math.pi * (dd / p))
+            sine = torch.sum(sd * sd, dim=-1)
+        else:
+            sine = torch.sin(math.pi * (_l1(x, x_) / p))
+            sine = sine * sine
+        r = torch.exp((-2.0 * sine) / (l * l))
+        return hyp[2] * r if scaled else r
+    raise ValueError(op)
+
+
+def _kmat(tree, hyp, x, x_, scaled, se_expanded):
+    op, arg = tree
+    if op in ("ADD", "MUL"):
+        idx, res = 0, None
+        for child in arg:
+            k = _n_hyp(child, scaled)
+            m = _kmat(child, hyp[idx:idx + k], x, x_, scaled, se_expanded)
+            idx += k
+            res = m if res is None else (res + m if op == "ADD" else res * m)
+        return res
+    return _base(op, arg, hyp, x, x_, scaled, se_expanded)
+
+
+def nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, scaled: bool = False,
+                  se_expanded: bool = False) -> Tuple[float, List[np.ndarray], float]:
+    """(-LML, [d/d h for h in hyp] shaped like h, d/d noise) by torch reverse mode on the CPU."""
+    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
+    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
+    X = torch.as_tensor(np.asarray(x, dtype=np.float64))
+    Y = torch.as_tensor(np.asarray(y, dtype=np.float64)).reshape(-1, 1)
+    n = X.shape[0]
+    K = _kmat(tree, params, X, X, scaled, se_expanded) + nz * torch.eye(n, dtype=F64)
+    L = torch.linalg.cholesky(K)
+    z = torch.linalg.solve_triangular(L, Y, upper=False)
+    alpha = torch.linalg.solve_triangular(L.T, z, upper=True)
+    fit = (Y.T @ alpha)[0, 0]
+    logdet = 2.0 * torch.sum(torch.log(torch.diagonal(L)))
+    nl = -((-0.5 * fit + -0.5 * logdet) + (-0.5 * (n * LOG_2PI)))
+    grads = torch.autograd.grad(nl, params + [nz])
+    return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1])
+
+
+def finite_difference(f, hyp: Sequence, noise: float, h: float = 1e-5):
+    """Central differences of f(hyp, noise) -> float over every scalar of hyp and noise."""
+    flat = [np.atleast_1d(np.asarray(v, dtype=np.float64)).copy() for v in hyp]
+    out = []
+    for i, v in enumerate(flat):
+        g = np.zeros_like(v)
+        for j in range(v.size):
+            step = h * max(1.0, abs(v[j]))
+            vp, vm = [u.copy() for u in flat], [u.copy() for u in flat]
+            vp[i][j] += step
+            vm[i][j] -= step
+            unpack = lambda vs: [u if np.ndim(hyp[k]) else float(u[0]) for k, u in enumerate(vs)]
+            g[j] = (f(unpack(vp), noise) - f(unpack(vm), noise)) / (2 * step)
+        out.append(g.reshape(np.shape(hyp[i])))
+    step = h * max(1.0, abs(noise))
+    unpack0 = [u if np.ndim(hyp[k]) else float(u[0]) for k, u in enumerate(flat)]
+    gn = (f(unpack0, noise + step) - f(unpack0, noise - step)) / (2 * step)
+    return out, gn
