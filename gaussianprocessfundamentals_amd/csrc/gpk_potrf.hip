@@ -68,6 +68,29 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 }
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// buffer loads / stores of one element (voffset per lane, soffset wave-uniform)
+template <typename T>
+struct BufIO;
+template <>
+struct BufIO<double> {
+  typedef decltype(__builtin_amdgcn_raw_buffer_load_b64(__amdgpu_buffer_rsrc_t(), 0, 0, 0)) raw_t;
+  static __device__ __forceinline__ double load(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
+  }
+  static __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t rs, int vo, int so, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(raw_t, v), rs, vo, so, 0);
+  }
+};
+template <>
+struct BufIO<float> {
+  static __device__ __forceinline__ float load(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0));
+  }
+  static __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t rs, int vo, int so, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rs, vo, so, 0);
+  }
+};
+
 // One 256-thread workgroup computes a TM x TN tile: acc = A_rows(TM x K) * B_rows(TN x K)^T,
 // K = the panel depth.  Waves 2 x 2, each (TM/2) x (TN/2) = MB x NBK blocks of 16 x 16.
 // Staging: global_load_lds (16 B per lane, no VGPR round trip) into two LDS stages; the chunk
@@ -149,11 +172,41 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
         glds16(src[i] + (int64_t)(kc) * GBK, smem + (stage) * STAGE + (wid * PW + i) * 1024);   \
   }
 
+#ifndef GPK_CFIRST
+#define GPK_CFIRST 1  // f64 update: C loaded into the accumulators before the K loop (A negated)
+#endif
+  // C first (f64): the C read overlaps the first chunk's staging instead of following the last
+  // MFMA, and the epilogue is stores only (+3 % update rate at N = 8192; neutral for f32)
+  constexpr bool CFIRST = (MODE == GEMM_UPDATE) && GPK_CFIRST && sizeof(T) == 8;
+  const int col = lane & 15;
+  // C tile through a buffer descriptor: one 32-bit per-lane offset (VGPR) plus, for block (m, n)
+  // and register r, the wave-uniform byte offset ((m 16 + r RSTEP) ld + n 16) sizeof(T) in an
+  // SGPR (rows of the C/D layout: row(lane, r) = row(lane, 0) + r RSTEP) -- no 64-bit address
+  // per access, which the 64 loads and stores of the epilogue would otherwise hold in VGPRs
+  T* const C = (MODE == GEMM_UPDATE) ? W + R * a.ld + a.row0 + tj * TN : W + R * a.ld + a.j0;
+  const uint64_t cu = reinterpret_cast<uint64_t>(C);
+  const uint64_t cuu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(cu >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cu);
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(cuu), 0, (int)(TM * a.ld * (int64_t)sizeof(T)), 0x00020000);
+  const int cvo = (int)(((int64_t)(wr * (TM / 2) + Mfma<T>::row(lane, 0)) * a.ld + wc * (TN / 2) + col) *
+                        (int64_t)sizeof(T));
+  constexpr int RSTEP = sizeof(T) == 8 ? 4 : 1;
+  const int ldb_s = wave_uniform((int)(a.ld * (int64_t)sizeof(T)));
+#define GPK_CSOFF(m, n, r) (((m) * 16 + (r) * RSTEP) * ldb_s + (n) * 16 * (int)sizeof(T))
+
   acc_t acc[MB][NBK];
 #pragma unroll
   for (int m = 0; m < MB; ++m)
 #pragma unroll
-    for (int n = 0; n < NBK; ++n) acc[m][n] = acc_t{0, 0, 0, 0};
+    for (int n = 0; n < NBK; ++n) {
+      if (CFIRST) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[m][n][r] = BufIO<T>::load(crs, cvo, GPK_CSOFF(m, n, r));
+      } else {
+        acc[m][n] = acc_t{0, 0, 0, 0};
+      }
+    }
 
   const int q = lane >> 4, lr = lane & 15;
   const int aoff = (wr * (TM / 2) + lr) * ROWB;
@@ -170,7 +223,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
     const int st = kc & 1;
     // one barrier per chunk, at the top: it retires the chunk kc glds (vmcnt(0), issued a whole
     // MFMA phase earlier) and frees stage st ^ 1, read during chunk kc - 1.  (At the bottom
-    // hipcc hoists it above the MFMAs, exposing the load latency.)
+    // hipcc hoists it above the MFMAs, exposing the load latency.)  The vmcnt(0) is explicit:
+    // hipcc's wait insertion does not always see the LDS write of global_load_lds across the
+    // loop back edge (it dropped it once the C loads were issued ahead of the loop).
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt(7), lgkmcnt(15)
     __syncthreads();
     if (kc + 1 < NK) GPK_GLDS(st ^ 1, (kc + 1) % NK0);
     const char* sb = smem + st * STAGE;
@@ -179,6 +235,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
     for (int m = 0; m < MB; ++m) {
       fa[m][0] = *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + p0);
       fa[m][1] = *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + p1);
+      if (CFIRST) {
+        fa[m][0] = -fa[m][0];
+        fa[m][1] = -fa[m][1];
+      }
     }
 #pragma unroll
     for (int n = 0; n < NBK; ++n) {
@@ -198,19 +258,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
   }
 #undef GPK_GLDS
 
-  const int col = lane & 15;
-  T* C = (MODE == GEMM_UPDATE) ? W + R * a.ld + a.row0 + tj * TN : W + R * a.ld + a.j0;
-  T* cp[MB][NBK];
-#pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int n = 0; n < NBK; ++n)
-      cp[m][n] = C + (int64_t)(wr * (TM / 2) + m * 16 + Mfma<T>::row(lane, 0)) * a.ld +
-                 wc * (TN / 2) + n * 16 + col;
-  // rows of the C/D layout: row(lane, r) = row(lane, 0) + r * RSTEP
-  constexpr int RSTEP = sizeof(T) == 8 ? 4 : 1;
   if (GPK_ABLATE == 2 && acc[0][0][0] != (T)12345.678) return;
-  if (MODE == GEMM_UPDATE && GPK_ABLATE != 1) {
+  if (MODE == GEMM_UPDATE && GPK_ABLATE != 1 && !CFIRST) {
     // every C value is loaded before the first store: interleaved load/store pairs may alias,
     // so hipcc would wait for each load in turn (64 dependent HBM round trips per tile)
 #pragma unroll
@@ -218,14 +267,15 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int n = 0; n < NBK; ++n)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[m][n][r] = cp[m][n][(int64_t)r * RSTEP * a.ld] - acc[m][n][r];
+        for (int r = 0; r < 4; ++r) acc[m][n][r] = BufIO<T>::load(crs, cvo, GPK_CSOFF(m, n, r)) - acc[m][n][r];
   }
 #pragma unroll
   for (int m = 0; m < MB; ++m)
 #pragma unroll
     for (int n = 0; n < NBK; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cp[m][n][(int64_t)r * RSTEP * a.ld] = acc[m][n][r];
+      for (int r = 0; r < 4; ++r) BufIO<T>::store(crs, cvo, GPK_CSOFF(m, n, r), acc[m][n][r]);
+#undef GPK_CSOFF
 }
 
 // ================================================================================ read-out
