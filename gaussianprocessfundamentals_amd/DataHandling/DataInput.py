@@ -167,3 +167,43 @@ class BatchDataInput(AbstractDataInput):
         if data_x_test is not None and data_y_test is not None:
             data_x_test, data_y_test = _f64(data_x_test), _f64(data_y_test)
         super().__init__(_f64(data_x_train), _f64(data_y_train), data_x_test, data_y_test, test_ratio, seed)
+
+
+class PartitionedDataInput(DataInput):
+    """A data set together with the DataInput of each of its partitions (DataInput.py:191-207).
+    The partitions are what SegmentedCovarianceMatrix factors as one ragged device batch."""
+
+    def __init__(self, data_x_train, data_y_train, data_x_test, data_y_test, data_inputs: List[DataInput]):
+        super().__init__(data_x_train, data_y_train, data_x_test, data_y_test)
+        self.data_inputs: List[DataInput] = list(data_inputs)
+
+    def set_mean_function(self, mean_function):
+        """Also sets the mean function of every partition (DataInput.py:197-207)."""
+        super().set_mean_function(mean_function)
+        for d in self.data_inputs:
+            d.set_mean_function(mean_function)
+
+
+class BlockwiseDataInput(PartitionedDataInput):
+    """Segments of a 1-D data set split at change points (DataInput.py:210-253): segment i holds
+    the records with cp_{i-1} <= x < cp_i (open-ended at both ends)."""
+
+    def __init__(self, data_x_train, data_y_train, data_x_test, data_y_test, change_points: List):
+        xtr, ytr = _f64(data_x_train), _f64(data_y_train)
+        xte, yte = _f64(data_x_test), _f64(data_y_test)
+        cps = [float(torch.as_tensor(c, dtype=torch.float64).reshape(())) for c in change_points]
+        blocks = []
+        for i in range(len(cps) + 1):
+            lo = cps[i - 1] if i > 0 else None
+            hi = cps[i] if i < len(cps) else None
+
+            def sel(x):
+                m = torch.ones(x.shape[0], dtype=torch.bool, device=x.device)
+                if hi is not None:
+                    m &= (x < hi).any(dim=1)
+                if lo is not None:
+                    m &= (x >= lo).any(dim=1)
+                return torch.nonzero(m).flatten()
+            tr, te = sel(xtr), sel(xte)
+            blocks.append(DataInput(xtr[tr], ytr[tr], xte[te], yte[te]))
+        super().__init__(xtr, ytr, xte, yte, blocks)

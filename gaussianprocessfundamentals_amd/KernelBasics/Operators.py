@@ -6,7 +6,10 @@ reference's ``result = op(result, child_i)`` loops (Operators.py:214-223, :314-3
 Hyperparameters are one flat list in child DFS order, sliced by each child's
 ``get_number_of_hyper_parameter`` (Operators.py:28-32).
 
-Out of scope: ChangePointOperator (Operators.py:370-681), PartitionOperator.
+ChangePointOperator (Operators.py:370-681) splits the (1-D) input axis at its change points; its
+matrix is the sum of the child matrices masked by the segment indicators, and its hyperparameters
+are the change points followed by the children's.  The segmented LML path does not build that
+matrix at all: SegmentedCovarianceMatrix factors the segments as one ragged device batch.
 """
 from __future__ import annotations
 
@@ -197,3 +200,187 @@ class AdditionOperator(Operator):
         for cn in (c.get_simplified_version() for c in self.child_nodes):
             flat.extend(cn.child_nodes if isinstance(cn, AdditionOperator) else [cn])
         return AdditionOperator(self.input_dimensionality, flat)
+
+
+class ChangePointOperator(Operator):
+    """Change-point operator (Operators.py:370-681).
+
+    K = sum_i K_i * (a_i a_i'^T), a_i(x) = (1 - ind_{i-1}(x)) ind_i(x) with ind_i the indicator of
+    x < cp_i (ind_{-1} = 0, ind_last = 1) -- the product of the mask outer products that
+    get_cp_encapsulated_kernel applies child by child (:410-440).  The indicator follows
+    ``global_parameters.p_cp_operator_type``: INDICATOR (default, :397-400), SIGMOID (:387-394) or
+    APPROX_INDICATOR (:379-385).  Every child matrix comes from the device kernel-matrix build; the
+    masks are applied on the device.
+    """
+    operator_sign = "]["
+
+    def __init__(self, input_dimensionality: int, child_nodes: List[k.Kernel], change_point_positions: List):
+        super().__init__(k.KernelManifestation.CP, input_dimensionality, child_nodes)
+        assert (len(child_nodes) - 1) == len(change_point_positions), \
+            "Error. Change Point positions and/or their positions wrongly initialized."
+        self.change_point_positions = list(change_point_positions)
+        self.sortable = False
+
+    def _emit(self, nodes: list, offset: int, ard_slots: list, dim: int) -> int:
+        if len(self.child_nodes) == 1:
+            return self.child_nodes[0]._emit(nodes, offset, ard_slots, dim)
+        raise NotImplementedError("a ChangePointOperator is evaluated segment by segment (masked child "
+                                  "matrices / SegmentedCovarianceMatrix), not as one device program")
+
+    @staticmethod
+    def _mask(x: torch.Tensor, cp) -> torch.Tensor:
+        xv = x.reshape(-1)
+        c = torch.as_tensor(cp, dtype=torch.float64, device=xv.device).reshape(())
+        t = global_param.p_cp_operator_type
+        if t == global_param.ChangePointOperatorType.SIGMOID:
+            return 0.5 * (1 + torch.tanh((c - xv) / 0.0025))
+        if t == global_param.ChangePointOperatorType.APPROX_INDICATOR:
+            return 1.0 / (1.0 + torch.exp(-100.0 * (xv - c)))
+        return (xv < c).to(torch.float64)
+
+    def get_tf_tensor(self, hyper_parameter: List, x_vector, x_vector_) -> torch.Tensor:
+        assert x_vector is not None and x_vector_ is not None, "Input vectors x and x_ uninitialized: " + str(self)
+        assert len(hyper_parameter) == self.get_number_of_hyper_parameter(), "Invalid hyper_param size: %s" % str(self)
+        if len(self.child_nodes) == 1:
+            return self.child_nodes[0].get_tf_tensor(hyper_parameter, x_vector, x_vector_)
+        from .. import engine
+        x = engine.as_device_f64(x_vector)
+        x_ = engine.as_device_f64(x_vector_)
+        ncp = len(self.change_point_positions)
+        cps = list(hyper_parameter[:ncp])
+        idx = ncp
+        prev, prev_ = torch.ones(x.shape[0], dtype=torch.float64, device=x.device), \
+            torch.ones(x_.shape[0], dtype=torch.float64, device=x.device)
+        result = None
+        for i, cn in enumerate(self.child_nodes):
+            nh = cn.get_number_of_hyper_parameter()
+            Ki = cn.get_tf_tensor(list(hyper_parameter[idx:idx + nh]), x, x_)
+            idx += nh
+            if i < ncp:
+                ind, ind_ = self._mask(x, cps[i]), self._mask(x_, cps[i])
+                a, a_ = prev * ind, prev_ * ind_
+                prev, prev_ = 1.0 - ind, 1.0 - ind_
+            else:
+                a, a_ = prev, prev_
+            term = Ki * (a[:, None] * a_[None, :])
+            result = term if result is None else result + term
+        self.last_hyper_parameter = cps
+        return result
+
+    get_tensor = get_tf_tensor
+
+    def _slices(self, hyper_parameter: List):
+        idx = len(self.change_point_positions)
+        for cn in self.child_nodes:
+            cnt = cn.get_number_of_hyper_parameter()
+            yield cn, list(hyper_parameter[idx:idx + cnt])
+            idx += cnt
+
+    def _record_hyper_parameter(self, hyper_parameter: List):
+        if len(self.child_nodes) == 1:
+            self.child_nodes[0]._record_hyper_parameter(hyper_parameter)
+            return
+        for cn, sl in self._slices(hyper_parameter):
+            cn._record_hyper_parameter(sl)
+
+    def get_number_of_hyper_parameter(self) -> int:
+        return sum(cn.get_number_of_hyper_parameter() for cn in self.child_nodes) + len(self.change_point_positions)
+
+    def get_hyper_parameter_dimensionalities(self) -> List[list]:
+        return [[len(self.change_point_positions), ]] + super().get_hyper_parameter_dimensionalities()
+
+    def set_last_hyper_parameter(self, last_hyper_parameter: List):
+        assert len(last_hyper_parameter) == self.get_number_of_hyper_parameter(), \
+            "Invalid hyper_param size: %s" % str(last_hyper_parameter)
+        if len(self.child_nodes) == 1:
+            self.child_nodes[0].set_last_hyper_parameter(last_hyper_parameter)
+            return
+        self.change_point_positions = list(last_hyper_parameter[0:len(self.change_point_positions)])
+        self.last_hyper_parameter = self.change_point_positions
+        for cn, sl in self._slices(last_hyper_parameter):
+            cn.set_last_hyper_parameter(sl)
+
+    def get_last_hyper_parameter(self, scaling_x_param=None):
+        out = []
+        for cn in self.child_nodes:
+            out.extend(cn.get_last_hyper_parameter(scaling_x_param))
+        return list(self.change_point_positions) + out
+
+    def add_kernel(self, kernel: k.Kernel, new_cp_position=None):
+        assert kernel is not None, "Adding None as kernel to ChangePoint is not allowed."
+        assert new_cp_position is not None
+        if self.change_point_positions:
+            assert float(torch.as_tensor(new_cp_position).min()) > \
+                float(torch.as_tensor(self.change_point_positions[-1]).max()), \
+                "New Changepoints _must_ be larger in value than the former largest change point."
+        self.child_nodes.append(kernel)
+        self.change_point_positions.append(new_cp_position)
+
+    def add_preceding_kernel(self, kernel, new_cp_position):
+        assert kernel is not None, "Adding None as kernel to ChangePoint is not allowed."
+        assert new_cp_position is not None
+        if self.change_point_positions:
+            assert float(torch.as_tensor(self.change_point_positions[-1]).min()) > \
+                float(torch.as_tensor(new_cp_position).max()), \
+                "New Changepoints _must_ be larger in value than the former largest change point."
+        self.child_nodes = [kernel] + self.child_nodes
+        self.change_point_positions = [new_cp_position] + self.change_point_positions
+
+    def get_default_hyper_parameter(self, xrange, n, from_distribution: bool = False) -> List:
+        return list(self.change_point_positions) + super().get_default_hyper_parameter(xrange, n, from_distribution)
+
+    def get_hyper_parameter_bounds(self, xrange, n) -> List[tuple]:
+        span = xrange[0][1] - xrange[0][0]
+        lo, hi = xrange[0][0] - 1.5 * span, xrange[0][1] + 1.5 * span
+        return [(lo, hi)] * len(self.change_point_positions) + super().get_hyper_parameter_bounds(xrange, n)
+
+    def get_simplified_kernel(self, data_range: List[float]):
+        """Drop change points outside the data range or overtaken by their successor, with the
+        children they separate (Operators.py:533-582); returns (kernel, changed)."""
+        cps = [float(torch.as_tensor(c)) for c in self.change_point_positions]
+        blur = 4 if global_param.p_cp_operator_type == global_param.ChangePointOperatorType.SIGMOID else 0
+        del_cp, del_cn = [], []
+        for i, c in enumerate(cps):
+            if c >= data_range[1] + blur:
+                del_cp.append(i)
+                del_cn.append(i + 1)
+            if c <= data_range[0] - blur:
+                del_cp.append(i)
+                del_cn.append(i)
+            if len(cps) - 1 > i and c >= cps[i + 1]:
+                del_cp.append(i)
+                del_cn.append(i + 1)
+        if not del_cp:
+            return self, False
+        new_cps = [self.change_point_positions[i] for i in range(len(cps)) if i not in del_cp]
+        new_cn = [cn for i, cn in enumerate(self.child_nodes) if i not in del_cn]
+        assert len(new_cps) + 1 == len(new_cn), \
+            "Error in get_simplified_kernel, new_change_points: %s, new_child_nodes: %s" % (new_cps, new_cn)
+        return ChangePointOperator(self.input_dimensionality, new_cn, new_cps), True
+
+    def get_json(self) -> dict:
+        if len(self.child_nodes) == 1:
+            return {"type": self.manifestation.name, "child_nodes": [self.child_nodes[0].get_json()]}
+        nodes = []
+        cps = [float(torch.as_tensor(c)) for c in self.change_point_positions]
+        for i, cn in enumerate(self.child_nodes):
+            j = cn.get_json()
+            j["start_index"] = 0 if i == 0 else cps[i - 1]
+            j["stop_index"] = 1.0 if i == len(cps) else cps[i]
+            nodes.append(j)
+        return {"type": self.manifestation.name, "child_nodes": nodes}
+
+    def get_simplified_version(self):
+        return ChangePointOperator(self.input_dimensionality, [cn.get_simplified_version() for cn in self.child_nodes],
+                                   self.change_point_positions)
+
+    def deepcopy(self):
+        c = ChangePointOperator(self.input_dimensionality, [cn.deepcopy() for cn in self.child_nodes],
+                                [torch.as_tensor(cp).clone() if isinstance(cp, torch.Tensor) else cp
+                                 for cp in self.change_point_positions])
+        if self.noise is not None:
+            c.set_noise(self.noise)
+        return c
+
+    def get_hash_tuple(self):
+        return super().get_hash_tuple() + tuple(hash(cn) for cn in self.child_nodes)

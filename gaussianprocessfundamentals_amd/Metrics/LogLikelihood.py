@@ -124,6 +124,55 @@ class _NegLogLikelihood(torch.autograd.Function):
         return tuple(res)
 
 
+def blockwise_hyper_parameter_offset(_gp) -> int:
+    """Offset of the first constituent's hyperparameters in a blockwise metric's hyperparameter
+    list.  Quirk kept: the reference tests ``hasattr(_gp, 'change_point_positions')``
+    on the GP object (LogLikelihood.py:80-83, MeanSquaredError.py:64-67), which no GP object has,
+    so the offset is always 0 -- even for a change-point kernel whose change points lead its list."""
+    return len(_gp.covariance_matrix.kernel.change_point_positions) if hasattr(_gp, "change_point_positions") else 0
+
+
 class BlockwiseLogLikelihood(AbstractMetric):
-    def __init__(self, *args, **kwargs):
-        raise NotImplementedError("blockwise likelihood is SURVEY §8f 'next' (variable-size batched potrf)")
+    """Sum of the constituent GPs' -LML (LogLikelihood.py:68-104).
+
+    The reference evaluates one LogLikelihood per segment, one TensorFlow Cholesky after another;
+    here all segments are factored by ONE ragged device batch (engine.RaggedFactorization), each
+    segment with its own kernel, hyperparameter slice and detrended targets.  Segments without
+    training points contribute 0 (an empty Cholesky).  Returns a [1, 1] tensor like LogLikelihood."""
+
+    def __init__(self, _gp, local_approx, numerical_matrix_handling, subset_size: int = None):
+        if local_approx is not mht.MatrixApproximations.NONE:
+            raise NotImplementedError("approximation %s is SURVEY §8f.4; the device engine is exact" % local_approx)
+        if numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
+            raise NotImplementedError("numerical handling %s is SURVEY §8f.4" % numerical_matrix_handling)
+        self.local_approx = local_approx
+        self.numerical_matrix_handling = numerical_matrix_handling
+        self.subset_size = subset_size
+        self._gp = _gp
+
+    def segment_factorization(self, hyper_parameter: List, noise):
+        from ..Statistics.CovarianceMatrix import factor_segments
+        index = blockwise_hyper_parameter_offset(self._gp)
+        kernels, slices, dis = [], [], []
+        for sub in self._gp.constituent_gps:
+            kern = sub.covariance_matrix.kernel
+            nh = kern.get_number_of_hyper_parameter()
+            kernels.append(kern)
+            slices.append(list(hyper_parameter[index:index + nh]))
+            dis.append(sub.data_input)
+            index += nh
+        return factor_segments(kernels, slices, dis, noise)
+
+    def get_metric(self, hyper_parameter: List, noise, indices=None, reset: bool = True) -> torch.Tensor:
+        f, _ = self.segment_factorization(hyper_parameter, noise)
+        for sub in self._gp.constituent_gps:
+            sub.covariance_matrix.reset()
+            sub.aux.reset()
+        if f is None:
+            return torch.zeros((1, 1), dtype=torch.float64, device=_device())
+        return torch.sum(f.nlml()).reshape(1, 1)
+
+
+def _device():
+    from .. import engine
+    return engine.device()

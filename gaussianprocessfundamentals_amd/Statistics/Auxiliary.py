@@ -99,5 +99,67 @@ class HolisticAuxiliaryGpProperties(AuxiliaryGpProperties):
         return self.posterior_sd
 
 
+def _segment_posterior(kernels, hyper_parameters, data_inputs, noise):
+    from .CovarianceMatrix import factor_segments
+    f, index = factor_segments(kernels, hyper_parameters, data_inputs, noise, with_test=True)
+    if f is not None:
+        f.check_info()
+    return f, index
+
+
+def segment_posterior_mu(kernels, hyper_parameters, data_inputs, noise) -> torch.Tensor:
+    """Posterior means of independent segments concatenated in segment order [sum M_i]
+    (the constituent-GP loop of GaussianProcess.predict, gpbasics/Statistics/GaussianProcess.py:64-77),
+    from ONE ragged factorisation with the test points as extra rows.  A segment without training
+    points has K_s of shape [0, M_i] and so a zero mean."""
+    f, index = _segment_posterior(kernels, hyper_parameters, data_inputs, noise)
+    parts = [torch.zeros(di.n_test, dtype=torch.float64, device=engine.device()) for di in data_inputs]
+    for j, i in enumerate(index):
+        parts[i] = f.posterior_mu(j).clone()
+    return torch.cat(parts) if parts else torch.zeros(0, dtype=torch.float64, device=engine.device())
+
+
 class BlockwiseAuxiliaryGpProperties(HolisticAuxiliaryGpProperties):
-    pass
+    """Posterior of a segmented GP (Auxiliary.py:106-107 inherits the holistic formulas, which over
+    a SegmentedCovarianceMatrix amount to the per-segment posteriors in segment order).  All segments
+    come out of one ragged factorisation: mu concatenated, the covariance block-diagonal."""
+
+    def _segments(self, hyper_parameter, noise):
+        if self._post is None:
+            cm = self.covariance_matrix
+            self._post = _segment_posterior(cm.kernel.child_nodes, cm._slices(hyper_parameter),
+                                            self.data_input.data_inputs, noise)
+        return self._post
+
+    def get_posterior_mu(self, hyper_parameter: List, noise):
+        if self.data_input is None:
+            return None
+        if self.posterior_mu is None:
+            cm = self.covariance_matrix
+            self.posterior_mu = segment_posterior_mu(cm.kernel.child_nodes, cm._slices(hyper_parameter),
+                                                     self.data_input.data_inputs, noise)
+        return self.posterior_mu
+
+    def get_posterior_var(self, hyper_parameter: List, noise):
+        if self.data_input is None:
+            return None
+        if self.posterior_var is None:
+            f, index = self._segments(hyper_parameter, noise)
+            dis = self.data_input.data_inputs
+            blocks = []
+            for i, di in enumerate(dis):
+                if i in index:
+                    blocks.append(f.corner(index.index(i)).to(torch.float64))
+                else:  # no training points: the prior K_ss
+                    cm = self.covariance_matrix
+                    blocks.append(cm.kernel.child_nodes[i].get_tf_tensor(cm._slices(hyper_parameter)[i],
+                                                                        di.data_x_test, di.data_x_test)
+                                  if di.n_test > 0 else None)
+            self.posterior_var = self.covariance_matrix._block_diag(blocks)
+        return self.posterior_var
+
+    def get_posterior_var_diag(self, hyper_parameter: List, noise):
+        return torch.diagonal(self.get_posterior_var(hyper_parameter, noise)).clone()
+
+    def get_inverse_cholesky_k_times_k_s(self, hyper_parameter: List, noise):
+        raise NotImplementedError("inv(L) K_s of a segmented GP: use get_posterior_var (block-diagonal)")

@@ -248,3 +248,242 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
             f.check_info()
             self.L_K_ss = f.cholesky(0).to(torch.float64)
         return self.L_K_ss
+
+
+# ============================================================================ segmented (blockwise)
+def factor_segments(kernels, hyper_parameters, data_inputs, noise, with_test: bool = False):
+    """ONE ragged device factorisation (engine.RaggedFactorization) of the independent segments
+    (kernel_i, hyp_i, data_input_i); segments without training points are left out.  Returns
+    (factorisation or None, index of the segment behind each batch member).
+
+    The reference factors the segments one after another, one TensorFlow Cholesky each
+    (SegmentedCovarianceMatrix.get_L_K_blocks / get_L_alpha_blocks, CovarianceMatrix.py:445-484;
+    BlockwiseLogLikelihood.get_metric, gpbasics/Metrics/LogLikelihood.py:76-104)."""
+    if not _is_scalar(noise):
+        raise Exception("Invalid Noise given")
+    members, index = [], []
+    dims = {int(di.data_x_train.shape[1]) for di in data_inputs}
+    if len(dims) != 1:
+        raise ValueError("segments must share the input dimensionality")
+    d = dims.pop()
+    for i, (kern, hyp, di) in enumerate(zip(kernels, hyper_parameters, data_inputs)):
+        if di.n_train == 0:
+            continue
+        kd = engine.kernel_descriptor(kern, d)
+        h = engine.pack_hyper_parameter(hyp, kd.n_hyp)
+        y = di.get_detrended_y_train().reshape(-1).to(torch.float64)
+        xs = di.data_x_test.contiguous() if with_test and di.n_test > 0 else None
+        members.append((kd, h, di.data_x_train.contiguous(), y, xs))
+        index.append(i)
+        kern._record_hyper_parameter(list(hyp))
+    if not members:
+        return None, index
+    sizes = [int(m[2].shape[0]) for m in members]
+    tsz = [int(m[4].shape[0]) if m[4] is not None else 0 for m in members] if with_test else None
+    f = engine.RaggedFactorization(sizes, d, tsz, global_param.p_dtype)
+    f.run(members, noise_vector(noise))
+    return f, index
+
+
+class SegmentedCovarianceMatrix(CovarianceMatrix):
+    """Block-diagonal covariance of a change-point / partition operator whose segments are
+    independent local models (CovarianceMatrix.py:289-565).  Every ``get_*_blocks`` returns one
+    entry per child (None for an empty segment) and the plain getters the block-diagonal matrix
+    (rows regrouped segment by segment, as LinearOperatorBlockDiag.to_dense does).  All segments are
+    factored together by one ragged device batch (:func:`factor_segments`)."""
+
+    def __init__(self, kernel):
+        super().__init__(CovarianceMatrixType.SEGMENTED, kernel)
+        self._seg = None
+
+    def reset(self):
+        super().reset()
+        self._seg = None
+
+    def set_data_input(self, data_input):
+        assert len(data_input.data_inputs) == len(self.kernel.child_nodes), \
+            "Invalid data input. Data input does not match segments prescribed by given kernel"
+        super().set_data_input(data_input)
+
+    def _require_data(self):
+        if self.data_input is None:
+            raise Exception("No Data Input given")
+
+    def _slices(self, hyper_parameter):
+        """Per child: its hyperparameters, after the change points of a ChangePointOperator
+        (CovarianceMatrix.py:318-335)."""
+        idx = len(self.kernel.change_point_positions) if hasattr(self.kernel, "change_point_positions") else 0
+        out = []
+        for cn in self.kernel.child_nodes:
+            nh = cn.get_number_of_hyper_parameter()
+            out.append(list(hyper_parameter[idx:idx + nh]))
+            idx += nh
+        return out
+
+    @staticmethod
+    def _block_diag(blocks):
+        present = [b for b in blocks if b is not None]
+        return torch.block_diag(*present) if present else \
+            torch.zeros((0, 0), dtype=torch.float64, device=engine.device())
+
+    def segment_factorization(self, hyper_parameter, noise):
+        """The ragged factorisation of all segments (memoised until reset)."""
+        self._require_data()
+        if self._seg is None:
+            self._seg = factor_segments(self.kernel.child_nodes, self._slices(hyper_parameter),
+                                        self.data_input.data_inputs, noise)
+        return self._seg
+
+    def _per_segment(self, values_by_member, index):
+        out = [None] * len(self.kernel.child_nodes)
+        for j, i in enumerate(index):
+            out[i] = values_by_member[j]
+        return out
+
+    # -- kernel matrices ------------------------------------------------------------------------
+    def get_K_blocks(self, hyper_parameter) -> List:
+        self._require_data()
+        out = []
+        for cn, hyp, di in zip(self.kernel.child_nodes, self._slices(hyper_parameter), self.data_input.data_inputs):
+            out.append(cn.get_tf_tensor(hyp, di.data_x_train, di.data_x_train) if di.n_train > 0 else None)
+        return out
+
+    def get_K(self, hyper_parameter: List) -> torch.Tensor:
+        self._require_data()
+        if self.K is None:
+            self.K = self._block_diag(self.get_K_blocks(hyper_parameter))
+        return self.K
+
+    def get_K_noised_blocks(self, hyper_parameter, noise) -> List:
+        if not _is_scalar(noise):
+            raise Exception("Invalid Noise given")
+        self._require_data()
+        nv = float(torch.as_tensor(noise))
+        out = []
+        for cn, hyp, di in zip(self.kernel.child_nodes, self._slices(hyper_parameter), self.data_input.data_inputs):
+            out.append(engine.kernel_matrix(cn, hyp, di.data_x_train, di.data_x_train, nv) if di.n_train > 0 else None)
+        return out
+
+    def get_K_noised(self, hyper_parameter: List, noise) -> torch.Tensor:
+        self._require_data()
+        if self.noised_K is None:
+            self.noised_K = self._block_diag(self.get_K_noised_blocks(hyper_parameter, noise))
+        return self.noised_K
+
+    def get_K_ss_blocks(self, hyper_parameter) -> List:
+        self._require_data()
+        out = []
+        for cn, hyp, di in zip(self.kernel.child_nodes, self._slices(hyper_parameter), self.data_input.data_inputs):
+            out.append(cn.get_tf_tensor(hyp, di.data_x_test, di.data_x_test) if di.n_test > 0 else None)
+        return out
+
+    def get_K_ss(self, hyper_parameter: List) -> torch.Tensor:
+        self._require_data()
+        if self.K_ss is None:
+            self.K_ss = self._block_diag(self.get_K_ss_blocks(hyper_parameter))
+        return self.K_ss
+
+    def get_K_ss_noised_blocks(self, hyper_parameter, noise) -> List:
+        if not _is_scalar(noise):
+            raise Exception("Invalid noise provided")
+        self._require_data()
+        nv = float(torch.as_tensor(noise))
+        out = []
+        for cn, hyp, di in zip(self.kernel.child_nodes, self._slices(hyper_parameter), self.data_input.data_inputs):
+            out.append(engine.kernel_matrix(cn, hyp, di.data_x_test, di.data_x_test, nv) if di.n_test > 0 else None)
+        return out
+
+    def get_K_ss_noised(self, hyper_parameter: List, noise) -> torch.Tensor:
+        self._require_data()
+        if self.noised_K_ss is None:
+            self.noised_K_ss = self._block_diag(self.get_K_ss_noised_blocks(hyper_parameter, noise))
+        return self.noised_K_ss
+
+    def get_L_K_ss_blocks(self, hyper_parameter, noise) -> List:
+        """Cholesky of every K_ss + noise I block: one ragged factorisation of the test segments."""
+        self._require_data()
+        from ..DataHandling.DataInput import DataInput
+        from ..MeanFunctionBasics.BaseMeanFunctions import ZeroMeanFunction
+        tests = []
+        for di in self.data_input.data_inputs:
+            xt = di.data_x_test
+            dtest = DataInput(xt, torch.zeros((xt.shape[0], 1), dtype=torch.float64, device=xt.device), xt,
+                              torch.zeros((xt.shape[0], 1), dtype=torch.float64, device=xt.device))
+            dtest.mean_function = ZeroMeanFunction(int(xt.shape[1]))
+            tests.append(dtest)
+        f, index = factor_segments(self.kernel.child_nodes, self._slices(hyper_parameter), tests, noise)
+        if f is None:
+            return [None] * len(tests)
+        f.check_info()
+        return self._per_segment([f.cholesky(j).to(torch.float64) for j in range(f.batch)], index)
+
+    def get_L_K_ss(self, hyper_parameter: List, noise) -> torch.Tensor:
+        if self.L_K_ss is None:
+            self.L_K_ss = self._block_diag(self.get_L_K_ss_blocks(hyper_parameter, noise))
+        return self.L_K_ss
+
+    # -- factorisation ----------------------------------------------------------------------------
+    def get_L_K_blocks(self, hyper_parameter, noise) -> List:
+        f, index = self.segment_factorization(hyper_parameter, noise)
+        if f is None:
+            return [None] * len(self.kernel.child_nodes)
+        f.check_info()
+        return self._per_segment([f.cholesky(j).to(torch.float64) for j in range(f.batch)], index)
+
+    def get_L_K(self, hyper_parameter: List, noise) -> torch.Tensor:
+        if self.L_K is None:
+            self.L_K = self._block_diag(self.get_L_K_blocks(hyper_parameter, noise))
+        return self.L_K
+
+    def get_L_alpha_blocks(self, hyper_parameter, noise) -> List:
+        """alpha of every segment, [n_i, 1] (CovarianceMatrix.py:469-484): one batched backward solve."""
+        f, index = self.segment_factorization(hyper_parameter, noise)
+        if f is None:
+            return [None] * len(self.kernel.child_nodes)
+        f.check_info()
+        return self._per_segment([a.reshape(-1, 1) for a in f.alphas()], index)
+
+    def get_L_alpha(self, hyper_parameter: List, noise) -> torch.Tensor:
+        if self.L_alpha is None:
+            blocks = [b for b in self.get_L_alpha_blocks(hyper_parameter, noise) if b is not None]
+            self.L_alpha = torch.cat(blocks, dim=0)
+        return self.L_alpha
+
+    def _inverse_blocks(self, hyper_parameter, noise, which):
+        out = []
+        for cn, hyp, di in zip(self.kernel.child_nodes, self._slices(hyper_parameter), self.data_input.data_inputs):
+            if di.n_train == 0:
+                out.append(None)
+                continue
+            h = HolisticCovarianceMatrix(cn)
+            h.set_data_input(di)
+            out.append(h.get_L_inv_K(hyp, noise) if which == "L" else h.get_K_inv(hyp, noise))
+        return out
+
+    def get_L_inv_K_blocks(self, hyper_parameter, noise) -> List:
+        """inv(L) per segment (CovarianceMatrix.py:497-509), from identity-augmented factorisations."""
+        self._require_data()
+        return self._inverse_blocks(hyper_parameter, noise, "L")
+
+    def get_L_inv_K(self, hyper_parameter: List, noise) -> torch.Tensor:
+        if self.L_inv_K is None:
+            self.L_inv_K = self._block_diag(self.get_L_inv_K_blocks(hyper_parameter, noise))
+        return self.L_inv_K
+
+    def get_K_inv_blocks(self, hyper_parameter, noise) -> List:
+        """inv(K_i + noise I) per segment (CovarianceMatrix.py:522-534)."""
+        self._require_data()
+        return self._inverse_blocks(hyper_parameter, noise, "K")
+
+    def get_K_inv(self, hyper_parameter: List, noise) -> torch.Tensor:
+        if self.K_inv is None:
+            self.K_inv = self._block_diag(self.get_K_inv_blocks(hyper_parameter, noise))
+        return self.K_inv
+
+    def get_K_s(self, hyper_parameter: List) -> torch.Tensor:
+        """kernel(X_train, X_test) of the whole operator (CovarianceMatrix.py:555-565)."""
+        self._require_data()
+        if self.K_s is None:
+            di = self.data_input
+            self.K_s = self.kernel.get_tf_tensor(hyper_parameter, di.data_x_train, di.data_x_test)
+        return self.K_s

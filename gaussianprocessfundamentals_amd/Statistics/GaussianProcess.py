@@ -1,7 +1,9 @@
-"""Gaussian process objects (gpbasics/Statistics/GaussianProcess.py:20-125).
+"""Gaussian process objects (gpbasics/Statistics/GaussianProcess.py:20-206).
 
-Only the holistic :class:`GaussianProcess` is on the hot path; the blockwise / partitioned /
-predefined variants are SURVEY §8f "next".
+:class:`GaussianProcess` is the holistic GP of the hot path.  :class:`BlockwiseGaussianProcess`
+(a change-point operator) and :class:`PartitionedGaussianProcess` (a partition operator) hold one
+constituent GaussianProcess per segment; their likelihood and posterior are computed for all
+segments at once by one ragged device factorisation (Statistics/CovarianceMatrix.factor_segments).
 """
 from __future__ import annotations
 
@@ -52,7 +54,22 @@ class AbstractGaussianProcess:
                 kernel_hyper_param = self.kernel.get_default_hyper_parameter(self.data_input.get_x_range(),
                                                                              self.data_input.n_train)
         mean_mu = self.mean_function.get_tf_tensor(mean_function_hyper_param, self.data_input.data_x_test)
-        post_mu = self.aux.get_posterior_mu(kernel_hyper_param, noise)
+        if isinstance(self, (PartitionedGaussianProcess, BlockwiseGaussianProcess)):
+            # per-segment posterior means concatenated in segment order (GaussianProcess.py:64-77);
+            # a change-point kernel's change points precede the children's hyperparameters.  (The
+            # reference reads them from self.covariance_matrix.change_point_positions, an attribute
+            # SegmentedCovarianceMatrix does not have -- it raises AttributeError there; the kernel's
+            # change points are the intended offset, as in SegmentedCovarianceMatrix.get_K_blocks.)
+            index = len(self.kernel.change_point_positions) if isinstance(self, BlockwiseGaussianProcess) else 0
+            kernels, slices = [], []
+            for sub in self.constituent_gps:
+                nh = sub.kernel.get_number_of_hyper_parameter()
+                kernels.append(sub.kernel)
+                slices.append(list(kernel_hyper_param[index:index + nh]))
+                index += nh
+            post_mu = ax.segment_posterior_mu(kernels, slices, [g.data_input for g in self.constituent_gps], noise)
+        else:
+            post_mu = self.aux.get_posterior_mu(kernel_hyper_param, noise)
         return mean_mu + post_mu, mean_mu, post_mu
 
     def copy(self):
@@ -69,3 +86,53 @@ class GaussianProcess(AbstractGaussianProcess):
         g = GaussianProcess(self.kernel, self.mean_function)
         g.set_inducing_points(self.inducing_points)
         return g
+
+
+
+class PredefinedGaussianProcess(AbstractGaussianProcess):
+    """A GP around a given covariance-matrix object (GaussianProcess.py:134-143)."""
+
+    def __init__(self, covariance_matrix, mean_function):
+        super().__init__(covariance_matrix.kernel, mean_function)
+        self.covariance_matrix = covariance_matrix
+        self.aux = ax.HolisticAuxiliaryGpProperties(self.covariance_matrix, self.mean_function)
+
+    def copy(self):
+        g = PredefinedGaussianProcess(self.covariance_matrix, self.mean_function)
+        g.set_inducing_points(self.inducing_points)
+        return g
+
+
+class _SegmentedGaussianProcess(AbstractGaussianProcess):
+    _WHAT = "Partitioned GP"
+
+    def __init__(self, kernel, mean_function):
+        super().__init__(kernel, mean_function)
+        self.constituent_gps: List[GaussianProcess] = [GaussianProcess(cn, self.mean_function)
+                                                       for cn in kernel.child_nodes]
+        self.covariance_matrix = cm.SegmentedCovarianceMatrix(kernel)
+        self.aux = ax.BlockwiseAuxiliaryGpProperties(self.covariance_matrix, self.mean_function)
+
+    def set_data_input(self, data_input):
+        assert len(data_input.data_inputs) == len(self.constituent_gps), \
+            "Data Input does not fit constituent GPs of %s" % self._WHAT
+        self.data_input = data_input
+        self.covariance_matrix.set_data_input(data_input)
+        self.aux.set_data_input(data_input)
+        for sub, di in zip(self.constituent_gps, data_input.data_inputs):
+            sub.set_data_input(di)
+
+    def copy(self):
+        g = type(self)(self.kernel, self.mean_function)
+        g.set_inducing_points(self.inducing_points)
+        return g
+
+
+class BlockwiseGaussianProcess(_SegmentedGaussianProcess):
+    """Globally segmented GP over a ChangePointOperator (GaussianProcess.py:146-175)."""
+    _WHAT = "blockwise GP"
+
+
+class PartitionedGaussianProcess(_SegmentedGaussianProcess):
+    """GP over a PartitionOperator (GaussianProcess.py:178-206)."""
+    _WHAT = "Partitioned GP"

@@ -29,10 +29,12 @@ _SUBMODULES = (
     "global_parameters", "engine", "sweep",
     "Auxiliary", "Auxiliary.BasicGPComponent",
     "KernelBasics", "KernelBasics.Kernel", "KernelBasics.BaseKernels", "KernelBasics.Operators",
+    "KernelBasics.PartitioningModel", "KernelBasics.PartitionOperator",
     "MeanFunctionBasics", "MeanFunctionBasics.MeanFunction", "MeanFunctionBasics.BaseMeanFunctions",
     "DataHandling", "DataHandling.DataInput", "DataHandling.AbstractDataInput", "DataHandling.BatchDataInput",
     "Statistics", "Statistics.CovarianceMatrix", "Statistics.Auxiliary", "Statistics.GaussianProcess",
     "Metrics", "Metrics.MatrixHandlingTypes", "Metrics.Metrics", "Metrics.LogLikelihood", "Metrics.Auxiliary",
+    "Metrics.BayesianInformationCriterion", "Metrics.MeanSquaredError", "Metrics.CrossValidation",
 )
 
 

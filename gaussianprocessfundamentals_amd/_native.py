@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must be loaded first: libgpk binds to torch's HIP r
 
 from . import _build
 
-GPK_ABI_VERSION = 2
+GPK_ABI_VERSION = 3
 GPK_F64, GPK_F32 = 0, 1
 OP_PER, OP_SE, OP_MAT32, OP_MAT52, OP_ADD, OP_MUL = 104, 105, 107, 108, 201, 202
 NODE_SCALED, NODE_ARD, NODE_SE_EXPANDED, NODE_STANDARD = 1, 2, 4, 8
@@ -28,7 +28,8 @@ EXPORTS = (
     "gpk_abi_version", "gpk_last_error", "gpk_plan", "gpk_assemble", "gpk_potrf_aug",
     "gpk_finalize", "gpk_nlml", "gpk_kernel_matrix", "gpk_trsv", "gpk_timing_enable",
     "gpk_timing_read", "gpk_timing_reset", "gpk_tune", "gpk_potrf_aug_ex", "gpk_assemble_inverse",
-    "gpk_grad_workspace_bytes", "gpk_nlml_grad",
+    "gpk_grad_workspace_bytes", "gpk_nlml_grad", "gpk_assemble_ragged", "gpk_potrf_aug_ragged",
+    "gpk_finalize_ragged", "gpk_nlml_ragged",
 )
 
 
@@ -85,6 +86,12 @@ def _declare(lib):
         "gpk_grad_workspace_bytes": (c_size_t, [POINTER(GpkKdesc), POINTER(GpkLayout)]),
         "gpk_nlml_grad": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64, P,
                                   c_int64, P, c_int64, P, P, P, P, P, P, c_size_t, P]),
+        "gpk_assemble_ragged": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64,
+                                        P, c_int64, P, c_int64, P, c_int64, P, P, P, P]),
+        "gpk_potrf_aug_ragged": (c_int, [POINTER(GpkLayout), P, P, P, P, P, P]),
+        "gpk_finalize_ragged": (c_int, [POINTER(GpkLayout), P, P, P, P, P, P, P]),
+        "gpk_nlml_ragged": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64, P,
+                                    c_int64, P, c_int64, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

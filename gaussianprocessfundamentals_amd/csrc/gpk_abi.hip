@@ -265,7 +265,7 @@ static int assemble_impl(const gpk_kdesc* kd, const gpk_layout* lay, const doubl
                          int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
                          const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
                          const double* E, int64_t e_bstride, const double* y, int64_t y_bstride,
-                         void* W, bool eye, void* stream) {
+                         void* W, bool eye, const int64_t* n_dev, const int64_t* m_dev, void* stream) {
   if (int e = check_layout(lay)) return e;
   if (!valid_kdesc(kd, lay->d)) return fail_arg(1, "kernel descriptor");
   if (!hyp_dev && kd->n_hyp > 0) return fail_arg(3, "hyp_dev");
@@ -302,6 +302,8 @@ static int assemble_impl(const gpk_kdesc* kd, const gpk_layout* lay, const doubl
   a.plain = 0;
   a.eye = eye ? 1 : 0;
   a.ntile = lay->p / ATILE;
+  a.nb = n_dev;
+  a.mb = m_dev;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const double es = (double)elem_size(lay->dtype);
   const double bytes = (double)lay->batch *
@@ -318,7 +320,19 @@ int gpk_assemble(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_d
                  const double* E, int64_t e_bstride, const double* y, int64_t y_bstride,
                  void* W, void* stream) {
   return assemble_impl(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, Xs,
-                       xs_bstride, E, e_bstride, y, y_bstride, W, false, stream);
+                       xs_bstride, E, e_bstride, y, y_bstride, W, false, nullptr, nullptr, stream);
+}
+
+int gpk_assemble_ragged(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+                        int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+                        const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
+                        const double* y, int64_t y_bstride, const int64_t* n_dev, const int64_t* m_dev,
+                        void* W, void* stream) {
+  if (!n_dev) return fail_arg(13, "n_dev");
+  if (lay && lay->m > 0 && !m_dev) return fail_arg(14, "m_dev (layout planned with m > 0)");
+  return assemble_impl(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, Xs,
+                       xs_bstride, nullptr, 0, y, y_bstride, W, false, n_dev, lay && lay->m > 0 ? m_dev : nullptr,
+                       stream);
 }
 
 int gpk_assemble_inverse(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
@@ -326,11 +340,11 @@ int gpk_assemble_inverse(const gpk_kdesc* kd, const gpk_layout* lay, const doubl
                          const double* X, int64_t x_bstride, const double* y, int64_t y_bstride,
                          void* W, void* stream) {
   return assemble_impl(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, nullptr,
-                       0, nullptr, 0, y, y_bstride, W, true, stream);
+                       0, nullptr, 0, y, y_bstride, W, true, nullptr, nullptr, stream);
 }
 
-int gpk_potrf_aug_ex(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, int32_t flags,
-                     void* stream) {
+static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, int32_t flags,
+                      const int64_t* n_dev, const int64_t* m_dev, void* stream) {
   if (int e = check_layout(lay)) return e;
   if (!W) return fail_arg(2, "W");
   if (!Winv) return fail_arg(3, "Winv");
@@ -372,12 +386,22 @@ int gpk_potrf_aug_ex(const gpk_layout* lay, void* W, void* Winv, int32_t* info_d
     return timed(1, (double)lay->batch * NB * NB * NB / 3.0, 0.0, sp,
                  [&] { return launch_diag(da, dt, lay->batch, sp); });
   };
+  // extra rows that are nonzero in panel columns left of c: all test rows, or the identity rows
+  // t < c (row n_pad + t of E L^-T is zero left of column t)
+  auto extra_nonzero = [&](int64_t c) -> double {
+    return (double)(eye ? std::min<int64_t>(lay->m, c) : lay->m);
+  };
   GemmArgs base;
   memset(&base, 0, sizeof(base));
   base.W = W;
   base.ld = lay->ld;
   base.w_bs = lay->w_batch_stride;
   base.inv_bs = lay->inv_batch_stride;
+  base.nb = n_dev;
+  base.mb = m_dev;
+  base.n_pad = lay->n_pad;
+  base.y_row = lay->y_row;
+  base.p = lay->p;
   // panel solve of block k: every row below the block (the y / test rows included)
   auto trsm = [&](int64_t k) -> hipError_t {
     GemmArgs ga = base;
@@ -393,7 +417,8 @@ int gpk_potrf_aug_ex(const gpk_layout* lay, void* W, void* Winv, int32_t* info_d
       ga.zlo = lay->n_pad + ga.j0 + NB;
       ga.zhi = lay->y_row;
     }
-    const double rK = (double)(lay->n_pad - ga.row0);  // algorithmic: K-part rows x nb^2
+    // algorithmic: rows that are nonzero in the panel (K part + extra rows) x nb^2
+    const double rK = (double)(lay->n_pad - ga.row0) + extra_nonzero(ga.j0 + NB);
     return timed(2, (double)lay->batch * rK * NB * NB, 0.0, sp,
                  [&] { return launch_gemm(ga, dt, GEMM_TRSM, tile, lay->batch, sp); });
   };
@@ -420,8 +445,9 @@ int gpk_potrf_aug_ex(const gpk_layout* lay, void* W, void* Winv, int32_t* info_d
       ga.zlo = lay->n_pad + j0 + kdepth;
       ga.zhi = lay->y_row;
     }
-    // algorithmic flops: 2 kdepth x (lower-triangle elements of the K part in the column range)
-    const double rK = (double)(lay->n_pad - ga.row0);
+    // algorithmic flops: 2 kdepth x (lower-triangle elements in the column range of the rows that
+    // are nonzero in the panel: the K part, then the extra rows, which follow it contiguously)
+    const double rK = (double)(lay->n_pad - ga.row0) + extra_nonzero(j0 + kdepth);
     const double cl = std::min(rK, (double)(c_lo * NB)), ch = std::min(rK, (double)(c_hi * NB));
     const double elems = (ch - cl) * rK - (cl + ch - 1.0) * (ch - cl) / 2.0;
     // algorithmic bytes: the updated tiles' elements read + written once (y / test rows too)
@@ -476,12 +502,24 @@ int gpk_potrf_aug_ex(const gpk_layout* lay, void* W, void* Winv, int32_t* info_d
   return 0;
 }
 
-int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, void* stream) {
-  return gpk_potrf_aug_ex(lay, W, Winv, info_dev, 0, stream);
+int gpk_potrf_aug_ex(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, int32_t flags,
+                     void* stream) {
+  return potrf_impl(lay, W, Winv, info_dev, flags, nullptr, nullptr, stream);
 }
 
-int gpk_finalize(const gpk_layout* lay, const void* W, const int32_t* info_dev, double* out_dev,
-                 double* mu_dev, double* var_dev, void* stream) {
+int gpk_potrf_aug(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, void* stream) {
+  return potrf_impl(lay, W, Winv, info_dev, 0, nullptr, nullptr, stream);
+}
+
+int gpk_potrf_aug_ragged(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
+                         const int64_t* n_dev, const int64_t* m_dev, void* stream) {
+  if (!n_dev) return fail_arg(5, "n_dev");
+  if (lay && lay->m > 0 && !m_dev) return fail_arg(6, "m_dev (layout planned with m > 0)");
+  return potrf_impl(lay, W, Winv, info_dev, 0, n_dev, lay && lay->m > 0 ? m_dev : nullptr, stream);
+}
+
+static int finalize_impl(const gpk_layout* lay, const void* W, const int32_t* info_dev, const int64_t* n_dev,
+                         double* out_dev, double* mu_dev, double* var_dev, void* stream) {
   if (int e = check_layout(lay)) return e;
   if (!W) return fail_arg(2, "W");
   if (!info_dev) return fail_arg(3, "info_dev");
@@ -498,10 +536,40 @@ int gpk_finalize(const gpk_layout* lay, const void* W, const int32_t* info_dev, 
   f.out = out_dev;
   f.mu = mu_dev;
   f.var = var_dev;
+  f.nb = n_dev;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   GPK_HIP(timed(4, 0.0, 0.0, s, [&] { return launch_finalize(f, lay->dtype, lay->batch, s); }),
           "finalize");
   return 0;
+}
+
+int gpk_finalize(const gpk_layout* lay, const void* W, const int32_t* info_dev, double* out_dev,
+                 double* mu_dev, double* var_dev, void* stream) {
+  return finalize_impl(lay, W, info_dev, nullptr, out_dev, mu_dev, var_dev, stream);
+}
+
+int gpk_finalize_ragged(const gpk_layout* lay, const void* W, const int32_t* info_dev, const int64_t* n_dev,
+                        double* out_dev, double* mu_dev, double* var_dev, void* stream) {
+  if (!n_dev) return fail_arg(4, "n_dev");
+  return finalize_impl(lay, W, info_dev, n_dev, out_dev, mu_dev, var_dev, stream);
+}
+
+int gpk_nlml_ragged(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, int64_t hyp_stride,
+                    const double* noise_dev, int64_t noise_stride, const double* X, int64_t x_bstride,
+                    const double* y, int64_t y_bstride, const int64_t* n_dev, void* W, void* Winv,
+                    int32_t* info_dev, double* out_dev, void* stream) {
+  if (int e = check_layout(lay)) return e;
+  if (lay->m != 0) return fail_arg(2, "gpk_nlml_ragged needs a layout planned with m = 0");
+  if (!n_dev) return fail_arg(11, "n_dev");
+  if (!info_dev) return fail_arg(14, "info_dev");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(hipMemsetAsync(info_dev, 0, sizeof(int32_t) * lay->batch, s), "memset info");
+  int e = gpk_assemble_ragged(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, nullptr, 0,
+                              y, y_bstride, n_dev, nullptr, W, stream);
+  if (e) return e;
+  e = gpk_potrf_aug_ragged(lay, W, Winv, info_dev, n_dev, nullptr, stream);
+  if (e) return e;
+  return gpk_finalize_ragged(lay, W, info_dev, n_dev, out_dev, nullptr, nullptr, stream);
 }
 
 int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, int64_t hyp_stride,

@@ -140,13 +140,18 @@ __device__ __forceinline__ double eval_tree(const gpk_kdesc& kd, const double* h
 
 enum { CLS_TRAIN = 0, CLS_PAD = 1, CLS_TEST = 2, CLS_Y = 3, CLS_ZERO = 4 };
 
-__device__ __forceinline__ int classify(const AsmArgs& a, int64_t g) {
-  if (g < a.n) return CLS_TRAIN;
+// row / column class of index g for a member with n training and m test points
+__device__ __forceinline__ int classify(const AsmArgs& a, int64_t g, int64_t n, int64_t m) {
+  if (g < n) return CLS_TRAIN;
   if (g < a.n_pad) return CLS_PAD;
-  if (g < a.n_pad + a.m) return CLS_TEST;
+  if (g < a.n_pad + m) return CLS_TEST;
   if (g == a.y_row) return CLS_Y;
   return CLS_ZERO;
 }
+
+// training / test points of member b (ragged batches: its own counts)
+__device__ __forceinline__ int64_t member_n(const AsmArgs& a, int b) { return a.nb ? a.nb[b] : a.n; }
+__device__ __forceinline__ int64_t member_m(const AsmArgs& a, int b) { return a.mb ? a.mb[b] : a.m; }
 
 // Stage 64 points (raw + per-ARD-node rescaled copies) of one tile edge into LDS.
 __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs& a, const double* hyp,
@@ -161,7 +166,7 @@ __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs&
       const double* src = rows ? a.X : a.Xs;
       if (g < lim) v = src[g * a.d + k];
     } else {
-      const int c = classify(a, g);
+      const int c = classify(a, g, member_n(a, b), member_m(a, b));
       if (c == CLS_TRAIN) v = a.X[(int64_t)b * a.x_bs + g * a.d + k];
       else if (c == CLS_TEST && a.E == nullptr && !a.eye) v = a.Xs[(int64_t)b * a.xs_bs + (g - a.n_pad) * a.d + k];
     }
@@ -223,11 +228,12 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
     return;
   }
   const double noise = a.noise[(int64_t)b * a.noise_stride];
-  const int ccls = classify(a, gj);
+  const int64_t nm = member_n(a, b), mm = member_m(a, b);
+  const int ccls = classify(a, gj, nm, mm);
   const double yv = (ccls == CLS_TRAIN) ? a.y[(int64_t)b * a.y_bs + gj] : 0.0;
   for (int rr = r0; rr < ATILE; rr += 4) {
     const int64_t gi = gi0 + rr;
-    const int rcls = classify(a, gi);
+    const int rcls = classify(a, gi, nm, mm);
     double v = 0.0;
     if (rcls == CLS_PAD || ccls == CLS_PAD) {
       v = (gi == gj) ? 1.0 : 0.0;

@@ -39,6 +39,10 @@ struct AsmArgs {
   int64_t ntile;     // augmented: 64-tiles per dimension
   double diag_add;   // plain mode
   int32_t eye;       // augmented: the m extra rows are the identity (E = I, m == n), zero corner
+  // ragged batches (NULL: every member uses n / m): member b uses its first nb[b] training points
+  // (rows nb[b] .. n_pad-1 become identity rows) and its first mb[b] test points (zero rows after)
+  const int64_t* nb;
+  const int64_t* mb;
 };
 
 struct GemmArgs {
@@ -55,6 +59,11 @@ struct GemmArgs {
   // rows [zlo, zhi) are structurally zero in the panel columns [j0, j0 + kdepth) (identity extra
   // rows: row n_pad + t of E L^-T is zero left of column t); tiles inside the range are skipped
   int64_t zlo, zhi;
+  // ragged batches (NULL: uniform): member b's training rows nb[b] .. n_pad-1 are identity rows and
+  // its test rows n_pad + mb[b] .. y_row-1 zero rows; tiles of rows that are zero in the panel are skipped
+  const int64_t* nb;
+  const int64_t* mb;
+  int64_t n_pad, y_row, p;
 };
 
 struct DiagArgs {
@@ -78,6 +87,7 @@ struct FinArgs {
   double* out;
   double* mu;
   double* var;
+  const int64_t* nb;  // ragged batches: training points of member b (NULL: n)
 };
 
 struct GradArgs {

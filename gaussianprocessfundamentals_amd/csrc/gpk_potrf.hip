@@ -96,6 +96,19 @@ struct BufIO<float> {
   }
 };
 
+// Rows [r0, r1) are zero in the panel columns [j0, j0 + kdepth): identity extra rows past the
+// panel (zlo / zhi), or, in a ragged batch, member b's identity padding rows below the panel and
+// its unused test rows -- and, once the panel lies in the member's padding, every row below it.
+__device__ __forceinline__ bool zero_rows(const GemmArgs& a, int b, int64_t r0, int64_t r1) {
+  if (r0 >= a.zlo && r1 <= a.zhi) return true;
+  if (a.nb == nullptr) return false;
+  const int64_t npb = (a.nb[b] + NB - 1) / NB * NB;
+  const int64_t jend = a.j0 + a.kdepth;
+  if (a.j0 >= npb) return r0 >= jend && r1 <= a.p;
+  if (r0 >= (npb > jend ? npb : jend) && r1 <= a.n_pad) return true;
+  return a.mb != nullptr && r0 >= a.n_pad + a.mb[b] && r1 <= a.y_row;
+}
+
 // One 256-thread workgroup computes a TM x TN tile: acc = A_rows(TM x K) * B_rows(TN x K)^T,
 // K = the panel depth.  Waves 2 x 2, each (TM/2) x (TN/2) = MB x NBK blocks of 16 x 16.
 // Staging: global_load_lds (16 B per lane, no VGPR round trip) into two LDS stages; the chunk
@@ -141,11 +154,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
   T* W = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs;
   const int64_t R = a.row0 + ti * TM;
   // structurally zero operand rows: the product (and so the update / solve) of the tile is zero
-  if (R >= a.zlo && R + TM <= a.zhi) return;
-  if (MODE == GEMM_UPDATE) {
-    const int64_t Rb = a.row0 + tj * TN;
-    if (Rb >= a.zlo && Rb + TN <= a.zhi) return;
-  }
+  if (zero_rows(a, b, R, R + TM)) return;
+  if (MODE == GEMM_UPDATE && zero_rows(a, b, a.row0 + tj * TN, a.row0 + tj * TN + TN)) return;
   const T* Ag = W + R * a.ld + a.j0;
   const T* Bg;
   int64_t ldb;
@@ -314,13 +324,14 @@ __global__ __launch_bounds__(256) void finalize_kernel(FinArgs a) {
     const double logdet = 2.0 * red[0];                          // Metrics.py:153-154
     const double fit = -(double)W[a.y_row * a.ld + a.y_row];     // y^T alpha = z^T z
     const double log2pi = log(2.0 * 3.141592653589793);
-    const double ll = (-0.5 * fit + -0.5 * logdet) + (-0.5 * ((double)a.n * log2pi));  // LogLikelihood.py:39-49
+    const double nm = (double)(a.nb ? a.nb[b] : a.n);             // padding rows add log 1 = 0
+    const double ll = (-0.5 * fit + -0.5 * logdet) + (-0.5 * (nm * log2pi));  // LogLikelihood.py:39-49
     double nl = -ll;
     if (a.info[b] != 0) nl = INFINITY;
     a.out[b * 4 + 0] = nl;
     a.out[b * 4 + 1] = fit;
     a.out[b * 4 + 2] = logdet;
-    a.out[b * 4 + 3] = (double)a.n;
+    a.out[b * 4 + 3] = nm;
   }
   // posterior read-out from the Schur complement corner
   for (int64_t t = tid; t < a.m; t += 256) {

@@ -330,3 +330,135 @@ class InverseFactorization(AugmentedFactorization):
     def alpha(self, b: int = 0) -> torch.Tensor:
         lay = self.layout
         return -self.w(b)[lay.y_row, lay.n_pad:lay.n_pad + self.n].to(torch.float64)
+
+
+def _offset_ptr(t: torch.Tensor, elements: int):
+    """ctypes pointer to element ``elements`` of t (for per-member launches)."""
+    return ctypes.c_void_p(t.data_ptr() + int(elements) * t.element_size())
+
+
+class RaggedFactorization(AugmentedFactorization):
+    """One factorisation of independent problems of DIFFERENT sizes (gpk_*_ragged).
+
+    Member b has ``sizes[b]`` training points and ``test_sizes[b]`` test points; the layout is
+    planned for the largest member and every smaller member's block is completed with identity
+    rows (training) or zero rows (test), which the device skips tile by tile.  This replaces the
+    reference's one-segment-at-a-time loops over constituent GPs (SegmentedCovarianceMatrix
+    get_*_blocks, gpbasics/Statistics/CovarianceMatrix.py:289-565; BlockwiseLogLikelihood,
+    gpbasics/Metrics/LogLikelihood.py:68-104) by one set of batched launches: the panel chain is
+    paid once for all segments instead of once per segment.
+
+    Members may carry different kernel trees (the children of a change-point or partition
+    operator): members sharing one device program are assembled by one launch, the others by a
+    launch each; the factorisation and read-out are always one set of launches.
+    """
+
+    def __init__(self, sizes: Sequence[int], d: int, test_sizes: Optional[Sequence[int]] = None, dtype=None):
+        sizes = [int(s) for s in sizes]
+        if not sizes or min(sizes) < 1:
+            raise ValueError("every member of a ragged batch needs at least one training point")
+        tsz = [int(s) for s in test_sizes] if test_sizes is not None else [0] * len(sizes)
+        if len(tsz) != len(sizes) or min(tsz) < 0:
+            raise ValueError("test_sizes must hold one count >= 0 per member")
+        super().__init__(max(sizes), d, max(tsz), len(sizes), dtype)
+        self.sizes, self.test_sizes = sizes, tsz
+        dev = self.W.device
+        self.n_dev = torch.tensor(sizes, dtype=torch.int64, device=dev)
+        self.m_dev = torch.tensor(tsz, dtype=torch.int64, device=dev)
+
+    def run(self, members: Sequence, noise) -> "RaggedFactorization":
+        """members[b] = (kdesc, hyp [n_hyp] fp64, X_b [n_b, d], y_b [n_b], Xs_b [m_b, d] or None);
+        noise: rank-0 or one value per member."""
+        B, n, m, d = self.batch, self.n, self.m, self.d
+        if len(members) != B:
+            raise ValueError("expected %d members, got %d" % (B, len(members)))
+        dev = self.W.device
+        X = torch.zeros((B, n, d), dtype=torch.float64, device=dev)
+        y = torch.zeros((B, n), dtype=torch.float64, device=dev)
+        Xs = torch.zeros((B, max(m, 1), d), dtype=torch.float64, device=dev)
+        hyp = torch.zeros((B, nat.MAX_HYP), dtype=torch.float64, device=dev)
+        kds = []
+        for b, (kd, h, xb, yb, xsb) in enumerate(members):
+            nb, mb = self.sizes[b], self.test_sizes[b]
+            if tuple(xb.shape) != (nb, d) or yb.numel() != nb:
+                raise ValueError("member %d: X must be [%d, %d] and y hold %d values" % (b, nb, d, nb))
+            if h.numel() != kd.n_hyp:
+                raise ValueError("member %d: %d hyperparameters, kernel expects %d" % (b, h.numel(), kd.n_hyp))
+            X[b, :nb] = xb
+            y[b, :nb] = yb.reshape(-1)
+            if mb:
+                if xsb is None or tuple(xsb.shape) != (mb, d):
+                    raise ValueError("member %d: X_test must be [%d, %d]" % (b, mb, d))
+                Xs[b, :mb] = xsb
+            hyp[b, :kd.n_hyp] = h
+            kds.append(kd)
+        nz = noise if isinstance(noise, torch.Tensor) else torch.as_tensor(noise, dtype=torch.float64)
+        nz = nz.detach().to(device=dev, dtype=torch.float64).reshape(-1)
+        nz = (nz.expand(B) if nz.numel() == 1 else nz).contiguous()
+        if nz.numel() != B:
+            raise ValueError("noise must be rank-0 or hold one value per member")
+        L, s = self.L, nat.stream_handle(dev)
+        lay = self.layout
+        self.info.zero_()
+        mptr = nat.ptr(self.m_dev) if m else None
+        xs_ptr = nat.ptr(Xs) if m else None
+        if all(bytes(k) == bytes(kds[0]) for k in kds):
+            nat.check(L.gpk_assemble_ragged(ctypes.byref(kds[0]), ctypes.byref(lay), nat.ptr(hyp), nat.MAX_HYP,
+                                            nat.ptr(nz), 1, nat.ptr(X), n * d, xs_ptr, max(m, 1) * d,
+                                            nat.ptr(y), n, nat.ptr(self.n_dev), mptr, nat.ptr(self.W), s),
+                      "gpk_assemble_ragged")
+        else:
+            one = nat.plan(self.code, 1, n, m, d)   # same p / ld as the batched layout
+            for b, kd in enumerate(kds):
+                nat.check(L.gpk_assemble_ragged(
+                    ctypes.byref(kd), ctypes.byref(one), _offset_ptr(hyp, b * nat.MAX_HYP), 0,
+                    _offset_ptr(nz, b), 0, _offset_ptr(X, b * n * d), 0,
+                    _offset_ptr(Xs, b * max(m, 1) * d) if m else None, 0, _offset_ptr(y, b * n), 0,
+                    _offset_ptr(self.n_dev, b), _offset_ptr(self.m_dev, b) if m else None,
+                    _offset_ptr(self.W, b * lay.w_batch_stride), s), "gpk_assemble_ragged")
+        nat.check(L.gpk_potrf_aug_ragged(ctypes.byref(lay), nat.ptr(self.W), nat.ptr(self.Winv),
+                                         nat.ptr(self.info), nat.ptr(self.n_dev), mptr, s), "gpk_potrf_aug_ragged")
+        nat.check(L.gpk_finalize_ragged(ctypes.byref(lay), nat.ptr(self.W), nat.ptr(self.info),
+                                        nat.ptr(self.n_dev), nat.ptr(self.out),
+                                        nat.ptr(self.mu) if m else None, nat.ptr(self.var) if m else None, s),
+                  "gpk_finalize_ragged")
+        self._keep = (X, y, Xs, hyp, nz)  # operands stay alive until the stream has consumed them
+        self.kd = kds
+        self.done = True
+        return self
+
+    # -- per-member read-out ------------------------------------------------------------------
+    def cholesky(self, b: int = 0) -> torch.Tensor:
+        nb = self.sizes[b]
+        return torch.tril(self.w(b)[:nb, :nb])
+
+    def z(self, b: int = 0) -> torch.Tensor:
+        return self.w(b)[self.layout.y_row, :self.sizes[b]]
+
+    def extra_rows(self, b: int = 0) -> torch.Tensor:
+        lay = self.layout
+        return self.w(b)[lay.n_pad:lay.n_pad + self.test_sizes[b], :self.sizes[b]]
+
+    def corner(self, b: int = 0) -> torch.Tensor:
+        lay, mb = self.layout, self.test_sizes[b]
+        c = self.w(b)[lay.n_pad:lay.n_pad + mb, lay.n_pad:lay.n_pad + mb]
+        return torch.tril(c) + torch.tril(c, -1).transpose(0, 1)
+
+    def posterior_mu(self, b: int = 0) -> torch.Tensor:
+        return self.mu[b * self.m:b * self.m + self.test_sizes[b]]
+
+    def posterior_var_diag(self, b: int = 0) -> torch.Tensor:
+        return self.var[b * self.m:b * self.m + self.test_sizes[b]]
+
+    def alphas(self) -> List[torch.Tensor]:
+        """alpha_b = L_b^-T z_b for every member: one batched backward solve (gpk_trsv)."""
+        lay = self.layout
+        x = torch.zeros((self.batch, lay.n_pad), dtype=torch.float64, device=self.W.device)
+        for b in range(self.batch):
+            x[b, :self.sizes[b]] = self.z(b).to(torch.float64)
+        nat.check(self.L.gpk_trsv(ctypes.byref(lay), 1, nat.ptr(self.W), nat.ptr(self.Winv),
+                                  nat.ptr(x), nat.stream_handle(self.W.device)), "gpk_trsv")
+        return [x[b, :self.sizes[b]] for b in range(self.batch)]
+
+    def alpha(self, b: int = 0) -> torch.Tensor:
+        return self.alphas()[b]

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GPK_ABI_VERSION 2
+#define GPK_ABI_VERSION 3
 
 /* arithmetic types of the factorisation */
 enum { GPK_F64 = 0, GPK_F32 = 1 };
@@ -182,6 +182,34 @@ int gpk_nlml_grad(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_
                   const double* noise_dev, int64_t noise_stride, const double* X, int64_t x_bstride,
                   const double* y, int64_t y_bstride, void* W, void* Winv, int32_t* info_dev,
                   double* out_dev, double* grad_dev, void* work, size_t work_bytes, void* stream);
+/* Ragged batches: independent problems of different sizes factored by the same launches.
+ * Replaces the per-segment loops of SegmentedCovarianceMatrix.get_K_noised_blocks / get_L_K_blocks /
+ * get_L_alpha_blocks (Statistics/CovarianceMatrix.py:346-357, :445-456, :469-484) and the per-block
+ * LogLikelihood of BlockwiseLogLikelihood.get_metric (Metrics/LogLikelihood.py:68-104), which the
+ * reference runs one TensorFlow Cholesky after another.
+ * The layout is planned for the largest member (n = max n_b, m = max m_b); member b uses the first
+ * n_dev[b] points of X[b] / y[b] and the first m_dev[b] points of Xs[b] (device int64 arrays,
+ * 1 <= n_dev[b] <= n, 0 <= m_dev[b] <= m).  Its rows n_dev[b] .. n_pad-1 are assembled as identity
+ * rows (contributing log 1 = 0 to the log-determinant and 0 to the data fit) and its test rows past
+ * m_dev[b] as zero rows; the factorisation skips every tile made of such rows.  m_dev may be NULL
+ * when the layout has m = 0.  Results are those of each member factored on its own:
+ * out_dev[b*4 + 3] = n_dev[b] and the -LML uses n_dev[b] in its normalising constant.
+ * The flop counts of gpk_timing_read for ragged launches are those of the padded problem. */
+int gpk_assemble_ragged(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev,
+                        int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
+                        const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
+                        const double* y, int64_t y_bstride, const int64_t* n_dev, const int64_t* m_dev,
+                        void* W, void* stream);
+int gpk_potrf_aug_ragged(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev,
+                         const int64_t* n_dev, const int64_t* m_dev, void* stream);
+int gpk_finalize_ragged(const gpk_layout* lay, const void* W, const int32_t* info_dev, const int64_t* n_dev,
+                        double* out_dev, double* mu_dev, double* var_dev, void* stream);
+/* gpk_assemble_ragged + gpk_potrf_aug_ragged + gpk_finalize_ragged with m = 0 */
+int gpk_nlml_ragged(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, int64_t hyp_stride,
+                    const double* noise_dev, int64_t noise_stride, const double* X, int64_t x_bstride,
+                    const double* y, int64_t y_bstride, const int64_t* n_dev, void* W, void* Winv,
+                    int32_t* info_dev, double* out_dev, void* stream);
+
 /* Plain kernel matrix K[i*ldk + j] = k(X_i, Y_j) (+ diag_add where i == j) for i < n, j < m.
  * uplo: 0 = full, 1 = lower triangle only.  dtype selects the stored element type. */
 int gpk_kernel_matrix(const gpk_kdesc* kd, const double* hyp_dev, int dtype, int uplo,

@@ -249,6 +249,67 @@ def posterior(tree, hyp, noise, x, y, xs, scaled=False, se_expanded=False):
     return mu, var
 
 
+# ---------------------------------------------------------------- segmented models
+def cp_indicator(x, cp, mode: str = "INDICATOR"):
+    """Change-point masks of ChangePointOperator (K/Operators.py:379-408) on 1-D inputs:
+    INDICATOR = [x < cp]; SIGMOID = 0.5 (1 + tanh((cp - x) / 0.0025)); APPROX_INDICATOR =
+    1 / (1 + exp(-100 (x - cp)))."""
+    x = np.asarray(x, dtype=np.float64).reshape(-1)
+    if mode == "SIGMOID":
+        return 0.5 * (1 + np.tanh((cp - x) / 0.0025))
+    if mode == "APPROX_INDICATOR":
+        return 1.0 / (1.0 + np.exp(-100.0 * (x - cp)))
+    return (x < cp).astype(np.float64)
+
+
+def change_point_matrix(trees, hyps, cps, x, x_, mode: str = "INDICATOR", scaled=False):
+    """ChangePointOperator.get_tf_tensor (K/Operators.py:410-476): child i's matrix times
+    previous_sigmoid (the complement mask of cp_{i-1}) times the outer indicator of cp_i, summed."""
+    prev = np.ones((x.shape[0], x_.shape[0]))
+    total = np.zeros((x.shape[0], x_.shape[0]))
+    for i, (t, h) in enumerate(zip(trees, hyps)):
+        K = kernel_matrix(t, h, x, x_, scaled) * prev                                  # :414-417
+        if i < len(cps):
+            xi, xsi = cp_indicator(x, cps[i], mode), cp_indicator(x_, cps[i], mode)
+            K = K * np.outer(xi, xsi)                                                   # :431-436
+            prev = np.outer(1.0 - xi, 1.0 - xsi)                                        # :433-434
+        total = total + K                                                               # :476
+    return total
+
+
+def blockwise_nlml(segments, noise, scaled=False) -> float:
+    """BlockwiseLogLikelihood.get_metric (M/LogLikelihood.py:76-104): the sum of the segments'
+    -LML; segments = [(tree, hyp, x_i, y_i)], an empty segment contributes 0."""
+    return float(sum(nlml(t, h, noise, x, y, scaled) if x.shape[0] > 0 else 0.0 for t, h, x, y in segments))
+
+
+def bic(nl: float, n_hyp: int, n_train: int) -> float:
+    """BIC.get_metric (M/BayesianInformationCriterion.py:27-38): -2 LL + |M| log n with LL = -nl."""
+    return -2.0 * (-nl) + n_hyp * math.log(n_train)
+
+
+def mse(tree, hyp, noise, x, y, xs, ys, scaled=False) -> float:
+    """MeanSquaredError.get_metric (M/MeanSquaredError.py:26-42): mean((K_s^T alpha - y_test)^2)."""
+    mu, _ = posterior(tree, hyp, noise, x, y, xs, scaled)
+    return float(np.mean((mu.reshape(-1, 1) - np.asarray(ys).reshape(-1, 1)) ** 2))
+
+
+def cv_folds(n: int, test_ratio: float = 0.2):
+    """Fold indices of get_data_inputs (M/CrossValidation.py:16-44), drawn from numpy's GLOBAL
+    generator exactly as the reference draws them: [(train_idx, test_idx)]."""
+    n_test = int(round(n * test_ratio))
+    epochs = int(np.floor(1 / test_ratio))
+    idx = np.linspace(start=0, num=n, stop=n, endpoint=False, dtype=int)
+    np.random.shuffle(idx)
+    out, at = [], 0
+    for _ in range(epochs):
+        stop = n_test + at
+        out.append((np.array(sorted(np.concatenate([idx[:at], idx[stop:]])), dtype=int),
+                    np.array(sorted(idx[at:stop]), dtype=int)))
+        at += n_test
+    return out
+
+
 # ---------------------------------------------------------------- synthetic configs (SURVEY §8d)
 def make_inputs(cfg: str, n: int = None, seed: int = None) -> Tuple[np.ndarray, np.ndarray]:
     """Synthetic data generators of SURVEY §8(d) (numpy default_rng(seed))."""
