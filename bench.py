@@ -28,7 +28,7 @@ sys.path.insert(0, HERE)
 
 PEAK = {"f64": 78.6, "f32": 157.3}   # TFLOP/s dense MFMA (AMD MI355X spec; microarch guide for f32)
 HBM_PEAK = 8000.0                      # GB/s spec
-DEFAULT_BATCH = 8                      # candidates per rank per step on the metric config
+DEFAULT_BATCH = 16                     # candidates per rank per step on the metric config
 
 CONFIGS = {
     # name: (kernel, d, n, noise, dtype, hyp)

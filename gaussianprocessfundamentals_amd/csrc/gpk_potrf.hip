@@ -50,6 +50,15 @@ struct Mfma<float> {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Waves along N of the 128 x 128 update tile: 2 (4 waves of 64 x 64 each) or 4 (8 waves of 64 x 32:
+// 111 VGPRs, so two 512-thread workgroups -- four waves per SIMD -- share a CU; f64 update +2.8 %)
+#ifndef GPK_UPD_WN
+#define GPK_UPD_WN 4
+#endif
+#ifndef GPK_UPD_WN_F32
+#define GPK_UPD_WN_F32 2
+#endif
+
 constexpr int ROWB = 128;  // bytes of one row of a staged K chunk (8 pieces of 16 B)
 
 // bijective XCD-aware remap: consecutive logical tiles land on one XCD (blockIdx % 8 group)
@@ -116,14 +125,16 @@ __device__ __forceinline__ bool zero_rows(const GemmArgs& a, int b, int64_t r0, 
 // ends chunk kc.  K is permuted identically for both operands so that one ds_read_b128 yields
 // the operands of EPC consecutive MFMA k-steps: in k-step s, lane group q = lane >> 4 uses
 // logical piece q + 4 (s / EPC), element s % EPC.
-template <typename T, int MODE, int TM, int TN>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
+template <typename T, int MODE, int TM, int TN, int WN>
+__global__ __launch_bounds__(128 * WN, 2) void gemm_kernel(GemmArgs a) {
   constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B piece
   constexpr int GBK = ROWB / (int)sizeof(T); // K depth per stage (16 f64, 32 f32)
   constexpr int KS = GBK / 4;                // MFMA k-steps per stage
-  constexpr int MB = TM / 32, NBK = TN / 32; // 16 x 16 blocks per wave
+  constexpr int WM = 2;                      // waves along M (rows); WN along N (columns)
+  constexpr int NW = WM * WN;                // waves per workgroup
+  constexpr int MB = TM / (16 * WM), NBK = TN / (16 * WN);  // 16 x 16 blocks per wave
   constexpr int STAGE = (TM + TN) * ROWB;    // bytes per stage
-  constexpr int PW = (TM + TN) / 32;         // glds wave-instructions (8 rows each) per wave
+  constexpr int PW = (TM + TN) / (8 * NW);   // glds wave-instructions (8 rows each) per wave
   typedef typename Mfma<T>::acc_t acc_t;
   typedef T vec_t __attribute__((ext_vector_type(EPC)));
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
@@ -170,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = wave_uniform(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid / WN, wc = wid % WN;
 
   // per-lane source of each of this wave's glds instructions: rows [0, TM) are A, [TM, TM+TN) B
   const T* src[PW];
@@ -206,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cu);
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<void*>(cuu), 0, (int)(TM * a.ld * (int64_t)sizeof(T)), 0x00020000);
-  const int cvo = (int)(((int64_t)(wr * (TM / 2) + Mfma<T>::row(lane, 0)) * a.ld + wc * (TN / 2) + col) *
+  const int cvo = (int)(((int64_t)(wr * (TM / WM) + Mfma<T>::row(lane, 0)) * a.ld + wc * (TN / WN) + col) *
                         (int64_t)sizeof(T));
   constexpr int RSTEP = sizeof(T) == 8 ? 4 : 1;
   const int ldb_s = wave_uniform((int)(a.ld * (int64_t)sizeof(T)));
@@ -226,8 +237,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
     }
 
   const int q = lane >> 4, lr = lane & 15;
-  const int aoff = (wr * (TM / 2) + lr) * ROWB;
-  const int boff = (TM + wc * (TN / 2) + lr) * ROWB;
+  const int aoff = (wr * (TM / WM) + lr) * ROWB;
+  const int boff = (TM + wc * (TN / WN) + lr) * ROWB;
   const int p0 = swz(lr, q) * 16, p1 = swz(lr, q + 4) * 16;
 
 #ifndef GPK_ABLATE
@@ -276,7 +287,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int n = 0; n < NBK; ++n) {
         // TRSM against the lower-triangular inverse: K chunk kc feeds output columns >= kc GBK only
-        if (MODE == GEMM_TRSM && kc * GBK > wc * (TN / 2) + n * 16 + 15) continue;
+        if (MODE == GEMM_TRSM && kc * GBK > wc * (TN / WN) + n * 16 + 15) continue;
 #pragma unroll
         for (int m = 0; m < MB; ++m)
           acc[m][n] = CFIRST ? Mfma<T>::op_neg(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n])
@@ -387,7 +398,7 @@ __global__ __launch_bounds__(256) void trsv_update_kernel(TrsvArgs a) {
   }
 }
 
-template <typename T, int MODE, int TM, int TN>
+template <typename T, int MODE, int TM, int TN, int WN = 2>
 hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
   // a.nt / c_lo / c_hi are in units of this launch's tile sizes
   unsigned nblk;
@@ -398,7 +409,7 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
     nblk = (unsigned)a.nt;
   }
   if (nblk == 0) return hipSuccess;
-  hipLaunchKernelGGL((gemm_kernel<T, MODE, TM, TN>), dim3(nblk, batch), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<T, MODE, TM, TN, WN>), dim3(nblk, batch), dim3(128 * WN), 0, s, a);
   return hipGetLastError();
 }
 
@@ -407,13 +418,13 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s) {
   if (dtype == GPK_F64) {
     if (mode == GEMM_UPDATE)
-      return tile == 128 ? launch_gemm_t<double, GEMM_UPDATE, 128, 128>(a, batch, s)
+      return tile == 128 ? launch_gemm_t<double, GEMM_UPDATE, 128, 128, GPK_UPD_WN>(a, batch, s)
                          : launch_gemm_t<double, GEMM_UPDATE, 64, 64>(a, batch, s);
     return tile == 128 ? launch_gemm_t<double, GEMM_TRSM, 128, 128>(a, batch, s)
                        : launch_gemm_t<double, GEMM_TRSM, 64, 128>(a, batch, s);
   }
   if (mode == GEMM_UPDATE)
-    return tile == 128 ? launch_gemm_t<float, GEMM_UPDATE, 128, 128>(a, batch, s)
+    return tile == 128 ? launch_gemm_t<float, GEMM_UPDATE, 128, 128, GPK_UPD_WN_F32>(a, batch, s)
                        : launch_gemm_t<float, GEMM_UPDATE, 64, 64>(a, batch, s);
   return tile == 128 ? launch_gemm_t<float, GEMM_TRSM, 128, 128>(a, batch, s)
                      : launch_gemm_t<float, GEMM_TRSM, 64, 128>(a, batch, s);

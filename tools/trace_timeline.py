@@ -43,8 +43,11 @@ def main():
     path = sys.argv[1]
     back = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     rows = []
+    meta = {}
     for r in csv.DictReader(open(path)):
-        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), klass(r["Kernel_Name"])))
+        key = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]), klass(r["Kernel_Name"]))
+        rows.append(key)
+        meta[key] = (r["Queue_Id"], r["Grid_Size_X"], r["Grid_Size_Y"])
     rows.sort()
     starts = [i for i, r in enumerate(rows) if r[2] == "assemble"]
     i0 = starts[-back]
@@ -67,6 +70,12 @@ def main():
         a, b = t0 + span * w // nwin, t0 + span * (w + 1) // nwin
         clip = [(max(s, a), min(e, b)) for s, e, k in step if k == "update" and e > a and s < b]
         print("  window %d: update busy %.0f%%" % (w, 100.0 * union(clip) / (b - a)))
+    if len(sys.argv) > 3:
+        # kernel sequence of the last N kernels of the step: queue, class, start offset, duration, grid
+        nlast = int(sys.argv[3])
+        for s_, e_, k_ in sorted(step)[-nlast:]:
+            q, gx, gy = meta[(s_, e_, k_)]
+            print("    q%-3s %-9s +%9.1f us  %7.1f us  grid %s x %s" % (q, k_, (s_ - t0) / 1e3, (e_ - s_) / 1e3, gx, gy))
 
 
 if __name__ == "__main__":
