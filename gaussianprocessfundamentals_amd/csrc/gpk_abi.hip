@@ -148,7 +148,7 @@ int64_t env_i64(const char* name, int64_t dflt) {
 Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
-                         env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 4)};
+                         env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8)};
   return t;
 }
 
@@ -460,8 +460,9 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
                  [&] { return launch_gemm(ga, dt, GEMM_UPDATE, tile, lay->batch, st); });
   };
 
-  // Groups of G 128-column panels per trailing update (K = 128 G): factor panel k of the group and
-  // apply it to the group's remaining block columns only (thin), ..., then update the trailing
+  // Groups of G 128-column panels per trailing update (K = 128 G): inside the group, block column k
+  // is brought up to date with the group's earlier panels (one left-looking update of depth
+  // 128 (k - g0)) and then factored and solved, ..., then update the trailing
   // matrix with all G panels at once -- its first G block columns (look-ahead, on the panel
   // stream: the next group's panels) and the rest (bulk stream, overlapping the next group's
   // panel chain).  A deeper K halves the read-modify-write passes over the trailing matrix per
@@ -476,9 +477,12 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   for (int64_t g0 = 0; g0 < nblk; g0 += G) {
     const int64_t gend = std::min(g0 + G, nblk);
     for (int64_t k = g0; k < gend; ++k) {
+      // left-looking inside the group: block column k receives the group's earlier panels in ONE
+      // update of depth 128 (k - g0) right before its diagonal block is factored (right-looking
+      // thin updates would read and write the group's columns once per panel)
+      if (k > g0) GPK_HIP(update(g0 * NB, (int)((k - g0) * NB), 0, 1, sp), "update thin");
       GPK_HIP(diag(k), "diag");
       GPK_HIP(trsm(k), "trsm");
-      if (k + 1 < gend) GPK_HIP(update(k * NB, NB, 0, gend - k - 1, sp), "update thin");
     }
     const int kd = (int)((gend - g0) * NB);
     if (!la) {

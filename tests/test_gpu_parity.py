@@ -338,7 +338,7 @@ def test_sweep_matches_single_evaluations():
 
 
 # ------------------------------------------------------------------------------ schedules
-@pytest.mark.parametrize("group", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("group", [1, 2, 3, 4, 5, 8])
 @pytest.mark.parametrize("lookahead", [0, 1])
 def test_schedule_variants_match_oracle(group, lookahead):
     """Every panel-group size and both stream schedules give the same -LML, posterior mean and
