@@ -138,6 +138,7 @@ struct Tune {
   int64_t lookahead;      // 1: panel chain on a high-priority side stream (default), 0: one stream
   int64_t reserve_cus;    // CUs kept free of the bulk trailing update for the panel chain
   int64_t group;          // panels per trailing update (K = 128 group)
+  int64_t group_first;    // panels of the first group (a short first chain lets the bulk start early)
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -148,7 +149,8 @@ int64_t env_i64(const char* name, int64_t dflt) {
 Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
-                         env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8)};
+                         env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
+                         env_i64("GPK_GROUP_FIRST", 8)};
   return t;
 }
 
@@ -466,16 +468,18 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // matrix with all G panels at once -- its first G block columns (look-ahead, on the panel
   // stream: the next group's panels) and the rest (bulk stream, overlapping the next group's
   // panel chain).  A deeper K halves the read-modify-write passes over the trailing matrix per
-  // doubling of G.
+  // doubling of G.  The first group has G0 <= G panels: its chain is exposed (nothing to overlap
+  // yet), so a short one lets the first bulk update start early.
   const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tn.group, 8));
+  const int64_t G0 = std::max<int64_t>(1, std::min<int64_t>(tn.group_first, G));
   if (la) {
     GPK_HIP(hipEventRecord(ss->fork, s), "event");
     GPK_HIP(hipStreamWaitEvent(sp, ss->fork, 0), "event");
     GPK_HIP(hipStreamWaitEvent(sb, ss->fork, 0), "event");
   }
   bool bulk_pending = false;
-  for (int64_t g0 = 0; g0 < nblk; g0 += G) {
-    const int64_t gend = std::min(g0 + G, nblk);
+  for (int64_t g0 = 0, gsize = G0; g0 < nblk; g0 += gsize, gsize = G) {
+    const int64_t gend = std::min(g0 + gsize, nblk);
     for (int64_t k = g0; k < gend; ++k) {
       // left-looking inside the group: block column k receives the group's earlier panels in ONE
       // update of depth 128 (k - g0) right before its diagonal block is factored (right-looking
@@ -724,6 +728,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "trsm_t128_min")) slot = &t.trsm_t128_min;
   else if (!strcmp(key, "diag_debug")) slot = &t.diag_dbg;
   else if (!strcmp(key, "group")) slot = &t.group;
+  else if (!strcmp(key, "group_first")) slot = &t.group_first;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

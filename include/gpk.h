@@ -234,7 +234,8 @@ int gpk_timing_reset(void);
 /* Scheduling knobs of the factorisation (no reference counterpart: tf.linalg.cholesky exposes
  * none).  Keys: "lookahead" (1: panel chain on a high-priority stream overlapping the bulk
  * trailing update, 0: one stream), "reserve_cus" (CUs masked off the bulk-update stream; read
- * when that stream is first created), "group" (panels per trailing update, K = 128 group),
+ * when that stream is first created), "group" (panels per trailing update, K = 128 group), "group_first"
+ * (panels of the first group),
  * "upd_t128_min", "trsm_t128_min" (128-tile thresholds).
  * Stores the value and returns the previous one through *old (may be NULL); 0 or -1 (unknown
  * key).  Defaults come from the environment (GPK_LOOKAHEAD, GPK_RESERVE_CUS, ...). */

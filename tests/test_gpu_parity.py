@@ -338,13 +338,15 @@ def test_sweep_matches_single_evaluations():
 
 
 # ------------------------------------------------------------------------------ schedules
-@pytest.mark.parametrize("group", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("group,group_first", [(1, 1), (2, 2), (3, 1), (4, 4), (5, 2), (8, 2), (8, 3), (8, 8)])
 @pytest.mark.parametrize("lookahead", [0, 1])
-def test_schedule_variants_match_oracle(group, lookahead):
-    """Every panel-group size and both stream schedules give the same -LML, posterior mean and
-    variance (N = 1100: 9 panels, so groups end ragged; m = 70 test rows ride along)."""
+def test_schedule_variants_match_oracle(group, group_first, lookahead):
+    """Every panel-group size (first group and the rest) and both stream schedules give the same
+    -LML, posterior mean and variance (N = 1100: 9 panels, so groups end ragged; m = 70 test rows
+    ride along)."""
     from gaussianprocessfundamentals_amd import _native as nat
     old_g = nat.tune("group", group)
+    old_f = nat.tune("group_first", group_first)
     old_l = nat.tune("lookahead", lookahead)
     try:
         x, y = o.make_inputs("C2", n=1100, seed=7)
@@ -365,4 +367,5 @@ def test_schedule_variants_match_oracle(group, lookahead):
             np.testing.assert_allclose(fact.posterior_var_diag(b).cpu().numpy(), np.diag(var), rtol=0, atol=1e-8)
     finally:
         nat.tune("group", old_g)
+        nat.tune("group_first", old_f)
         nat.tune("lookahead", old_l)
