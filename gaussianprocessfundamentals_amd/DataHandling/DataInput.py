@@ -159,6 +159,48 @@ class DataInput(AbstractDataInput):
         super().__init__(_f64(data_x_train), _f64(data_y_train), data_x_test, data_y_test, test_ratio, seed)
 
 
+    def get_inducting_x_train(self, indices) -> torch.Tensor:
+        """Rows of the training inputs at ``indices`` (DataInput.py:41-50)."""
+        self.inducting_x_train = self.data_x_train[torch.as_tensor(indices, device=self.data_x_train.device)]
+        return self.inducting_x_train
+
+    def get_inducting_x_test(self, indices) -> torch.Tensor:
+        self.inducting_x_test = self.data_x_test[torch.as_tensor(indices, device=self.data_x_test.device)]
+        return self.inducting_x_test
+
+    def _subset(self, idx):
+        separate = not (self.data_x_train.shape == self.data_x_test.shape and
+                        bool(torch.equal(self.data_x_train, self.data_x_test)))
+        idx = idx.to(self.data_x_train.device)
+        xs, ys = (self.data_x_test, self.data_y_test) if separate else (self.data_x_train, self.data_y_train)
+        d = DataInput(self.data_x_train[idx], self.data_y_train[idx], xs, ys)
+        d.set_mean_function(self.mean_function)
+        return d
+
+    def get_random_subset(self, subset_size: int):
+        """subset_size training records drawn uniformly WITH replacement and sorted
+        (DataInput.py:126-145).  The draw uses torch's generator seeded with self.seed, not
+        TensorFlow's stateless Philox stream, so the indices differ from the reference's."""
+        gen = torch.Generator().manual_seed(int(self.seed))
+        idx = torch.sort(torch.randint(0, self.n_train, (int(subset_size),), generator=gen)).values
+        return self._subset(idx)
+
+    def get_grid_subset(self, subset_size: int):
+        """Every (n / subset_size)-th training record: linspace(0, n, subset_size, endpoint=False)
+        cast to int (DataInput.py:147-167) -- the reference's exact indices."""
+        import numpy as np
+        idx = torch.as_tensor(np.linspace(start=0, stop=self.n_train, num=int(subset_size), endpoint=False, dtype=int))
+        return self._subset(idx)
+
+    def get_subset(self, subset_size: int, subset_of_data_approach):
+        from ..Metrics import MatrixHandlingTypes as mht
+        if subset_of_data_approach is mht.SubsetOfDataApproaches.SOD_GRID:
+            return self.get_grid_subset(subset_size)
+        if subset_of_data_approach is mht.SubsetOfDataApproaches.SOD_RANDOM:
+            return self.get_random_subset(subset_size)
+        raise Exception("Invalid subset-of-data approach: %s" % str(subset_of_data_approach))
+
+
 class BatchDataInput(AbstractDataInput):
     """B data sets evaluated together: X [B, N, D], y [B, N, 1] (BatchDataInput.py:24-28)."""
 

@@ -48,6 +48,8 @@ class LogLikelihood(AbstractLogLikelihood):
             # differentiable form: what the reference's tf.GradientTape sees through get_metric
             # (Optimizer/Fitter.py:104-158); backward() uses the analytic device gradient
             return _NegLogLikelihood.apply(self, _as_tensor(noise), *[_as_tensor(h) for h in hyper_parameter])
+        if self.numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
+            return self._get_metric_by_strategy(hyper_parameter, noise, indices)
         f = self.covariance_matrix.factorization(hyper_parameter, noise)
         if self.data_input.data_x_train.dim() == 3:
             n = float(self.data_input.n_train)
@@ -57,6 +59,17 @@ class LogLikelihood(AbstractLogLikelihood):
             agg = global_param.p_batch_metric_aggregator or torch.mean
             return -agg(ll)
         return f.nlml().reshape(1, 1)
+
+    def _get_metric_by_strategy(self, hyper_parameter: List, noise, indices=None) -> torch.Tensor:
+        """The reference's formula with the bound get_alpha / get_log_determinant (LogLikelihood.py:36-49)
+        for the STRICT / PSEUDO inverse and linear-CG handlings."""
+        y = self.data_input.get_detrended_y_train().reshape(-1, 1).to(torch.float64)
+        alpha = self.get_alpha(hyper_parameter, noise, y, indices).reshape(-1, 1)
+        fit = torch.sum(y * alpha)
+        logdet = self.get_log_determinant(hyper_parameter, noise, indices)
+        n = float(self.data_input.n_train)
+        ll = (-0.5 * fit + -0.5 * logdet) + (-0.5 * (n * LOG_2PI))
+        return -ll.reshape(1, 1)
 
     def get_metric_and_gradient(self, hyper_parameter: List, noise, reset: bool = True):
         """(-LML [1, 1], [d(-LML)/d h for h in hyper_parameter] (each shaped like h), d(-LML)/d noise).

@@ -52,7 +52,15 @@ class MeanSquaredError(AbstractMSE):
         return torch.mean((mu - yt) ** 2)
 
     def get_posterior_mu(self, hyper_parameter: List, noise, indices=None):
-        return posterior_mu(self.covariance_matrix.kernel, hyper_parameter, noise, self.data_input)
+        """K_s^T alpha (MeanSquaredError.py:33-42).  CHOLESKY_BASED: one augmented factorisation with
+        the test rows; the other handlings: their alpha (Metrics.get_alpha) and one device GEMV."""
+        from .. import engine
+        from . import MatrixHandlingTypes as mht
+        if self.numerical_matrix_handling is mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
+            return posterior_mu(self.covariance_matrix.kernel, hyper_parameter, noise, self.data_input)
+        alpha = self.get_alpha(hyper_parameter, noise, None, indices)
+        ks_t = self.covariance_matrix.get_K_s(hyper_parameter).transpose(0, 1).contiguous()
+        return engine.gemv(ks_t, alpha.reshape(-1)).reshape(-1)
 
 
 class BlockwiseMeanSquaredError(AbstractMetric):

@@ -1,9 +1,20 @@
-"""Metric framework (gpbasics/Metrics/Metrics.py:17-154), CHOLESKY_BASED strategy on the device.
+"""Metric framework (gpbasics/Metrics/Metrics.py:17-154) on the device.
 
 The reference binds ``get_alpha`` / ``get_log_determinant`` per numerical handling
-(Metrics.py:82-107).  The device engine implements the default pair, CHOLESKY_BASED with no
-approximation (Metrics.py:85-87, :138-139, :152-154); the other strategies raise
-``NotImplementedError`` naming SURVEY §8f.
+(Metrics.py:82-107); the same binding happens here:
+
+  CHOLESKY_BASED (default)   alpha = L^-T L^-1 y, logdet = 2 sum log diag L     (:138-139, :152-154)
+  STRICT_INVERSE             alpha = inv(K) y: K^-1 from the identity-augmented factorisation,
+                             one device GEMV; logdet = slogdet(K)                (:132-133, :148-149)
+  PSEUDO_INVERSE             alpha = pinv(K) y: equal to inv(K) y for the positive-definite K the
+                             kernels produce; a K that is not positive definite (where pinv's
+                             rank truncation would matter) raises NotImplementedError (:135-136)
+  LINEAR_CONJUGATE_GRADIENT  alpha = linear_cg(K, y, 0) (device GEMV per iteration) (:141-144)
+
+slogdet(K)[1] is log|det K| = 2 sum log diag L for a positive-definite K (the device Cholesky);
+for any other K it raises NotImplementedError (the reference's LU-based slogdet is not provided).
+Subset-of-data approximations (SOD_GRID, SOD_RANDOM) evaluate the exact path on the subset
+(:60-68); the Nystroem / SKC / SKI approximations are not provided and raise.
 """
 from __future__ import annotations
 
@@ -40,32 +51,86 @@ class AbstractMetric:
 class Metric(AbstractMetric):
     def __init__(self, data_input, covariance_matrix, metric_type: MetricType, local_approx,
                  numerical_matrix_handling, subset_size: int = None):
-        if local_approx is not mht.MatrixApproximations.NONE and not (
-                subset_size is not None and subset_size >= data_input.n_train):
-            raise NotImplementedError("approximation %s is SURVEY §8f 'next'; the device engine is exact" % local_approx)
-        if numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
-            raise NotImplementedError("numerical handling %s is SURVEY §8f 'next'; use CHOLESKY_BASED"
-                                      % numerical_matrix_handling)
         self.covariance_matrix = covariance_matrix
-        self.local_approx = mht.MatrixApproximations.NONE
+        self.local_approx = local_approx
         self.numerical_matrix_handling = numerical_matrix_handling
         self.subset_size = subset_size
-        self.data_input = data_input
+        if self.local_approx is not mht.MatrixApproximations.NONE and self.subset_size is None:
+            self.subset_size = int(data_input.n_train * global_param.p_nystroem_ratio)     # :54-55
+        if self.subset_size is not None and self.subset_size >= data_input.n_train:
+            self.local_approx = mht.MatrixApproximations.NONE                              # :57-58
+        if isinstance(self.local_approx, mht.SubsetOfDataApproaches):                      # :60-66
+            self.data_input = data_input.get_subset(subset_size=self.subset_size,
+                                                    subset_of_data_approach=self.local_approx)
+        elif self.local_approx is not mht.MatrixApproximations.NONE:
+            raise NotImplementedError("approximation %s (Nystroem / SKC / SKI) is not provided by the device engine "
+                                      "(SURVEY §8f.4); use NONE or a subset-of-data approach" % self.local_approx)
+        else:
+            self.data_input = data_input
         self.covariance_matrix.set_data_input(self.data_input)
         self.type = metric_type
         self.last_covariance_matrix = None
+        h = mht.NumericalMatrixHandlingType
+        if numerical_matrix_handling is h.PSEUDO_INVERSE:                                  # :82-94
+            self.get_alpha, self.get_log_determinant = self.get_alpha_pseudo_inverse, self.get_log_determinant_slodget
+        elif numerical_matrix_handling is h.CHOLESKY_BASED:
+            self.get_alpha, self.get_log_determinant = self.get_alpha_cholesky, self.get_log_determinant_cholesky
+        elif numerical_matrix_handling is h.LINEAR_CONJUGATE_GRADIENT:
+            self.get_alpha, self.get_log_determinant = self.get_alpha_lcg, self.get_log_determinant_slodget
+        else:
+            self.get_alpha, self.get_log_determinant = self.get_alpha_strict_inverse, self.get_log_determinant_slodget
 
     def get_covariance_matrix(self, hyper_parameter: List, noise, indices=None):
         if self.last_covariance_matrix is None:
             self.last_covariance_matrix = self.covariance_matrix.get_K_noised(hyper_parameter, noise)
         return self.last_covariance_matrix
 
-    def get_alpha(self, hyper_parameter: List, noise, y=None, indices=None):
+    def _y(self, y):
+        return (self.data_input.get_detrended_y_train() if y is None else y).reshape(-1, 1).to(torch.float64)
+
+    def _require_plain(self):
+        if self.data_input.data_x_train.dim() == 3:
+            raise NotImplementedError("numerical handling %s is provided for DataInput, not BatchDataInput"
+                                      % self.numerical_matrix_handling)
+
+    def get_alpha_cholesky(self, hyper_parameter: List, noise, y=None, indices=None):
         """get_alpha_cholesky (Metrics.py:138-139)."""
         return self.covariance_matrix.get_L_alpha(hyper_parameter, noise)
 
-    def get_log_determinant(self, hyper_parameter: List, noise, indices=None):
+    def get_alpha_strict_inverse(self, hyper_parameter: List, noise, y=None, indices=None):
+        """inv(K) y (Metrics.py:132-133): the explicit inverse, then one device GEMV."""
+        from .. import engine
+        self._require_plain()
+        return engine.gemv(self.covariance_matrix.get_K_inv(hyper_parameter, noise).contiguous(), self._y(y))
+
+    def get_alpha_pseudo_inverse(self, hyper_parameter: List, noise, y=None, indices=None):
+        """pinv(K) y (Metrics.py:135-136) = inv(K) y for a positive-definite K (raises otherwise)."""
+        from .. import engine
+        self._require_plain()
+        f = self.covariance_matrix.factorization(hyper_parameter, noise)
+        if int(f.info.abs().max()) != 0:
+            raise NotImplementedError("pinv of a matrix that is not positive definite is not provided")
+        return self.get_alpha_strict_inverse(hyper_parameter, noise, y, indices)
+
+    def get_alpha_lcg(self, hyper_parameter: List, noise, y=None, indices=None):
+        """linear_cg(K, y, 0) (Metrics.py:141-144; Auxiliary/LinearConjugateGradients.py)."""
+        from ..Auxiliary.LinearConjugateGradients import linear_cg
+        self._require_plain()
+        yv = self._y(y)
+        return linear_cg(self.get_covariance_matrix(hyper_parameter, noise, indices).contiguous(), yv,
+                         torch.zeros_like(yv))
+
+    def get_log_determinant_cholesky(self, hyper_parameter: List, noise, indices=None):
         """2 * reduce_sum(log(diag L)) (Metrics.py:152-154); summed over the whole batch for
         BatchDataInput, exactly like the reference's axis-free reduce_sum (quirk Q7)."""
         f = self.covariance_matrix.factorization(hyper_parameter, noise)
+        return torch.sum(f.logdet())
+
+    def get_log_determinant_slodget(self, hyper_parameter: List, noise, indices=None):
+        """slogdet(K)[1] = log|det K| (Metrics.py:146-147), from the device Cholesky for a
+        positive-definite K; other K raise NotImplementedError."""
+        self._require_plain()
+        f = self.covariance_matrix.factorization(hyper_parameter, noise)
+        if int(f.info.abs().max()) != 0:
+            raise NotImplementedError("slogdet of a matrix that is not positive definite is not provided")
         return torch.sum(f.logdet())

@@ -29,7 +29,7 @@ EXPORTS = (
     "gpk_finalize", "gpk_nlml", "gpk_kernel_matrix", "gpk_trsv", "gpk_timing_enable",
     "gpk_timing_read", "gpk_timing_reset", "gpk_tune", "gpk_potrf_aug_ex", "gpk_assemble_inverse",
     "gpk_grad_workspace_bytes", "gpk_nlml_grad", "gpk_assemble_ragged", "gpk_potrf_aug_ragged",
-    "gpk_finalize_ragged", "gpk_nlml_ragged",
+    "gpk_finalize_ragged", "gpk_nlml_ragged", "gpk_gemv",
 )
 
 
@@ -92,6 +92,7 @@ def _declare(lib):
         "gpk_finalize_ragged": (c_int, [POINTER(GpkLayout), P, P, P, P, P, P, P]),
         "gpk_nlml_ragged": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64, P,
                                     c_int64, P, c_int64, P, P, P, P, P, P]),
+        "gpk_gemv": (c_int, [P, c_int64, c_int64, c_int64, P, P, c_double, c_double, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

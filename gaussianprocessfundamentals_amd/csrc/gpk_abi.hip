@@ -712,6 +712,21 @@ int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, 
   return 0;
 }
 
+int gpk_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x, double* y, double alpha,
+             double beta, void* stream) {
+  if (!A) return fail_arg(1, "A");
+  if (n < 0) return fail_arg(2, "n");
+  if (m < 0) return fail_arg(3, "m");
+  if (lda < m) return fail_arg(4, "lda");
+  if (!x && m > 0) return fail_arg(5, "x");
+  if (!y && n > 0) return fail_arg(6, "y");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(timed(5, 2.0 * (double)n * (double)m, 8.0 * (double)n * (double)m, s,
+                [&] { return launch_gemv(A, n, m, lda, x, y, alpha, beta, s); }),
+          "gemv");
+  return 0;
+}
+
 int gpk_timing_enable(int on) {
   std::lock_guard<std::mutex> lk(g_timing.mu);
   g_timing.on = on != 0;

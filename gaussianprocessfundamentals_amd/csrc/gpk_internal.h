@@ -130,6 +130,8 @@ hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream
 hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_trsv_diag(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
+hipError_t launch_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x, double* y,
+                       double alpha, double beta, hipStream_t s);
 
 enum { GEMM_UPDATE = 0, GEMM_TRSM = 1 };
 

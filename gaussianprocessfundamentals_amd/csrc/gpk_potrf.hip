@@ -398,6 +398,38 @@ __global__ __launch_bounds__(256) void trsv_update_kernel(TrsvArgs a) {
   }
 }
 
+
+// ================================================================================ matrix-vector
+// y <- alpha A x + beta y, A row-major fp64 [n, m] (ld).  HBM-bound (8 n m bytes): one wave per
+// row, lanes stride the row with 16-B loads (two fp64 each), wave reduction by shuffles.  Used by
+// the iterative / explicit-inverse numerical handlings (linear_cg, inv(K) y) of the metrics.
+__global__ __launch_bounds__(256) void gemv_kernel(const double* __restrict__ A, int64_t n, int64_t m, int64_t lda,
+                                                   const double* __restrict__ x, double* __restrict__ y,
+                                                   double alpha, double beta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const double* a = A + row * lda;
+  double s0 = 0.0, s1 = 0.0;
+  const bool vec = ((lda & 1) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+  int64_t j = 0;
+  if (vec) {
+    typedef double dbl2 __attribute__((ext_vector_type(2)));
+    for (; j + 2 * 64 <= m; j += 2 * 64) {
+      const dbl2 av = *reinterpret_cast<const dbl2*>(a + j + 2 * lane);
+      const dbl2 xv = *reinterpret_cast<const dbl2*>(x + j + 2 * lane);
+      s0 = fma(av.x, xv.x, s0);
+      s1 = fma(av.y, xv.y, s1);
+    }
+  }
+  for (int64_t k = j + lane; k < m; k += 64) s0 = fma(a[k], x[k], s0);
+  double sum = s0 + s1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if (lane == 0) y[row] = alpha * sum + (beta == 0.0 ? 0.0 : beta * y[row]);
+}
+
 template <typename T, int MODE, int TM, int TN, int WN = 2>
 hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
   // a.nt / c_lo / c_hi are in units of this launch's tile sizes
@@ -443,6 +475,13 @@ hipError_t launch_trsv_diag(const TrsvArgs& a, int dtype, int32_t batch, hipStre
     hipLaunchKernelGGL(trsv_diag_kernel<double>, dim3(batch), dim3(NB), 0, s, a);
   else
     hipLaunchKernelGGL(trsv_diag_kernel<float>, dim3(batch), dim3(NB), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x, double* y,
+                       double alpha, double beta, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gemv_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, A, n, m, lda, x, y, alpha, beta);
   return hipGetLastError();
 }
 

@@ -462,3 +462,25 @@ class RaggedFactorization(AugmentedFactorization):
 
     def alpha(self, b: int = 0) -> torch.Tensor:
         return self.alphas()[b]
+
+
+def gemv(A: torch.Tensor, x: torch.Tensor, y: Optional[torch.Tensor] = None, alpha: float = 1.0,
+         beta: float = 0.0) -> torch.Tensor:
+    """y <- alpha A x + beta y on the device (gpk_gemv; A row-major fp64 [n, m], x [m] or [m, 1]).
+    Returns y with x's trailing shape ([n] or [n, 1])."""
+    if A.dim() != 2 or A.dtype != torch.float64 or A.stride(1) != 1:
+        raise ValueError("A must be a row-major float64 matrix")
+    n, m = int(A.shape[0]), int(A.shape[1])
+    xv = x.reshape(-1)
+    if xv.numel() != m or xv.dtype != torch.float64:
+        raise ValueError("x must hold %d float64 values" % m)
+    xv = xv.contiguous()
+    out_shape = (n, 1) if x.dim() == 2 else (n,)
+    if y is None:
+        y = torch.empty(out_shape, dtype=torch.float64, device=A.device)
+        beta = 0.0
+    elif y.numel() != n or not y.is_contiguous():
+        raise ValueError("y must be a contiguous tensor of %d values" % n)
+    nat.check(nat.lib().gpk_gemv(nat.ptr(A), n, m, int(A.stride(0)), nat.ptr(xv), nat.ptr(y), float(alpha),
+                                 float(beta), nat.stream_handle(A.device)), "gpk_gemv")
+    return y

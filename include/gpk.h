@@ -222,6 +222,13 @@ int gpk_kernel_matrix(const gpk_kdesc* kd, const double* hyp_dev, int dtype, int
 int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, double* x,
              void* stream);
 
+/* y <- alpha A x + beta y for a row-major fp64 matrix A [n, m] (leading dimension lda >= m).
+ * The matrix-vector products of the non-Cholesky numerical handlings of the metrics:
+ * A p_k of linear_cg (Auxiliary/LinearConjugateGradients.py:44-45) and inv(K) y of
+ * get_alpha_strict_inverse (Metrics/Metrics.py:132-133).  Timed under class 5. */
+int gpk_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x, double* y, double alpha,
+             double beta, void* stream);
+
 /* Per-kernel-class timing with HIP events recorded on the launch stream.
  * class: 0 assemble, 1 diag, 2 trsm, 3 update, 4 finalize, 5 trsv, 6 grad */
 #define GPK_NUM_CLASSES 7

@@ -310,6 +310,41 @@ def cv_folds(n: int, test_ratio: float = 0.2):
     return out
 
 
+def linear_cg(A, b, x):
+    """linear_cg (A/LinearConjugateGradients.py:9-41): CG from x with the reference's stopping rule
+    |max(r_k)| > 1e-2 (absolute value of the maximum) and its n-iteration guard."""
+    n = A.shape[0]
+    b = np.asarray(b, dtype=np.float64).reshape(-1, 1)
+    x = np.asarray(x, dtype=np.float64).reshape(-1, 1).copy()
+    r = A @ x - b
+    p = -r
+    k = 0
+    first = True
+    while first or abs(np.max(r)) > 1e-2:
+        Ap = A @ p
+        rr = float((r.T @ r)[0, 0])
+        a = rr / float((p.T @ Ap)[0, 0])
+        nx = x + a * p
+        if np.any(np.isnan(nx)):
+            return x
+        x = nx
+        r2 = r + a * Ap
+        beta = float((r2.T @ r2)[0, 0]) / rr
+        p = -r2 + beta * p
+        r = r2
+        k += 1
+        first = False
+        if k % (n / 4) == 0 and k > n:
+            break
+    return x
+
+
+def nlml_with_alpha(alpha, y, logdet, n) -> float:
+    """-LML from a given alpha and log-determinant (M/LogLikelihood.py:36-49)."""
+    fit = float(np.asarray(y).reshape(-1) @ np.asarray(alpha).reshape(-1))
+    return -((-0.5 * fit + -0.5 * logdet) + (-0.5 * (n * LOG_2PI)))
+
+
 # ---------------------------------------------------------------- synthetic configs (SURVEY §8d)
 def make_inputs(cfg: str, n: int = None, seed: int = None) -> Tuple[np.ndarray, np.ndarray]:
     """Synthetic data generators of SURVEY §8(d) (numpy default_rng(seed))."""

@@ -120,9 +120,11 @@ def test_metric_strategy_rejection_messages():
     class Dummy:
         n_train = 10
 
-    with pytest.raises(NotImplementedError):
-        Metric(Dummy(), None, MetricType.LL, mht.MatrixApproximations.NONE,
-               mht.NumericalMatrixHandlingType.STRICT_INVERSE)
+    # Nystroem / SKC / SKI approximations are not provided by the device engine
+    for approx in (mht.MatrixApproximations.BASIC_NYSTROEM, mht.MatrixApproximations.SKI,
+                   mht.MatrixApproximations.SKC_LOWER_BOUND):
+        with pytest.raises(NotImplementedError):
+            Metric(Dummy(), None, MetricType.LL, approx, mht.NumericalMatrixHandlingType.CHOLESKY_BASED, subset_size=5)
 
 
 @pytest.mark.parametrize("n,world", [(128, 1), (128, 2), (128, 8), (10, 3), (3, 8), (0, 4)])
