@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="hyperparameter candidates factorised together per rank per step "
                          "(default: %d for the metric config, 1 otherwise)" % DEFAULT_BATCH)
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="factorisation buffers / streams that consecutive steps rotate over (overlap of batches)")
+    ap.add_argument("--lookahead", type=int, default=None,
+                    help="panel look-ahead on side streams (default: on, off when --pipeline > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events")
@@ -226,22 +230,36 @@ def main():
     H = torch.tensor(rows, dtype=torch.float64, device=dev).contiguous()
     NZ = torch.tensor([noise], dtype=torch.float64, device=dev)
     grad_mode = args.mode == "grad"
+    # --pipeline P: P factorisation buffers on P streams, consecutive steps round-robin over them,
+    # so that one batch's exposed panel chain (start and tail of the factorisation) overlaps the
+    # trailing updates of the next (the batches are independent candidate sets of the sweep)
+    P = max(1, args.pipeline)
+    la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 1)
+    nat.tune("lookahead", la)
     if grad_mode:
-        fact = engine.InverseFactorization(n, d, batch, dt)
+        facts = [engine.InverseFactorization(n, d, batch, dt) for _ in range(P)]
     else:
-        fact = engine.AugmentedFactorization(n, d, 0, batch, dt)
-    gathered = torch.empty(2 * chunk * world, dtype=torch.float64, device=dev) if world > 1 else None
-    mine = torch.full((2 * chunk,), float("nan"), dtype=torch.float64, device=dev)
+        facts = [engine.AugmentedFactorization(n, d, 0, batch, dt) for _ in range(P)]
+    fact = facts[0]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(P - 1)]
+    step_no = [0]
+    gathered = [torch.empty(2 * chunk * world, dtype=torch.float64, device=dev) if world > 1 else None
+                for _ in range(P)]
+    mine = [torch.full((2 * chunk,), float("nan"), dtype=torch.float64, device=dev) for _ in range(P)]
 
-    def step():
-        if grad_mode:
-            fact.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0, gradient=True)
-        else:
-            fact.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
-        if world > 1:
-            mine[:batch] = fact.nlml()
-            mine[chunk:chunk + batch] = fact.info.to(torch.float64)
-            dist.all_gather_into_tensor(gathered, mine)
+    def step(slot=None):
+        i = step_no[0] % P if slot is None else slot
+        step_no[0] += 1
+        f = facts[i]
+        with torch.cuda.stream(streams[i]):
+            if grad_mode:
+                f.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0, gradient=True)
+            else:
+                f.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
+            if world > 1:
+                mine[i][:batch] = f.nlml()
+                mine[i][chunk:chunk + batch] = f.info.to(torch.float64)
+                dist.all_gather_into_tensor(gathered[i], mine[i])
 
     for _ in range(args.warmup):
         step()
@@ -279,12 +297,12 @@ def main():
     iso = None
     if use_events:
         old_la = nat.tune("lookahead", 0)
-        step()
+        step(slot=0)
         torch.cuda.synchronize()
         nat.timing_reset()
         nat.timing_enable(True)
         for _ in range(args.roofline_steps):
-            step()
+            step(slot=0)
         torch.cuda.synchronize()
         nat.timing_enable(False)
         iso = nat.timing_read()
@@ -347,6 +365,10 @@ def main():
                                    ("%s GP -LML, kernel=%s, D=%d, N=%d, noise=%g; %d candidate evaluations per rank per step (batched factorisation)"
                                     % (args.config, kname, d, n, noise, batch)),
                        "candidates_per_rank_step": batch,
+                       "batches_in_flight": P,
+                       "schedule": ("consecutive steps rotate over %d factorisation buffers on %d HIP streams (one "
+                                    "batch's panel chain overlaps the next batch's trailing updates), panel "
+                                    "look-ahead %s" % (P, P, "on" if la else "off")),
                        "n": n, "d": d, "kernel": kname, "panel": int(lay.nb), "parallelism": "dp%d (independent candidates)" % world},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -30,8 +30,15 @@ def shard_range(n_items: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def native_batched_evaluator(kernel, X: torch.Tensor, y: torch.Tensor, noise, dtype=None,
-                             max_batch: Optional[int] = None) -> Callable[[torch.Tensor], torch.Tensor]:
+                             max_batch: Optional[int] = None,
+                             pipeline: int = 1) -> Callable[[torch.Tensor], torch.Tensor]:
     """Evaluator running gpk_assemble/gpk_potrf_aug/gpk_finalize over candidate batches.
+
+    Candidates are factored in chunks of ``max_batch`` (all at once when None).  With
+    ``pipeline`` = P > 1 the chunks rotate over P factorisation buffers on P HIP streams, so one
+    chunk's exposed panel chain overlaps the next chunk's trailing updates (the panel look-ahead
+    is then left to the pipelining: each chunk runs its kernels on its own stream).  The result is
+    ordered on the caller's stream.
 
     Returns f(cands [c, n_hyp] fp64) -> [c, 2] fp64 device tensor of (nlml, info)."""
     X = engine.as_device_f64(X)
@@ -42,6 +49,8 @@ def native_batched_evaluator(kernel, X: torch.Tensor, y: torch.Tensor, noise, dt
     nv = noise_vector(noise)
     dt = dtype or gp.p_dtype
     cache = {}
+    P = max(1, int(pipeline))
+    streams = [torch.cuda.Stream(X.device) for _ in range(P - 1)] if P > 1 else []
 
     def evaluate(cands: torch.Tensor) -> torch.Tensor:
         cands = cands.to(device=X.device, dtype=torch.float64).contiguous()
@@ -52,17 +61,32 @@ def native_batched_evaluator(kernel, X: torch.Tensor, y: torch.Tensor, noise, dt
         if cands.shape[1] != kd.n_hyp:
             raise ValueError("candidate rows must have %d hyperparameter values" % kd.n_hyp)
         step = c if max_batch is None else max(1, int(max_batch))
-        for s0 in range(0, c, step):
-            s1 = min(c, s0 + step)
-            b = s1 - s0
-            f = cache.get(b)
-            if f is None:
-                f = engine.AugmentedFactorization(n, d, 0, b, dt)
-                cache.clear()
-                cache[b] = f
-            f.run(kd, cands[s0:s1], kd.n_hyp, nv, 0, X, 0, yv, 0)
-            out[s0:s1, 0] = f.nlml()
-            out[s0:s1, 1] = f.info.to(torch.float64)
+        caller = torch.cuda.current_stream(X.device)
+        slots = [caller] + streams
+        for st in streams:
+            st.wait_stream(caller)
+        old_la = None
+        if P > 1:
+            from . import _native as nat
+            old_la = nat.tune("lookahead", 0)
+        try:
+            for i, s0 in enumerate(range(0, c, step)):
+                s1 = min(c, s0 + step)
+                b = s1 - s0
+                slot = i % P
+                f = cache.get((b, slot))
+                if f is None:
+                    f = engine.AugmentedFactorization(n, d, 0, b, dt)
+                    cache[(b, slot)] = f
+                with torch.cuda.stream(slots[slot]):
+                    f.run(kd, cands[s0:s1], kd.n_hyp, nv, 0, X, 0, yv, 0)
+                    out[s0:s1, 0] = f.nlml()
+                    out[s0:s1, 1] = f.info.to(torch.float64)
+        finally:
+            if old_la is not None:
+                nat.tune("lookahead", old_la)
+        for st in streams:
+            caller.wait_stream(st)
         return out
 
     return evaluate

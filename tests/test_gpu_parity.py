@@ -337,6 +337,20 @@ def test_sweep_matches_single_evaluations():
     assert best == int(np.argmin(exp))
 
 
+@pytest.mark.parametrize("pipeline", [2, 3])
+def test_pipelined_sweep_chunks_match_single_evaluations(pipeline):
+    """Chunks rotating over P buffers / streams give the same results, in candidate order."""
+    x, y = o.make_inputs("C1", n=700, seed=6)
+    k = make_kernel(SE, 1)
+    cands = torch.tensor([[v] for v in np.geomspace(0.02, 0.5, 23)], dtype=torch.float64)
+    ev = native_batched_evaluator(k, x, y, 1e-2, max_batch=5, pipeline=pipeline)
+    for _ in range(2):   # buffers are reused across calls
+        nlml, info, best = HyperparameterSweep(ev).run(cands)
+        exp = [o.nlml(SE, [float(c)], 1e-2, x, y) for c in cands[:, 0]]
+        assert np.max(np.abs(nlml.cpu().numpy() - exp) / np.abs(exp)) < 1e-10
+        assert best == int(np.argmin(exp)) and int(info.abs().max()) == 0
+
+
 # ------------------------------------------------------------------------------ schedules
 @pytest.mark.parametrize("group,group_first", [(1, 1), (2, 2), (3, 1), (4, 4), (5, 2), (8, 2), (8, 3), (8, 8)])
 @pytest.mark.parametrize("lookahead", [0, 1])
