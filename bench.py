@@ -55,8 +55,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="hyperparameter candidates factorised together per rank per step "
                          "(default: %d for the metric config, 1 otherwise)" % DEFAULT_BATCH)
-    ap.add_argument("--pipeline", type=int, default=3,
-                    help="factorisation buffers / streams that consecutive steps rotate over (overlap of batches)")
+    ap.add_argument("--pipeline", type=int, default=None,
+                    help="factorisation buffers / streams that consecutive steps rotate over (overlap of batches); "
+                         "default 3 on one GPU, 2 with --gpus > 1 (RCCL's stream then keeps the process within "
+                         "GPU_MAX_HW_QUEUES = 4 hardware queues)")
     ap.add_argument("--lookahead", type=int, default=None,
                     help="panel look-ahead on side streams (default: on, off when --pipeline > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
@@ -233,7 +235,7 @@ def main():
     # --pipeline P: P factorisation buffers on P streams, consecutive steps round-robin over them,
     # so that one batch's exposed panel chain (start and tail of the factorisation) overlaps the
     # trailing updates of the next (the batches are independent candidate sets of the sweep)
-    P = max(1, args.pipeline)
+    P = max(1, args.pipeline if args.pipeline is not None else (3 if world == 1 else 2))
     la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 1)
     nat.tune("lookahead", la)
     if grad_mode:
