@@ -29,6 +29,7 @@ def _hipcc() -> str:
 def _inputs():
     files = [os.path.join(CSRC, s) for s in SOURCES]
     files.append(os.path.join(CSRC, "gpk_internal.h"))
+    files.append(os.path.join(CSRC, "gpk_kernels.h"))
     files.append(os.path.join(INCLUDE, "gpk.h"))
     return files
 

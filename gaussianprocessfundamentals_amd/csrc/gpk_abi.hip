@@ -139,6 +139,7 @@ struct Tune {
   int64_t reserve_cus;    // CUs kept free of the bulk trailing update for the panel chain
   int64_t group;          // panels per trailing update (K = 128 group)
   int64_t group_first;    // panels of the first group (a short first chain lets the bulk start early)
+  int64_t fuse_kbuild;    // gpk_nlml: K build fused into the first trailing update (single-node kernels)
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -150,7 +151,7 @@ Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
-                         env_i64("GPK_GROUP_FIRST", 8)};
+                         env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1)};
   return t;
 }
 
@@ -267,7 +268,8 @@ static int assemble_impl(const gpk_kdesc* kd, const gpk_layout* lay, const doubl
                          int64_t hyp_stride, const double* noise_dev, int64_t noise_stride,
                          const double* X, int64_t x_bstride, const double* Xs, int64_t xs_bstride,
                          const double* E, int64_t e_bstride, const double* y, int64_t y_bstride,
-                         void* W, bool eye, const int64_t* n_dev, const int64_t* m_dev, void* stream) {
+                         void* W, bool eye, const int64_t* n_dev, const int64_t* m_dev, void* stream,
+                         int64_t tcol_hi = 0) {
   if (int e = check_layout(lay)) return e;
   if (!valid_kdesc(kd, lay->d)) return fail_arg(1, "kernel descriptor");
   if (!hyp_dev && kd->n_hyp > 0) return fail_arg(3, "hyp_dev");
@@ -306,10 +308,12 @@ static int assemble_impl(const gpk_kdesc* kd, const gpk_layout* lay, const doubl
   a.ntile = lay->p / ATILE;
   a.nb = n_dev;
   a.mb = m_dev;
+  a.tcol_hi = tcol_hi;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const double es = (double)elem_size(lay->dtype);
+  const double cols = (tcol_hi > 0 && tcol_hi < a.ntile) ? (double)(tcol_hi * ATILE) : (double)lay->p;
   const double bytes = (double)lay->batch *
-                       (es * (double)lay->p * (double)(lay->p + ATILE) / 2.0 +
+                       (es * (cols * (double)lay->p - cols * (cols - (double)ATILE) / 2.0) +
                         8.0 * (double)(lay->n + lay->m) * (double)lay->d + 8.0 * (double)lay->n);
   GPK_HIP(timed(0, 0.0, bytes, s, [&] { return launch_assemble(*kd, a, lay->dtype, lay->batch, s); }),
           "assemble");
@@ -346,7 +350,7 @@ int gpk_assemble_inverse(const gpk_kdesc* kd, const gpk_layout* lay, const doubl
 }
 
 static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, int32_t flags,
-                      const int64_t* n_dev, const int64_t* m_dev, void* stream) {
+                      const int64_t* n_dev, const int64_t* m_dev, void* stream, const GemmArgs* kb = nullptr) {
   if (int e = check_layout(lay)) return e;
   if (!W) return fail_arg(2, "W");
   if (!Winv) return fail_arg(3, "Winv");
@@ -426,8 +430,23 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   };
   // trailing update from panel columns [j0, j0 + kdepth) of the lower tiles whose 128-column
   // block lies in [c_lo, c_hi) (relative to row0 = j0 + kdepth; c_hi < 0: to the end)
-  auto update = [&](int64_t j0, int kdepth, int64_t c_lo, int64_t c_hi, hipStream_t st) -> hipError_t {
+  auto update = [&](int64_t j0, int kdepth, int64_t c_lo, int64_t c_hi, hipStream_t st,
+                    bool fused_k = false) -> hipError_t {
     GemmArgs ga = base;
+    if (fused_k && kb) {  // first trailing update: C is evaluated, not loaded (gpk_nlml's fused K build)
+      ga.kbuild = 1;
+      ga.d = kb->d;
+      ga.n = kb->n;
+      ga.node = kb->node;
+      ga.hyp = kb->hyp;
+      ga.hyp_stride = kb->hyp_stride;
+      ga.noise = kb->noise;
+      ga.noise_stride = kb->noise_stride;
+      ga.X = kb->X;
+      ga.x_bs = kb->x_bs;
+      ga.y = kb->y;
+      ga.y_bs = kb->y_bs;
+    }
     ga.j0 = j0;
     ga.row0 = j0 + kdepth;
     ga.kdepth = kdepth;
@@ -470,7 +489,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // panel chain).  A deeper K halves the read-modify-write passes over the trailing matrix per
   // doubling of G.  The first group has G0 <= G panels: its chain is exposed (nothing to overlap
   // yet), so a short one lets the first bulk update start early.
-  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tn.group, 8));
+  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tn.group, 16));
   const int64_t G0 = std::max<int64_t>(1, std::min<int64_t>(tn.group_first, G));
   if (la) {
     GPK_HIP(hipEventRecord(ss->fork, s), "event");
@@ -490,14 +509,14 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
     }
     const int kd = (int)((gend - g0) * NB);
     if (!la) {
-      GPK_HIP(update(g0 * NB, kd, 0, -1, s), "update");
+      GPK_HIP(update(g0 * NB, kd, 0, -1, s, g0 == 0), "update");
       continue;
     }
     GPK_HIP(hipEventRecord(ss->panel, sp), "event");      // panels g0 .. gend-1 solved
     if (bulk_pending) GPK_HIP(hipStreamWaitEvent(sp, ss->bulk, 0), "event");
-    GPK_HIP(update(g0 * NB, kd, 0, G, sp), "update look-ahead");
+    GPK_HIP(update(g0 * NB, kd, 0, G, sp, g0 == 0), "update look-ahead");
     GPK_HIP(hipStreamWaitEvent(sb, ss->panel, 0), "event");
-    GPK_HIP(update(g0 * NB, kd, G, -1, sb), "update bulk");
+    GPK_HIP(update(g0 * NB, kd, G, -1, sb, g0 == 0), "update bulk");
     GPK_HIP(hipEventRecord(ss->bulk, sb), "event");
     bulk_pending = true;
   }
@@ -589,6 +608,36 @@ int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, 
   if (!info_dev) return fail_arg(13, "info_dev");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   GPK_HIP(hipMemsetAsync(info_dev, 0, sizeof(int32_t) * lay->batch, s), "memset info");
+  // Fused K build (single-base-node kernels): only the first panel group's block columns are
+  // assembled; the first trailing update evaluates its C tiles instead of reading them, so the
+  // trailing part of K is never written to HBM and read back.
+  const Tune& tn = tune();
+  const int64_t nblk = lay->n_pad / NB;
+  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tn.group, 16));
+  const int64_t G0 = std::max<int64_t>(1, std::min<int64_t>(tn.group_first, G));
+  const int op0 = kd ? kd->nodes[0].op : 0;
+  if (tn.fuse_kbuild && lay->dtype == GPK_F64 && valid_kdesc(kd, lay->d) && kd->n_nodes == 1 && G0 < nblk &&
+      (op0 == GPK_OP_SE || op0 == GPK_OP_MAT32 || op0 == GPK_OP_MAT52)) {
+    int e = assemble_impl(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, nullptr, 0,
+                          nullptr, 0, y, y_bstride, W, false, nullptr, nullptr, stream, G0 * NB / ATILE);
+    if (e) return e;
+    GemmArgs kb;
+    memset(&kb, 0, sizeof(kb));
+    kb.d = (int32_t)lay->d;
+    kb.n = lay->n;
+    kb.node = kd->nodes[0];
+    kb.hyp = hyp_dev;
+    kb.hyp_stride = hyp_stride;
+    kb.noise = noise_dev;
+    kb.noise_stride = noise_stride;
+    kb.X = X;
+    kb.x_bs = x_bstride;
+    kb.y = y;
+    kb.y_bs = y_bstride;
+    e = potrf_impl(lay, W, Winv, info_dev, 0, nullptr, nullptr, stream, &kb);
+    if (e) return e;
+    return gpk_finalize(lay, W, info_dev, out_dev, nullptr, nullptr, stream);
+  }
   int e = gpk_assemble(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, nullptr,
                        0, nullptr, 0, y, y_bstride, W, stream);
   if (e) return e;
@@ -744,6 +793,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "diag_debug")) slot = &t.diag_dbg;
   else if (!strcmp(key, "group")) slot = &t.group;
   else if (!strcmp(key, "group_first")) slot = &t.group_first;
+  else if (!strcmp(key, "fuse_kbuild")) slot = &t.fuse_kbuild;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -20,310 +20,10 @@
 #include <string.h>
 
 #include "gpk_internal.h"
+#include "gpk_kernels.h"
 
 namespace gpk {
 namespace {
-
-constexpr double SQRT3 = 1.7320508075688772;
-constexpr double SQRT5 = 2.23606797749979;
-constexpr double PI = 3.141592653589793;
-
-// Values of one base node for R row points a[i] against one column point b.  The R evaluations
-// are independent, so the compiler interleaves their long f64 chains (exp / sin / sqrt / div).
-template <int R>
-__device__ __forceinline__ void base_values(const gpk_node& nd, const double* __restrict__ hyp,
-                                            const double* const (&a)[R], const double* b, int d, double (&r)[R]) {
-  const int fl = nd.flags;
-  const bool ard = (fl & GPK_NODE_ARD) != 0;
-  const double* h = hyp + nd.hyp_offset;
-  int sg_at;
-  if (nd.op == GPK_OP_SE) {
-    double s[R];
-    if (fl & GPK_NODE_SE_EXPANDED) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        double na = 0.0, nb = 0.0, ab = 0.0;
-        for (int k = 0; k < d; ++k) {
-          na += a[i][k] * a[i][k];
-          nb += b[k] * b[k];
-          ab += a[i][k] * b[k];
-        }
-        const double dist = sqrt((na - 2.0 * ab) + nb);  // NaN on a negative argument, as the reference
-        s[i] = dist * dist;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < R; ++i) s[i] = 0.0;
-      for (int k = 0; k < d; ++k) {
-        const double bk = b[k];
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          const double t = a[i][k] - bk;
-          s[i] += t * t;
-        }
-      }
-    }
-    const double l = ard ? 1.0 : h[0];
-    const double l2 = l * l;
-#pragma unroll
-    for (int i = 0; i < R; ++i) r[i] = exp(-0.5 * (s[i] / l2));
-    sg_at = ard ? d : 1;
-  } else if (nd.op == GPK_OP_PER) {
-    const double l = h[0], per = h[1];
-    double sn[R];
-    if (fl & GPK_NODE_STANDARD) {  // product of 1-D periodic kernels
-#pragma unroll
-      for (int i = 0; i < R; ++i) sn[i] = 0.0;
-      for (int k = 0; k < d; ++k) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          const double t = sin(PI * (fabs(a[i][k] - b[k]) / per));
-          sn[i] += t * t;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        double dist = 0.0;
-        for (int k = 0; k < d; ++k) dist += fabs(a[i][k] - b[k]);
-        const double t = sin(PI * (dist / per));
-        sn[i] = t * t;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < R; ++i) r[i] = exp((-2.0 * sn[i]) / (l * l));
-    sg_at = 2;
-  } else {  // MAT32 / MAT52
-    double dist[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) dist[i] = 0.0;
-    if (fl & GPK_NODE_STANDARD) {  // Euclidean distance
-      for (int k = 0; k < d; ++k) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-          const double t = a[i][k] - b[k];
-          dist[i] += t * t;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < R; ++i) dist[i] = sqrt(dist[i]);
-    } else {
-      for (int k = 0; k < d; ++k) {
-#pragma unroll
-        for (int i = 0; i < R; ++i) dist[i] += fabs(a[i][k] - b[k]);
-      }
-    }
-    const double l = ard ? 1.0 : fabs(h[0]);
-    if (nd.op == GPK_OP_MAT52) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const double frac = (SQRT5 * dist[i]) / l;
-        const double third = (5.0 * (dist[i] * dist[i])) / (3.0 * (l * l));
-        r[i] = ((1.0 + frac) + third) * exp(-frac);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const double frac = (SQRT3 * dist[i]) / l;
-        r[i] = (1.0 + frac) * exp(-frac);
-      }
-    }
-    sg_at = ard ? d : 1;
-  }
-  if (fl & GPK_NODE_SCALED) {
-    const double sg = h[sg_at];
-#pragma unroll
-    for (int i = 0; i < R; ++i) r[i] = sg * r[i];
-  }
-}
-
-__device__ __forceinline__ double base_value(const gpk_node& nd, const double* __restrict__ hyp,
-                                             const double* a, const double* b, int d) {
-  const double* aa[1] = {a};
-  double r[1];
-  base_values<1>(nd, hyp, aa, b, d, r);
-  return r[0];
-}
-
-// Register stack of the postfix program.  The stack pointer is wave-uniform, so the switch
-// lowers to scalar branches and nothing is indexed dynamically (no scratch).
-struct Stack {
-  double s0, s1, s2, s3, s4, s5, s6, s7;
-  __device__ __forceinline__ double get(int i) const {
-    switch (i) {
-      case 0: return s0; case 1: return s1; case 2: return s2; case 3: return s3;
-      case 4: return s4; case 5: return s5; case 6: return s6; default: return s7;
-    }
-  }
-  __device__ __forceinline__ void set(int i, double v) {
-    switch (i) {
-      case 0: s0 = v; break; case 1: s1 = v; break; case 2: s2 = v; break; case 3: s3 = v; break;
-      case 4: s4 = v; break; case 5: s5 = v; break; case 6: s6 = v; break; default: s7 = v; break;
-    }
-  }
-};
-
-__device__ __forceinline__ double eval_tree(const gpk_kdesc& kd, const double* hyp, const double* pa,
-                                            const double* pb, int slot_stride, int d) {
-  Stack st;
-  st.s0 = 0.0;
-  int sp = 0;
-  for (int q = 0; q < kd.n_nodes; ++q) {
-    const gpk_node nd = kd.nodes[q];
-    if (nd.op == GPK_OP_ADD || nd.op == GPK_OP_MUL) {
-      const double top = st.get(sp - 1);
-      const double below = st.get(sp - 2);
-      st.set(sp - 2, nd.op == GPK_OP_ADD ? below + top : below * top);
-      sp -= 1;
-    } else {
-      const int off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
-      st.set(sp, base_value(nd, hyp, pa + off, pb + off, d));
-      sp += 1;
-    }
-  }
-  return st.s0;
-}
-
-// eval_tree for R rows pa + i * row_step at once (one column point): a single base node is
-// evaluated directly; trees run the postfix program on R-wide stack entries.
-template <int R>
-__device__ __forceinline__ void eval_tree_rows(const gpk_kdesc& kd, const double* hyp, const double* pa,
-                                               int row_step, const double* pb, int slot_stride, int d,
-                                               double (&out)[R]) {
-  if (kd.n_nodes == 1) {
-    const gpk_node nd = kd.nodes[0];
-    const int off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
-    const double* aa[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) aa[i] = pa + off + i * row_step;
-    base_values<R>(nd, hyp, aa, pb + off, d, out);
-    return;
-  }
-  Stack st[R];
-#pragma unroll
-  for (int i = 0; i < R; ++i) st[i].s0 = 0.0;
-  int sp = 0;
-  for (int q = 0; q < kd.n_nodes; ++q) {
-    const gpk_node nd = kd.nodes[q];
-    if (nd.op == GPK_OP_ADD || nd.op == GPK_OP_MUL) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const double top = st[i].get(sp - 1);
-        const double below = st[i].get(sp - 2);
-        st[i].set(sp - 2, nd.op == GPK_OP_ADD ? below + top : below * top);
-      }
-      sp -= 1;
-    } else {
-      const int off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
-      const double* aa[R];
-#pragma unroll
-      for (int i = 0; i < R; ++i) aa[i] = pa + off + i * row_step;
-      double v[R];
-      base_values<R>(nd, hyp, aa, pb + off, d, v);
-#pragma unroll
-      for (int i = 0; i < R; ++i) st[i].set(sp, v[i]);
-      sp += 1;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < R; ++i) out[i] = st[i].s0;
-}
-
-// Single-base-node trees (the common case, e.g. every SURVEY config but C5): the node's constants
-// are computed once per thread into registers and every division by a hyperparameter becomes a
-// multiplication by its reciprocal (|error| <= ~1e-14 relative in K; the generic postfix path keeps
-// the reference's literal operation order).
-struct FastNode {
-  int op, flags, d, off;
-  double il, il2, i3l2, iper, sg;
-};
-
-__device__ __forceinline__ int fast_off(const gpk_kdesc& kd, int slot_stride) {
-  return (kd.nodes[0].flags & GPK_NODE_ARD) ? (kd.nodes[0].ard_slot + 1) * slot_stride : 0;
-}
-
-__device__ __forceinline__ FastNode make_fast_node(const gpk_node& nd, const double* hyp, int d) {
-  FastNode f;
-  f.op = nd.op;
-  f.flags = nd.flags;
-  f.d = d;
-  f.off = 0;
-  const double* h = hyp + nd.hyp_offset;
-  const bool ard = (nd.flags & GPK_NODE_ARD) != 0;
-  double l = 1.0;
-  int sg_at = 1;
-  if (nd.op == GPK_OP_PER) {
-    l = h[0];
-    f.iper = 1.0 / h[1];
-    sg_at = 2;
-  } else {
-    l = ard ? 1.0 : (nd.op == GPK_OP_SE ? h[0] : fabs(h[0]));
-    f.iper = 0.0;
-    sg_at = ard ? d : 1;
-  }
-  f.il = 1.0 / l;
-  f.il2 = 1.0 / (l * l);
-  f.i3l2 = 1.0 / (3.0 * (l * l));
-  f.sg = (nd.flags & GPK_NODE_SCALED) ? h[sg_at] : 1.0;
-  return f;
-}
-
-__device__ __forceinline__ double fast_value(const FastNode& f, const double* a, const double* b) {
-  const int d = f.d;
-  double r;
-  if (f.op == GPK_OP_SE) {
-    double s = 0.0;
-    if (f.flags & GPK_NODE_SE_EXPANDED) {
-      double na = 0.0, nb = 0.0, ab = 0.0;
-      for (int k = 0; k < d; ++k) {
-        na += a[k] * a[k];
-        nb += b[k] * b[k];
-        ab += a[k] * b[k];
-      }
-      const double dist = sqrt((na - 2.0 * ab) + nb);
-      s = dist * dist;
-    } else {
-      for (int k = 0; k < d; ++k) {
-        const double t = a[k] - b[k];
-        s += t * t;
-      }
-    }
-    r = exp(-0.5 * (s * f.il2));
-  } else if (f.op == GPK_OP_PER) {
-    double sn = 0.0;
-    if (f.flags & GPK_NODE_STANDARD) {
-      for (int k = 0; k < d; ++k) {
-        const double t = sin(PI * (fabs(a[k] - b[k]) * f.iper));
-        sn += t * t;
-      }
-    } else {
-      double dist = 0.0;
-      for (int k = 0; k < d; ++k) dist += fabs(a[k] - b[k]);
-      const double t = sin(PI * (dist * f.iper));
-      sn = t * t;
-    }
-    r = exp((-2.0 * sn) * f.il2);
-  } else {
-    double dist = 0.0;
-    if (f.flags & GPK_NODE_STANDARD) {
-      for (int k = 0; k < d; ++k) {
-        const double t = a[k] - b[k];
-        dist += t * t;
-      }
-      dist = sqrt(dist);
-    } else {
-      for (int k = 0; k < d; ++k) dist += fabs(a[k] - b[k]);
-    }
-    if (f.op == GPK_OP_MAT52) {
-      const double frac = (SQRT5 * dist) * f.il;
-      r = ((1.0 + frac) + (5.0 * (dist * dist)) * f.i3l2) * exp(-frac);
-    } else {
-      const double frac = (SQRT3 * dist) * f.il;
-      r = (1.0 + frac) * exp(-frac);
-    }
-  }
-  return f.sg * r;
-}
 
 enum { CLS_TRAIN = 0, CLS_PAD = 1, CLS_TEST = 2, CLS_Y = 3, CLS_ZERO = 4 };
 
@@ -382,13 +82,21 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
     tj = blockIdx.x - ti * ((a.m + ATILE - 1) / ATILE);
     if (a.uplo && tj > ti) return;
   } else {
-    // lower-triangular tile enumeration, row-major
+    // lower-triangular tile enumeration, row-major; with tcol_hi > 0 only the tile columns
+    // [0, tcol_hi): their triangle, then the full rows below it
     const int64_t t = blockIdx.x;
-    int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-    while (r * (r + 1) / 2 > t) --r;
-    while ((r + 1) * (r + 2) / 2 <= t) ++r;
-    ti = r;
-    tj = t - r * (r + 1) / 2;
+    const int64_t w = a.tcol_hi;
+    if (w > 0 && t >= w * (w + 1) / 2) {
+      const int64_t u = t - w * (w + 1) / 2;
+      ti = w + u / w;
+      tj = u % w;
+    } else {
+      int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+      while (r * (r + 1) / 2 > t) --r;
+      while ((r + 1) * (r + 2) / 2 <= t) ++r;
+      ti = r;
+      tj = t - r * (r + 1) / 2;
+    }
   }
   const int tid = threadIdx.x;
   const double* hyp_g = a.hyp + (int64_t)b * a.hyp_stride;
@@ -771,6 +479,9 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
   if (a.plain) {
     const int64_t tr = (a.n + ATILE - 1) / ATILE, tc = (a.m + ATILE - 1) / ATILE;
     grid = dim3((unsigned)(tr * tc), 1, 1);
+  } else if (a.tcol_hi > 0 && a.tcol_hi < a.ntile) {
+    const int64_t w = a.tcol_hi;
+    grid = dim3((unsigned)(w * (w + 1) / 2 + (a.ntile - w) * w), (unsigned)batch, 1);
   } else {
     grid = dim3((unsigned)(a.ntile * (a.ntile + 1) / 2), (unsigned)batch, 1);
   }

@@ -39,6 +39,7 @@ struct AsmArgs {
   int64_t ntile;     // augmented: 64-tiles per dimension
   double diag_add;   // plain mode
   int32_t eye;       // augmented: the m extra rows are the identity (E = I, m == n), zero corner
+  int64_t tcol_hi;   // augmented: > 0 builds only the tiles of 64-tile columns [0, tcol_hi) (all rows below)
   // ragged batches (NULL: every member uses n / m): member b uses its first nb[b] training points
   // (rows nb[b] .. n_pad-1 become identity rows) and its first mb[b] test points (zero rows after)
   const int64_t* nb;
@@ -64,6 +65,21 @@ struct GemmArgs {
   const int64_t* nb;
   const int64_t* mb;
   int64_t n_pad, y_row, p;
+  // fused K build (first trailing update of an m = 0, single-base-node factorisation): the tile's C is
+  // evaluated -- k(x_i, x_j) + noise [i == j], identity padding, y row -- instead of loaded; the K
+  // build then wrote only the panel columns of the first group
+  int32_t kbuild;
+  int32_t d;
+  int64_t n;
+  gpk_node node;
+  const double* hyp;
+  int64_t hyp_stride;
+  const double* noise;
+  int64_t noise_stride;
+  const double* X;
+  int64_t x_bs;
+  const double* y;
+  int64_t y_bs;
 };
 
 struct DiagArgs {

@@ -18,6 +18,7 @@
 #include <math.h>
 
 #include "gpk_internal.h"
+#include "gpk_kernels.h"
 
 namespace gpk {
 namespace {
@@ -125,8 +126,34 @@ __device__ __forceinline__ bool zero_rows(const GemmArgs& a, int b, int64_t r0, 
 // ends chunk kc.  K is permuted identically for both operands so that one ds_read_b128 yields
 // the operands of EPC consecutive MFMA k-steps: in k-step s, lane group q = lane >> 4 uses
 // logical piece q + 4 (s / EPC), element s % EPC.
-template <typename T, int MODE, int TM, int TN, int WN>
-__global__ __launch_bounds__(128 * WN, 2) void gemm_kernel(GemmArgs a) {
+// C value (i, j) of member b's augmented matrix for the fused K build (m = 0 layout): kernel value +
+// noise on the diagonal, identity padding, the y row (gpk_assemble.hip's classes for m = 0).  ls:
+// the ARD length scales (u = x / ls, the reference kernel with l = 1) or NULL.
+template <int OPK>
+__device__ __forceinline__ double kbuild_value(const FastNode& fn, const double* ls, const double* X,
+                                               const double* y, double noise, int64_t n, int64_t n_pad,
+                                               int64_t y_row, int64_t gi, int64_t gj) {
+  if (gi < n && gj < n) {
+    FastNode f = fn;
+    f.op = OPK;  // compile-time kernel: only its branch of fast_value_at is generated
+    const int d = fn.d;
+    const double* xi = X + gi * d;
+    const double* xj = X + gj * d;
+    double v;
+    if (ls) {
+      v = fast_value_at(f, [xi, ls](int k) { return xi[k] / ls[k]; }, [xj, ls](int k) { return xj[k] / ls[k]; });
+    } else {
+      v = fast_value_at(f, [xi](int k) { return xi[k]; }, [xj](int k) { return xj[k]; });
+    }
+    return gi == gj ? v + noise : v;
+  }
+  if (gi < n_pad && gj < n_pad) return gi == gj ? 1.0 : 0.0;
+  if (gi == y_row && gj < n) return y[gj];
+  return 0.0;
+}
+
+template <typename T, int MODE, int TM, int TN, int WN, int KB = 0>
+__global__ __launch_bounds__(128 * WN, WN == 4 ? 4 : 2) void gemm_kernel(GemmArgs a) {
   constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B piece
   constexpr int GBK = ROWB / (int)sizeof(T); // K depth per stage (16 f64, 32 f32)
   constexpr int KS = GBK / 4;                // MFMA k-steps per stage
@@ -205,7 +232,7 @@ __global__ __launch_bounds__(128 * WN, 2) void gemm_kernel(GemmArgs a) {
 #endif
   // C first (f64): the C read overlaps the first chunk's staging instead of following the last
   // MFMA, and the epilogue is stores only (+3 % update rate at N = 8192; neutral for f32)
-  constexpr bool CFIRST = (MODE == GEMM_UPDATE) && GPK_CFIRST && sizeof(T) == 8;
+  constexpr bool CFIRST = (MODE == GEMM_UPDATE) && ((GPK_CFIRST && sizeof(T) == 8) || KB != 0);
   const int col = lane & 15;
   // C tile through a buffer descriptor: one 32-bit per-lane offset (VGPR) plus, for block (m, n)
   // and register r, the wave-uniform byte offset ((m 16 + r RSTEP) ld + n 16) sizeof(T) in an
@@ -224,17 +251,60 @@ __global__ __launch_bounds__(128 * WN, 2) void gemm_kernel(GemmArgs a) {
 #define GPK_CSOFF(m, n, r) (((m) * 16 + (r) * RSTEP) * ldb_s + (n) * 16 * (int)sizeof(T))
 
   acc_t acc[MB][NBK];
+  if (KB != 0) {
+    // fused K build: evaluate this tile's C instead of loading it (the values gpk_assemble would
+    // have written; the tile's points are read straight from X, cached in L1 / L2)
+    const double* hyp = a.hyp + (int64_t)b * a.hyp_stride;
+    const double* Xb = a.X + (int64_t)b * a.x_bs;
+    const double* yb = a.y + (int64_t)b * a.y_bs;
+    const double noise = a.noise[(int64_t)b * a.noise_stride];
+    gpk_node nd;  // register copy (taking the kernel argument's address would put it on the stack)
+    nd.op = a.node.op;
+    nd.hyp_offset = a.node.hyp_offset;
+    nd.ard_slot = a.node.ard_slot;
+    nd.flags = a.node.flags;
+    const FastNode fn = make_fast_node(nd, hyp, a.d);
+    const double* ls = (nd.flags & GPK_NODE_ARD) ? hyp + nd.hyp_offset : nullptr;
+    const int64_t nn = a.n, npad = a.n_pad, yrow = a.y_row;
+    // the tile in two halves of TM / 2 rows through the (still unused) staging LDS: every thread
+    // evaluates (TM / 2) TN / (128 WN) values, then the waves of that half load their accumulators
+    double* cs = reinterpret_cast<double*>(smem);
+    constexpr int HALF = (TM / 2) * TN;
+    constexpr int NT = 128 * WN;
+    static_assert(HALF * (int)sizeof(double) <= 2 * STAGE, "half tile must fit the staging LDS");
+    const int64_t cj_tile = a.row0 + tj * TN;
 #pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int n = 0; n < NBK; ++n) {
-      if (CFIRST) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[m][n][r] = BufIO<T>::load(crs, cvo, GPK_CSOFF(m, n, r));
-      } else {
-        acc[m][n] = acc_t{0, 0, 0, 0};
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll 1
+      for (int e = tid; e < HALF; e += NT) {
+        const int rr = e / TN, cc = e - rr * TN;
+        cs[e] = kbuild_value<KB>(fn, ls, Xb, yb, noise, nn, npad, yrow, R + h * (TM / 2) + rr, cj_tile + cc);
       }
+      __syncthreads();
+      if (wr == h) {
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+#pragma unroll
+          for (int n = 0; n < NBK; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc[m][n][r] = (T)cs[(m * 16 + r * RSTEP + Mfma<T>::row(lane, 0)) * TN + wc * (TN / WN) + n * 16 + col];
+      }
+      __syncthreads();
     }
+  } else {
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int n = 0; n < NBK; ++n) {
+        if (CFIRST) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[m][n][r] = BufIO<T>::load(crs, cvo, GPK_CSOFF(m, n, r));
+        } else {
+          acc[m][n] = acc_t{0, 0, 0, 0};
+        }
+      }
+  }
 
   const int q = lane >> 4, lr = lane & 15;
   const int aoff = (wr * (TM / WM) + lr) * ROWB;
@@ -430,7 +500,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const double* __restrict__ A,
   if (lane == 0) y[row] = alpha * sum + (beta == 0.0 ? 0.0 : beta * y[row]);
 }
 
-template <typename T, int MODE, int TM, int TN, int WN = 2>
+template <typename T, int MODE, int TM, int TN, int WN = 2, int KB = 0>
 hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
   // a.nt / c_lo / c_hi are in units of this launch's tile sizes
   unsigned nblk;
@@ -441,13 +511,29 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
     nblk = (unsigned)a.nt;
   }
   if (nblk == 0) return hipSuccess;
-  hipLaunchKernelGGL((gemm_kernel<T, MODE, TM, TN, WN>), dim3(nblk, batch), dim3(128 * WN), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<T, MODE, TM, TN, WN, KB>), dim3(nblk, batch), dim3(128 * WN), 0, s, a);
   return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s) {
+  if (a.kbuild) {  // first trailing update with the fused K build (SE / MAT32 / MAT52 nodes)
+    if (mode != GEMM_UPDATE || dtype != GPK_F64) return hipErrorInvalidValue;
+    switch (a.node.op) {
+      case GPK_OP_SE:
+        return tile == 128 ? launch_gemm_t<double, GEMM_UPDATE, 128, 128, GPK_UPD_WN, GPK_OP_SE>(a, batch, s)
+                           : launch_gemm_t<double, GEMM_UPDATE, 64, 64, 2, GPK_OP_SE>(a, batch, s);
+      case GPK_OP_MAT32:
+        return tile == 128 ? launch_gemm_t<double, GEMM_UPDATE, 128, 128, GPK_UPD_WN, GPK_OP_MAT32>(a, batch, s)
+                           : launch_gemm_t<double, GEMM_UPDATE, 64, 64, 2, GPK_OP_MAT32>(a, batch, s);
+      case GPK_OP_MAT52:
+        return tile == 128 ? launch_gemm_t<double, GEMM_UPDATE, 128, 128, GPK_UPD_WN, GPK_OP_MAT52>(a, batch, s)
+                           : launch_gemm_t<double, GEMM_UPDATE, 64, 64, 2, GPK_OP_MAT52>(a, batch, s);
+      default:
+        return hipErrorInvalidValue;
+    }
+  }
   if (dtype == GPK_F64) {
     if (mode == GEMM_UPDATE)
       return tile == 128 ? launch_gemm_t<double, GEMM_UPDATE, 128, 128, GPK_UPD_WN>(a, batch, s)

@@ -195,6 +195,15 @@ class AugmentedFactorization:
                 raise ValueError("m = %d extra rows need X_test or E" % m)
         s = nat.stream_handle(self.W.device)
         L = self.L
+        if m == 0:
+            # gpk_nlml: K build (fused into the first trailing update for single-node kernels) +
+            # factorisation + read-out; zeroes info itself
+            nat.check(L.gpk_nlml(ctypes.byref(kd), ctypes.byref(lay), nat.ptr(hyp), hyp_stride, nat.ptr(noise),
+                                 noise_stride, nat.ptr(X), x_bstride, nat.ptr(y), y_bstride, nat.ptr(self.W),
+                                 nat.ptr(self.Winv), nat.ptr(self.info), nat.ptr(self.out), s), "gpk_nlml")
+            self.kd = kd
+            self.done = True
+            return self
         self.info.zero_()
         nat.check(L.gpk_assemble(ctypes.byref(kd), ctypes.byref(lay), nat.ptr(hyp), hyp_stride,
                                  nat.ptr(noise), noise_stride, nat.ptr(X), x_bstride,

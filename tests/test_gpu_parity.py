@@ -351,6 +351,41 @@ def test_pipelined_sweep_chunks_match_single_evaluations(pipeline):
         assert best == int(np.argmin(exp)) and int(info.abs().max()) == 0
 
 
+@pytest.mark.parametrize("tree,hyp,d", [(SE, [0.1], 1), (("MAT52", {"ard": True, "standard": True}),
+                                                        [[0.25, 0.5, 0.75, 1.0]], 4),
+                                          (("MAT32", {}), [0.3], 1), (("PER", {}), [0.7, 0.45], 1)])
+def test_fused_kbuild_is_bitwise_the_unfused_path(tree, hyp, d):
+    """The K build fused into the first trailing update (gpk_nlml, single-node kernels) evaluates the
+    same values as gpk_assemble: every factor element and the -LML are bitwise equal."""
+    from gaussianprocessfundamentals_amd import _native as nat
+    rng = np.random.default_rng(11)
+    n = 1500   # 12 panels: a first group of 8 and a trailing update
+    x = rng.uniform(0, 1, (n, d))
+    y = np.sin(3 * x[:, 0])
+    X = torch.as_tensor(x, device="cuda").contiguous()
+    Y = torch.as_tensor(y, device="cuda").reshape(1, -1).contiguous()
+    k = make_kernel(tree, d)
+    kd = engine.kernel_descriptor(k, d)
+    H = engine.pack_hyper_parameter(hyp_list(hyp), kd.n_hyp).reshape(1, -1).repeat(2, 1).contiguous()
+    H[1, 0] *= 1.1
+    NZ = torch.tensor([1e-1], dtype=torch.float64, device="cuda")
+    res = []
+    for fuse in (0, 1):
+        old = nat.tune("fuse_kbuild", fuse)
+        try:
+            f = engine.AugmentedFactorization(n, d, 0, 2, torch.float64)
+            f.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
+            res.append((f.nlml().clone(), torch.tril(f.w(0)[:n, :n]).clone(), torch.tril(f.w(1)[:n, :n]).clone(),
+                        f.z(1).clone(), int(f.info.abs().max())))
+        finally:
+            nat.tune("fuse_kbuild", old)
+    a, b = res
+    assert a[4] == 0 and b[4] == 0
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+    exp = o.nlml(tree, hyp, 1e-1, x, y)
+    assert rel(float(b[0][0]), exp) < 1e-9
+
+
 # ------------------------------------------------------------------------------ schedules
 @pytest.mark.parametrize("group,group_first", [(1, 1), (2, 2), (3, 1), (4, 4), (5, 2), (8, 2), (8, 3), (8, 8)])
 @pytest.mark.parametrize("lookahead", [0, 1])
