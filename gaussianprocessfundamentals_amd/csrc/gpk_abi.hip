@@ -140,6 +140,7 @@ struct Tune {
   int64_t group;          // panels per trailing update (K = 128 group)
   int64_t group_first;    // panels of the first group (a short first chain lets the bulk start early)
   int64_t fuse_kbuild;    // gpk_nlml: K build fused into the first trailing update (single-node kernels)
+  int64_t upd_band;       // trailing-update tile order: 0 row-major, B > 0 bands of B tile rows
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -151,7 +152,8 @@ Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
-                         env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1)};
+                         env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
+                         env_i64("GPK_UPD_BAND", 0)};
   return t;
 }
 
@@ -462,6 +464,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
     ga.nt = (int32_t)(rows / tile);
     ga.c_lo = (int32_t)(c_lo * scale);
     ga.c_hi = (int32_t)(c_hi * scale);
+    ga.band = (int32_t)std::max<int64_t>(0, tn.upd_band);
     if (eye) {  // identity rows t >= j0 + kdepth are zero in the panel columns
       ga.zlo = lay->n_pad + j0 + kdepth;
       ga.zhi = lay->y_row;
@@ -794,6 +797,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "group")) slot = &t.group;
   else if (!strcmp(key, "group_first")) slot = &t.group_first;
   else if (!strcmp(key, "fuse_kbuild")) slot = &t.fuse_kbuild;
+  else if (!strcmp(key, "upd_band")) slot = &t.upd_band;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -68,6 +68,7 @@ struct GemmArgs {
   // fused K build (first trailing update of an m = 0, single-base-node factorisation): the tile's C is
   // evaluated -- k(x_i, x_j) + noise [i == j], identity padding, y row -- instead of loaded; the K
   // build then wrote only the panel columns of the first group
+  int32_t band;    // update tile order: 0 row-major lower triangle, B > 0 bands of B tile rows
   int32_t kbuild;
   int32_t d;
   int64_t n;

@@ -169,12 +169,42 @@ __global__ __launch_bounds__(128 * WN, WN == 4 ? 4 : 2) void gemm_kernel(GemmArg
   const int b = blockIdx.y;
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   int64_t ti, tj;  // tile coordinates in units of TM (rows) and TN (cols)
-  // tiles in row-major lower-triangle order (a banded, column-major order for L2 reuse of the
-  // panel slabs raised the L2 hit rate but not the update rate: measured 0.99x)
+  // tiles in row-major lower-triangle order, or banded (a.band > 0, gpk_tune("upd_band"))
   if (MODE == GEMM_UPDATE) {
     const int64_t w = a.c_hi - a.c_lo;
     const int64_t ttri = w * (w + 1) / 2;
-    if (t < ttri) {
+    const int64_t B = a.band;
+    if (t < ttri && B > 0) {
+      // banded order: bands of B tile rows, each walked column by column, so that the tiles one XCD
+      // runs at a time (consecutive ids, see xcd_remap) form ~B x B blocks sharing B A- and B
+      // B-panels in its L2 (row-major: 1 A- and 64 B-panels)
+      int64_t q = 0, start = 0;
+      for (;;) {
+        const int64_t h = (q * B + B <= w) ? B : w - q * B;
+        const int64_t cnt = q * B * h + h * (h + 1) / 2;
+        if (t < start + cnt) break;
+        start += cnt;
+        ++q;
+      }
+      const int64_t h = (q * B + B <= w) ? B : w - q * B;
+      int64_t u = t - start;
+      int64_t r, c;
+      if (u < q * B * h) {
+        c = u / h;
+        r = q * B + u % h;
+      } else {
+        u -= q * B * h;
+        int64_t j = 0;
+        while (u >= h - j) {
+          u -= h - j;
+          ++j;
+        }
+        c = q * B + j;
+        r = q * B + j + u;
+      }
+      ti = a.c_lo + r;
+      tj = a.c_lo + c;
+    } else if (t < ttri) {
       int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
       while (r * (r + 1) / 2 > t) --r;
       while ((r + 1) * (r + 2) / 2 <= t) ++r;
