@@ -141,6 +141,7 @@ struct Tune {
   int64_t group_first;    // panels of the first group (a short first chain lets the bulk start early)
   int64_t fuse_kbuild;    // gpk_nlml: K build fused into the first trailing update (single-node kernels)
   int64_t upd_band;       // trailing-update tile order: 0 row-major, B > 0 bands of B tile rows
+  int64_t skip_zero_rows; // skip the MFMAs of the all-zero 16-row blocks below the y row
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -153,7 +154,7 @@ Tune& tune() {
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
-                         env_i64("GPK_UPD_BAND", 0)};
+                         env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1)};
   return t;
 }
 
@@ -410,6 +411,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   base.n_pad = lay->n_pad;
   base.y_row = lay->y_row;
   base.p = lay->p;
+  base.row_end = tn.skip_zero_rows ? lay->y_row + 1 : 0;  // rows below the y row are zero
   // panel solve of block k: every row below the block (the y / test rows included)
   auto trsm = [&](int64_t k) -> hipError_t {
     GemmArgs ga = base;
@@ -798,6 +800,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "group_first")) slot = &t.group_first;
   else if (!strcmp(key, "fuse_kbuild")) slot = &t.fuse_kbuild;
   else if (!strcmp(key, "upd_band")) slot = &t.upd_band;
+  else if (!strcmp(key, "skip_zero_rows")) slot = &t.skip_zero_rows;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

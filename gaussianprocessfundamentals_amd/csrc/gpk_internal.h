@@ -69,6 +69,7 @@ struct GemmArgs {
   // evaluated -- k(x_i, x_j) + noise [i == j], identity padding, y row -- instead of loaded; the K
   // build then wrote only the panel columns of the first group
   int32_t band;    // update tile order: 0 row-major lower triangle, B > 0 bands of B tile rows
+  int64_t row_end; // rows >= row_end are zero in every panel (0: unknown); MFMAs on them are skipped
   int32_t kbuild;
   int32_t d;
   int64_t n;

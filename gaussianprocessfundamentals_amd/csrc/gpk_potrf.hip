@@ -347,6 +347,16 @@ __global__ __launch_bounds__(128 * WN, WN == 4 ? 4 : 2) void gemm_kernel(GemmArg
   const int NK0 = (MODE == GEMM_TRSM) ? NB / GBK : a.kdepth / GBK;
   const int NK = (GPK_ABLATE == 3 && MODE == GEMM_UPDATE) ? 2 * NK0 : NK0;
   GPK_GLDS(0, 0);
+#ifndef GPK_SETPRIO
+#define GPK_SETPRIO 0  // 1: static priority 1 for the second-dispatched half of the waves (MI355X guide)
+#endif
+  if (GPK_SETPRIO && MODE == GEMM_UPDATE && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  // 16-row blocks of this wave that hold a nonzero row: rows >= row_end (below the y row) are zero in
+  // every panel, so in the tiles of the y row's block most MFMAs would multiply zeros; those tiles
+  // take the guarded form of the chunk (wave-uniform, the other tiles are unaffected)
+  const int64_t wrow0 = R + wr * (TM / WM);
+  const int mact = a.row_end <= 0 ? MB
+                 : (int)(a.row_end <= wrow0 ? 0 : ((a.row_end - wrow0 + 15) / 16 < MB ? (a.row_end - wrow0 + 15) / 16 : MB));
   for (int kc = 0; kc < NK; ++kc) {
     const int st = kc & 1;
     // one barrier per chunk, at the top: it retires the chunk kc glds (vmcnt(0), issued a whole
@@ -382,17 +392,21 @@ __global__ __launch_bounds__(128 * WN, WN == 4 ? 4 : 2) void gemm_kernel(GemmArg
         }
     }
 
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int n = 0; n < NBK; ++n) {
-        // TRSM against the lower-triangular inverse: K chunk kc feeds output columns >= kc GBK only
-        if (MODE == GEMM_TRSM && kc * GBK > wc * (TN / WN) + n * 16 + 15) continue;
-#pragma unroll
-        for (int m = 0; m < MB; ++m)
-          acc[m][n] = CFIRST ? Mfma<T>::op_neg(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n])
-                             : Mfma<T>::op(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]);
-      }
+#define GPK_MFMA_CHUNK(MLIM)                                                                           \
+  _Pragma("unroll") for (int s = 0; s < KS; ++s)                                                       \
+  _Pragma("unroll") for (int n = 0; n < NBK; ++n) {                                                    \
+    /* TRSM against the lower-triangular inverse: K chunk kc feeds output columns >= kc GBK only */    \
+    if (MODE == GEMM_TRSM && kc * GBK > wc * (TN / WN) + n * 16 + 15) continue;                        \
+    _Pragma("unroll") for (int m = 0; m < (MLIM); ++m)                                                 \
+      acc[m][n] = CFIRST ? Mfma<T>::op_neg(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]) \
+                         : Mfma<T>::op(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]);   \
+  }
+    if (mact > 1) {
+      GPK_MFMA_CHUNK(MB)
+    } else if (mact == 1) {
+      GPK_MFMA_CHUNK(1)
+    }
+#undef GPK_MFMA_CHUNK
   }
 #undef GPK_GLDS
 

@@ -242,8 +242,9 @@ int gpk_timing_reset(void);
  * none).  Keys: "lookahead" (1: panel chain on a high-priority stream overlapping the bulk
  * trailing update, 0: one stream), "reserve_cus" (CUs masked off the bulk-update stream; read
  * when that stream is first created), "group" (panels per trailing update, K = 128 group), "group_first"
- * (panels of the first group),
- * "upd_t128_min", "trsm_t128_min" (128-tile thresholds).
+ * (panels of the first group), "fuse_kbuild" (K build inside the first trailing update),
+ * "upd_band" (trailing-update tile order), "skip_zero_rows" (skip the MFMAs of the zero rows below
+ * the y row), "upd_t128_min", "trsm_t128_min" (128-tile thresholds).
  * Stores the value and returns the previous one through *old (may be NULL); 0 or -1 (unknown
  * key).  Defaults come from the environment (GPK_LOOKAHEAD, GPK_RESERVE_CUS, ...). */
 int gpk_tune(const char* key, int64_t value, int64_t* old);
