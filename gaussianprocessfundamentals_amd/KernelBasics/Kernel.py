@@ -130,7 +130,7 @@ class Kernel(bgpc.Component):
             for h in self.last_hyper_parameter:
                 v = torch.as_tensor(h).detach().reshape(-1).tolist()
                 flat.extend(float(x) for x in v)
-        noise = None if self.noise is None else float(torch.as_tensor(self.noise))
+        noise = None if self.noise is None else float(torch.as_tensor(self.noise, dtype=torch.float64))
         return self.manifestation.value, noise, tuple(flat)
 
     def __hash__(self):

@@ -15,12 +15,16 @@ def get_metric_by_type(metric_type: MetricType, _gp,
                        numerical_matrix_handling: mht.NumericalMatrixHandlingType =
                        mht.NumericalMatrixHandlingType.CHOLESKY_BASED,
                        subset_size: int = None):
-    """Metric object for ``metric_type`` over ``_gp`` (default CHOLESKY_BASED, Auxiliary.py:16).
-    SKC_UPPER_BOUND (the Nystroem upper bound, Metrics/SkcLogLikelihood.py) is SURVEY §8f.4."""
+    """Metric object for ``metric_type`` over ``_gp`` (default CHOLESKY_BASED, Auxiliary.py:16);
+    SKC_UPPER_BOUND gives the Nystroem upper bound of Metrics/SkcLogLikelihood.py."""
     from ..Statistics import GaussianProcess as gp
     if metric_type is MetricType.LL:
-        if local_approx is mht.MatrixApproximations.SKC_UPPER_BOUND:
-            raise NotImplementedError("SKC upper bound is SURVEY §8f.4 (Nystroem approximations)")
+        if local_approx is mht.MatrixApproximations.SKC_UPPER_BOUND:                          # :19-22
+            from ..Statistics.Nystroem_K import NystroemMatrix
+            from .SkcLogLikelihood import LogLikelihoodUpperBound
+            nyk = NystroemMatrix(_gp.covariance_matrix)
+            nyk.set_data_input(_gp.data_input)
+            return LogLikelihoodUpperBound(_gp.data_input, _gp.covariance_matrix, nystroem_k=nyk)
         return LogLikelihood(_gp.data_input, _gp.covariance_matrix, local_approx, numerical_matrix_handling,
                              subset_size)
     if metric_type is MetricType.BIC:

@@ -44,11 +44,14 @@ class LogLikelihood(AbstractLogLikelihood):
         if reset:
             self.covariance_matrix.reset()
             self.last_covariance_matrix = None
+        approx = self.local_approx in _MATRIX_APPROX
+        if approx and _wants_grad(hyper_parameter, noise):
+            raise NotImplementedError("gradients through the %s approximation are not provided" % self.local_approx)
         if _wants_grad(hyper_parameter, noise):
             # differentiable form: what the reference's tf.GradientTape sees through get_metric
             # (Optimizer/Fitter.py:104-158); backward() uses the analytic device gradient
             return _NegLogLikelihood.apply(self, _as_tensor(noise), *[_as_tensor(h) for h in hyper_parameter])
-        if self.numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
+        if approx or self.numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
             return self._get_metric_by_strategy(hyper_parameter, noise, indices)
         f = self.covariance_matrix.factorization(hyper_parameter, noise)
         if self.data_input.data_x_train.dim() == 3:
@@ -69,6 +72,11 @@ class LogLikelihood(AbstractLogLikelihood):
         logdet = self.get_log_determinant(hyper_parameter, noise, indices)
         n = float(self.data_input.n_train)
         ll = (-0.5 * fit + -0.5 * logdet) + (-0.5 * (n * LOG_2PI))
+        if self.local_approx is mht.MatrixApproximations.SKC_LOWER_BOUND:
+            # Titsias' correction trace(K_hat + noise I - K) / (2 p_cov_matrix_jitter) (:51-60)
+            diff = torch.diagonal(self.get_covariance_matrix(hyper_parameter, noise, indices)) - \
+                torch.diagonal(self.covariance_matrix.get_K(hyper_parameter))
+            ll = ll - (1.0 / (2.0 * float(global_param.p_cov_matrix_jitter))) * torch.sum(diff)
         return -ll.reshape(1, 1)
 
     def get_metric_and_gradient(self, hyper_parameter: List, noise, reset: bool = True):
@@ -94,6 +102,10 @@ class LogLikelihood(AbstractLogLikelihood):
         out = self.get_metric(hyper_parameter, noise, reset=reset)
         self.covariance_matrix.factorization(hyper_parameter, noise).check_info()
         return out
+
+
+_MATRIX_APPROX = (mht.MatrixApproximations.BASIC_NYSTROEM, mht.MatrixApproximations.SKC_LOWER_BOUND,
+                  mht.MatrixApproximations.SKI)
 
 
 def _as_tensor(h) -> torch.Tensor:
@@ -154,10 +166,6 @@ class BlockwiseLogLikelihood(AbstractMetric):
     training points contribute 0 (an empty Cholesky).  Returns a [1, 1] tensor like LogLikelihood."""
 
     def __init__(self, _gp, local_approx, numerical_matrix_handling, subset_size: int = None):
-        if local_approx is not mht.MatrixApproximations.NONE:
-            raise NotImplementedError("approximation %s is SURVEY §8f.4; the device engine is exact" % local_approx)
-        if numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
-            raise NotImplementedError("numerical handling %s is SURVEY §8f.4" % numerical_matrix_handling)
         self.local_approx = local_approx
         self.numerical_matrix_handling = numerical_matrix_handling
         self.subset_size = subset_size
@@ -177,6 +185,9 @@ class BlockwiseLogLikelihood(AbstractMetric):
         return factor_segments(kernels, slices, dis, noise)
 
     def get_metric(self, hyper_parameter: List, noise, indices=None, reset: bool = True) -> torch.Tensor:
+        if (self.local_approx is not mht.MatrixApproximations.NONE or
+                self.numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED):
+            return self._per_segment(hyper_parameter, noise, indices)
         f, _ = self.segment_factorization(hyper_parameter, noise)
         for sub in self._gp.constituent_gps:
             sub.covariance_matrix.reset()
@@ -184,6 +195,25 @@ class BlockwiseLogLikelihood(AbstractMetric):
         if f is None:
             return torch.zeros((1, 1), dtype=torch.float64, device=_device())
         return torch.sum(f.nlml()).reshape(1, 1)
+
+
+    def _per_segment(self, hyper_parameter: List, noise, indices=None) -> torch.Tensor:
+        """One LogLikelihood per segment with the requested approximation / handling, as the
+        reference does for every strategy (LogLikelihood.py:86-104); segments without training
+        points contribute 0."""
+        index = blockwise_hyper_parameter_offset(self._gp)
+        total = torch.zeros((1, 1), dtype=torch.float64, device=_device())
+        for sub in self._gp.constituent_gps:
+            kern = sub.covariance_matrix.kernel
+            nh = kern.get_number_of_hyper_parameter()
+            if int(sub.data_input.n_train) > 0:
+                sub_ll = LogLikelihood(sub.data_input, sub.covariance_matrix, self.local_approx,
+                                       self.numerical_matrix_handling, self.subset_size)
+                total = total + sub_ll.get_metric(list(hyper_parameter[index:index + nh]), noise, indices).reshape(1, 1)
+            index += nh
+            sub.covariance_matrix.reset()
+            sub.aux.reset()
+        return total
 
 
 def _device():

@@ -1,7 +1,7 @@
 """Strategy enums of gpbasics/Metrics/MatrixHandlingTypes.py (same names and values).
 
-Only MatrixApproximations.NONE with NumericalMatrixHandlingType.CHOLESKY_BASED runs on the
-device; every other strategy is SURVEY §8f "next" and is rejected by ``Metric``.
+Every strategy runs on the device (Metrics/Metrics.py documents the binding); the fast path is
+MatrixApproximations.NONE with NumericalMatrixHandlingType.CHOLESKY_BASED.
 """
 from enum import Enum
 

@@ -14,7 +14,17 @@ The reference binds ``get_alpha`` / ``get_log_determinant`` per numerical handli
 slogdet(K)[1] is log|det K| = 2 sum log diag L for a positive-definite K (the device Cholesky);
 for any other K it raises NotImplementedError (the reference's LU-based slogdet is not provided).
 Subset-of-data approximations (SOD_GRID, SOD_RANDOM) evaluate the exact path on the subset
-(:60-68); the Nystroem / SKC / SKI approximations are not provided and raise.
+(:60-68).  Matrix approximations (:77-126) swap get_covariance_matrix / get_log_determinant:
+
+  BASIC_NYSTROEM, SKC_LOWER_BOUND  covariance K_hat + noise I, log-det of the Nystroem determinant
+                                   (Statistics/Nystroem_K.py); CHOLESKY_BASED keeps the exact alpha
+                                   because get_alpha_cholesky reads the holistic covariance matrix
+  SKC_UPPER_BOUND                  exact covariance, Nystroem log-det (Metrics/SkcLogLikelihood.py)
+  SKI                              covariance W K_mm W^T + noise I (Metrics/StructuredKernelInterpolation.py);
+                                   with CHOLESKY_BASED nothing reads it, so the metric is the exact one
+
+The STRICT / PSEUDO inverse and slogdet of an approximate covariance matrix factor it through the
+augmented Cholesky (engine.DenseFactorization); linear CG multiplies it with gpk_gemv.
 """
 from __future__ import annotations
 
@@ -62,14 +72,18 @@ class Metric(AbstractMetric):
         if isinstance(self.local_approx, mht.SubsetOfDataApproaches):                      # :60-66
             self.data_input = data_input.get_subset(subset_size=self.subset_size,
                                                     subset_of_data_approach=self.local_approx)
-        elif self.local_approx is not mht.MatrixApproximations.NONE:
-            raise NotImplementedError("approximation %s (Nystroem / SKC / SKI) is not provided by the device engine "
-                                      "(SURVEY §8f.4); use NONE or a subset-of-data approach" % self.local_approx)
         else:
             self.data_input = data_input
+        A = mht.MatrixApproximations
+        if self.local_approx is not A.NONE:                                                # :70-72
+            self.data_input.n_inducting_train = self.subset_size
+            self.data_input.n_inducting_test = self.data_input.n_test / self.data_input.n_train * self.subset_size
         self.covariance_matrix.set_data_input(self.data_input)
         self.type = metric_type
+        if self.local_approx in (A.SKC_LOWER_BOUND, A.BASIC_NYSTROEM, A.SKC_UPPER_BOUND):   # :77-80
+            self.nystroem_matrix = self.get_nystroem_handler()
         self.last_covariance_matrix = None
+        self._approx_fact = None
         h = mht.NumericalMatrixHandlingType
         if numerical_matrix_handling is h.PSEUDO_INVERSE:                                  # :82-94
             self.get_alpha, self.get_log_determinant = self.get_alpha_pseudo_inverse, self.get_log_determinant_slodget
@@ -79,8 +93,59 @@ class Metric(AbstractMetric):
             self.get_alpha, self.get_log_determinant = self.get_alpha_lcg, self.get_log_determinant_slodget
         else:
             self.get_alpha, self.get_log_determinant = self.get_alpha_strict_inverse, self.get_log_determinant_slodget
+        if self.local_approx is A.SKC_UPPER_BOUND:                                         # :95-106
+            self.get_covariance_matrix = self.get_default_covariance_matrix
+            self.get_log_determinant = self.get_log_determinant_nystroem
+        elif self.local_approx in (A.SKC_LOWER_BOUND, A.BASIC_NYSTROEM):
+            self.get_covariance_matrix = self.get_nystroem_matrix
+            self.get_log_determinant = self.get_log_determinant_nystroem
+        elif self.local_approx is A.SKI:
+            self.get_covariance_matrix = self.get_ski_matrix
+        else:
+            self.get_covariance_matrix = self.get_default_covariance_matrix
 
-    def get_covariance_matrix(self, hyper_parameter: List, noise, indices=None):
+    def get_nystroem_handler(self):
+        from ..Statistics.Nystroem_K import NystroemMatrix
+        nyk = NystroemMatrix(self.covariance_matrix)
+        nyk.set_data_input(self.data_input)
+        return nyk
+
+    def _approximate(self) -> bool:
+        """True when get_covariance_matrix is an approximation (not the holistic K + noise I)."""
+        return self.get_covariance_matrix.__func__ is not Metric.get_default_covariance_matrix
+
+    def get_nystroem_matrix(self, hyper_parameter: List, noise, indices=None):
+        """K_hat + noise I (Metrics.py:116-119)."""
+        if self.last_covariance_matrix is None:
+            self._require_plain()
+            self.last_covariance_matrix = self.nystroem_matrix.get_K_approx_noised(hyper_parameter, noise, indices)
+            self._approx_fact = None
+        return self.last_covariance_matrix
+
+    def get_ski_matrix(self, hyper_parameter: List, noise, indices=None):
+        """W K_mm W^T + noise I (Metrics.py:121-125)."""
+        if self.last_covariance_matrix is None:
+            from .StructuredKernelInterpolation import get_ski_matrix
+            self._require_plain()
+            self.last_covariance_matrix = get_ski_matrix(hyper_parameter, self.data_input,
+                                                         self.covariance_matrix.kernel, noise)
+            self._approx_fact = None
+        return self.last_covariance_matrix
+
+    def get_log_determinant_nystroem(self, hyper_parameter: List, noise, indices=None):
+        """get_K_approx_det (Metrics.py:149-150): cached by the Nystroem handler (quirk kept)."""
+        return self.nystroem_matrix.get_K_approx_det(hyper_parameter, noise, indices)
+
+    def _approx_factorization(self, hyper_parameter: List, noise, indices=None):
+        """Identity-augmented dense factorisation of the approximate covariance matrix (its inverse,
+        log-determinant and info), cached until the matrix is rebuilt."""
+        from .. import engine
+        A = self.get_covariance_matrix(hyper_parameter, noise, indices).contiguous()
+        if self._approx_fact is None:
+            self._approx_fact = engine.DenseFactorization(A.shape[0], inverse=True).run(A, 0.0)
+        return self._approx_fact
+
+    def get_default_covariance_matrix(self, hyper_parameter: List, noise, indices=None):
         if self.last_covariance_matrix is None:
             self.last_covariance_matrix = self.covariance_matrix.get_K_noised(hyper_parameter, noise)
         return self.last_covariance_matrix
@@ -101,13 +166,18 @@ class Metric(AbstractMetric):
         """inv(K) y (Metrics.py:132-133): the explicit inverse, then one device GEMV."""
         from .. import engine
         self._require_plain()
+        if self._approximate():
+            f = self._approx_factorization(hyper_parameter, noise, indices)
+            f.check_info()
+            return engine.gemv(f.k_inv(0).contiguous(), self._y(y))
         return engine.gemv(self.covariance_matrix.get_K_inv(hyper_parameter, noise).contiguous(), self._y(y))
 
     def get_alpha_pseudo_inverse(self, hyper_parameter: List, noise, y=None, indices=None):
         """pinv(K) y (Metrics.py:135-136) = inv(K) y for a positive-definite K (raises otherwise)."""
         from .. import engine
         self._require_plain()
-        f = self.covariance_matrix.factorization(hyper_parameter, noise)
+        f = (self._approx_factorization(hyper_parameter, noise, indices) if self._approximate()
+             else self.covariance_matrix.factorization(hyper_parameter, noise))
         if int(f.info.abs().max()) != 0:
             raise NotImplementedError("pinv of a matrix that is not positive definite is not provided")
         return self.get_alpha_strict_inverse(hyper_parameter, noise, y, indices)
@@ -130,7 +200,8 @@ class Metric(AbstractMetric):
         """slogdet(K)[1] = log|det K| (Metrics.py:146-147), from the device Cholesky for a
         positive-definite K; other K raise NotImplementedError."""
         self._require_plain()
-        f = self.covariance_matrix.factorization(hyper_parameter, noise)
+        f = (self._approx_factorization(hyper_parameter, noise, indices) if self._approximate()
+             else self.covariance_matrix.factorization(hyper_parameter, noise))
         if int(f.info.abs().max()) != 0:
             raise NotImplementedError("slogdet of a matrix that is not positive definite is not provided")
         return torch.sum(f.logdet())

@@ -33,6 +33,12 @@ def _is_scalar(noise) -> bool:
     return noise is not None and torch.as_tensor(noise).shape == torch.Size([])
 
 
+def _noise_float(noise) -> float:
+    """The noise as a Python float without a float32 detour (torch.as_tensor(0.01) is float32)."""
+    t = noise if isinstance(noise, torch.Tensor) else torch.as_tensor(noise, dtype=torch.float64)
+    return float(t)
+
+
 def noise_vector(noise) -> torch.Tensor:
     """Rank-0 noise as a 1-element fp64 device vector (no host round trip for device tensors)."""
     t = noise if isinstance(noise, torch.Tensor) else torch.tensor(float(noise), dtype=torch.float64)
@@ -135,7 +141,7 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
         if _is_scalar(noise) and self.data_input is not None:
             if self.noised_K is None:
                 x = self.data_input.data_x_train
-                nv = float(torch.as_tensor(noise))
+                nv = _noise_float(noise)
                 if x.dim() == 3:
                     self.noised_K = torch.stack([engine.kernel_matrix(self.kernel, hyper_parameter, xb, xb, nv) for xb in x])
                 else:
@@ -230,7 +236,7 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
         if _is_scalar(noise) and self.data_input is not None:
             if self.noised_K_ss is None:
                 xt = self.data_input.data_x_test
-                self.noised_K_ss = engine.kernel_matrix(self.kernel, hyper_parameter, xt, xt, float(torch.as_tensor(noise)))
+                self.noised_K_ss = engine.kernel_matrix(self.kernel, hyper_parameter, xt, xt, _noise_float(noise))
             return self.noised_K_ss
         raise Exception("No Data Input given or noise unspecified")
 
@@ -358,7 +364,7 @@ class SegmentedCovarianceMatrix(CovarianceMatrix):
         if not _is_scalar(noise):
             raise Exception("Invalid Noise given")
         self._require_data()
-        nv = float(torch.as_tensor(noise))
+        nv = _noise_float(noise)
         out = []
         for cn, hyp, di in zip(self.kernel.child_nodes, self._slices(hyper_parameter), self.data_input.data_inputs):
             out.append(engine.kernel_matrix(cn, hyp, di.data_x_train, di.data_x_train, nv) if di.n_train > 0 else None)
@@ -387,7 +393,7 @@ class SegmentedCovarianceMatrix(CovarianceMatrix):
         if not _is_scalar(noise):
             raise Exception("Invalid noise provided")
         self._require_data()
-        nv = float(torch.as_tensor(noise))
+        nv = _noise_float(noise)
         out = []
         for cn, hyp, di in zip(self.kernel.child_nodes, self._slices(hyper_parameter), self.data_input.data_inputs):
             out.append(engine.kernel_matrix(cn, hyp, di.data_x_test, di.data_x_test, nv) if di.n_test > 0 else None)

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must be loaded first: libgpk binds to torch's HIP r
 
 from . import _build
 
-GPK_ABI_VERSION = 3
+GPK_ABI_VERSION = 4
 GPK_F64, GPK_F32 = 0, 1
 OP_PER, OP_SE, OP_MAT32, OP_MAT52, OP_ADD, OP_MUL = 104, 105, 107, 108, 201, 202
 NODE_SCALED, NODE_ARD, NODE_SE_EXPANDED, NODE_STANDARD = 1, 2, 4, 8
@@ -30,6 +30,8 @@ EXPORTS = (
     "gpk_timing_read", "gpk_timing_reset", "gpk_tune", "gpk_potrf_aug_ex", "gpk_assemble_inverse",
     "gpk_grad_workspace_bytes", "gpk_nlml_grad", "gpk_assemble_ragged", "gpk_potrf_aug_ragged",
     "gpk_finalize_ragged", "gpk_nlml_ragged", "gpk_gemv",
+    "gpk_assemble_dense", "gpk_dgemm", "gpk_syevj_workspace_bytes", "gpk_syevj", "gpk_pinv_factor",
+    "gpk_ski_weights", "gpk_add_diagonal",
 )
 
 
@@ -93,6 +95,16 @@ def _declare(lib):
         "gpk_nlml_ragged": (c_int, [POINTER(GpkKdesc), POINTER(GpkLayout), P, c_int64, P, c_int64, P,
                                     c_int64, P, c_int64, P, P, P, P, P, P]),
         "gpk_gemv": (c_int, [P, c_int64, c_int64, c_int64, P, P, c_double, c_double, P]),
+        "gpk_assemble_dense": (c_int, [POINTER(GpkLayout), P, c_int64, c_int64, P, c_int64, P, c_int64,
+                                       c_int32, P, c_int64, P, P]),
+        "gpk_dgemm": (c_int, [c_int32, c_int32, c_int64, c_int64, c_int64, c_double, P, c_int64, c_int64,
+                              P, c_int64, c_int64, c_double, P, c_int64, c_int64, c_int32, P]),
+        "gpk_syevj_workspace_bytes": (c_size_t, [c_int64, c_int32]),
+        "gpk_syevj": (c_int, [c_int64, c_int32, P, c_int64, c_int64, P, P, P, c_size_t, c_int32,
+                              POINTER(c_int32), P]),
+        "gpk_pinv_factor": (c_int, [c_int64, c_int32, P, P, c_double, c_int32, P, P, P, P]),
+        "gpk_ski_weights": (c_int, [P, c_int64, P, c_int64, c_int32, P, P, P]),
+        "gpk_add_diagonal": (c_int, [P, c_int64, c_int64, c_int64, c_int32, c_double, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

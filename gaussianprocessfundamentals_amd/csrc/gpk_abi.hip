@@ -781,6 +781,163 @@ int gpk_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x
   return 0;
 }
 
+// ------------------------------------------------------------------ approximation paths (§8f.4)
+int gpk_assemble_dense(const gpk_layout* lay, const double* A, int64_t lda, int64_t a_bstride,
+                       const double* noise_dev, int64_t noise_stride, const double* E, int64_t e_bstride,
+                       int32_t eye, const double* y, int64_t y_bstride, void* W, void* stream) {
+  if (int e = check_layout(lay)) return e;
+  if (lay->dtype != GPK_F64) return fail_arg(1, "layout dtype (dense mode is fp64)");
+  if (!A) return fail_arg(2, "A");
+  if (lda < lay->n) return fail_arg(3, "lda");
+  if (!noise_dev) return fail_arg(5, "noise_dev");
+  if (eye && lay->m != lay->n) return fail_arg(9, "identity extra rows need a layout planned with m = n");
+  if (lay->m > 0 && !E && !eye) return fail_arg(7, "E (extra rows) or eye");
+  if (!y) return fail_arg(10, "y");
+  if (!W) return fail_arg(12, "W");
+  gpk_kdesc kd;
+  memset(&kd, 0, sizeof(kd));
+  kd.n_nodes = 1;
+  kd.dim = 1;
+  kd.nodes[0].op = GPK_OP_SE;
+  AsmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.noise = noise_dev;
+  a.noise_stride = noise_stride;
+  a.E = (lay->m > 0 && !eye) ? E : nullptr;
+  a.e_bs = e_bstride;
+  a.y = y;
+  a.y_bs = y_bstride;
+  a.W = W;
+  a.ld = lay->ld;
+  a.w_bs = lay->w_batch_stride;
+  a.n = lay->n;
+  a.m = lay->m;
+  a.n_pad = lay->n_pad;
+  a.y_row = lay->y_row;
+  a.p = lay->p;
+  a.d = 1;
+  a.dp = 1;
+  a.eye = eye ? 1 : 0;
+  a.ntile = lay->p / ATILE;
+  a.A = A;
+  a.a_ld = lda;
+  a.a_bs = a_bstride;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(launch_assemble(kd, a, lay->dtype, lay->batch, s), "assemble_dense");
+  return 0;
+}
+
+int gpk_dgemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, double alpha,
+              const double* A, int64_t lda, int64_t a_bstride, const double* B, int64_t ldb, int64_t b_bstride,
+              double beta, double* C, int64_t ldc, int64_t c_bstride, int32_t batch, void* stream) {
+  if (M < 0) return fail_arg(3, "M");
+  if (N < 0) return fail_arg(4, "N");
+  if (K < 0) return fail_arg(5, "K");
+  if (!A && M > 0 && K > 0) return fail_arg(7, "A");
+  if (lda < (trans_a ? M : K)) return fail_arg(8, "lda");
+  if (!B && N > 0 && K > 0) return fail_arg(10, "B");
+  if (ldb < (trans_b ? K : N)) return fail_arg(11, "ldb");
+  if (!C && M > 0 && N > 0) return fail_arg(14, "C");
+  if (ldc < N) return fail_arg(15, "ldc");
+  if (batch < 0) return fail_arg(17, "batch");
+  DgemmArgs g{trans_a ? 1 : 0, trans_b ? 1 : 0, M, N, K, A, lda, a_bstride, B, ldb, b_bstride,
+              C, ldc, c_bstride, alpha, beta};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(timed(5, 2.0 * (double)M * (double)N * (double)K * batch,
+                8.0 * ((double)M * K + (double)K * N + 2.0 * (double)M * N) * batch, s,
+                [&] { return launch_dgemm(g, batch, s); }),
+          "dgemm");
+  return 0;
+}
+
+size_t gpk_syevj_workspace_bytes(int64_t m, int32_t batch) {
+  if (m <= 0 || batch <= 0) return 8;
+  return (size_t)(4 * m * m * (int64_t)batch + 1) * sizeof(double);
+}
+
+int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
+              void* work, size_t work_bytes, int32_t max_sweeps, int32_t* sweeps_out, void* stream) {
+  if (m < 0 || m > (1 << 20)) return fail_arg(1, "m");
+  if (batch < 0) return fail_arg(2, "batch");
+  if (m == 0 || batch == 0) {
+    if (sweeps_out) *sweeps_out = 0;
+    return 0;
+  }
+  if (!A) return fail_arg(3, "A");
+  if (lda < m) return fail_arg(4, "lda");
+  if (!V) return fail_arg(6, "V");
+  if (!lam) return fail_arg(7, "lam");
+  if (!work || work_bytes < gpk_syevj_workspace_bytes(m, batch)) return fail_arg(9, "work_bytes");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t blk = m * m * (int64_t)batch;
+  double* buf = reinterpret_cast<double*>(work);
+  double* Ab[2] = {buf, buf + blk};
+  double* Vb[2] = {buf + 2 * blk, buf + 3 * blk};
+  int32_t* flag = reinterpret_cast<int32_t*>(buf + 4 * blk);
+  GPK_HIP(launch_jacobi_init(A, lda, a_bstride, (int)m, Ab[0], Vb[0], batch, s), "syevj init");
+  const int mm = (int)(m + (m & 1));
+  int cur = 0, sweeps = 0;
+  for (; sweeps < (max_sweeps > 0 ? max_sweeps : 60); ++sweeps) {
+    GPK_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s), "syevj flag");
+    for (int r = 0; r < mm - 1; ++r) {
+      JacobiArgs ja{Ab[cur], Ab[cur ^ 1], Vb[cur], Vb[cur ^ 1], (int32_t)m, mm, flag};
+      GPK_HIP(launch_jacobi_round(ja, r, batch, s), "syevj round");
+      cur ^= 1;
+    }
+    int32_t host_flag = 0;
+    GPK_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int32_t), hipMemcpyDeviceToHost, s), "syevj flag read");
+    GPK_HIP(hipStreamSynchronize(s), "syevj sync");
+    if (!host_flag) {
+      ++sweeps;
+      break;
+    }
+  }
+  GPK_HIP(launch_jacobi_out(Ab[cur], Vb[cur], (int)m, V, lam, batch, s), "syevj out");
+  if (sweeps_out) *sweeps_out = sweeps;
+  return 0;
+}
+
+int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam, double rcond, int32_t mode,
+                    double* mu, double* U, int32_t* rank_dev, void* stream) {
+  if (m <= 0) return fail_arg(1, "m");
+  if (batch <= 0) return fail_arg(2, "batch");
+  if (!V) return fail_arg(3, "V");
+  if (!lam) return fail_arg(4, "lam");
+  if (mode != 0 && mode != 1) return fail_arg(6, "mode");
+  if (!mu) return fail_arg(7, "mu");
+  if (!U) return fail_arg(8, "U");
+  if (!rank_dev) return fail_arg(9, "rank_dev");
+  if (rcond < 0.0) rcond = 10.0 * (double)m * 2.220446049250313e-16;  // tf.linalg.pinv's default
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(launch_pinv_factor(V, lam, (int)m, rcond, mode, mu, U, rank_dev, batch, s), "pinv_factor");
+  return 0;
+}
+
+int gpk_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int32_t d, double* Wm, double* work,
+                    void* stream) {
+  if (!X) return fail_arg(1, "X");
+  if (n <= 0) return fail_arg(2, "n");
+  if (!Z) return fail_arg(3, "Z");
+  if (m <= 0) return fail_arg(4, "m");
+  if (d <= 0 || d > GPK_MAX_DIM) return fail_arg(5, "d");
+  if (!Wm) return fail_arg(6, "Wm");
+  if (!work) return fail_arg(7, "work");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(launch_ski_weights(X, n, Z, m, d, Wm, work, s), "ski_weights");
+  return 0;
+}
+
+int gpk_add_diagonal(double* A, int64_t n, int64_t lda, int64_t a_bstride, int32_t batch, double value,
+                     void* stream) {
+  if (!A && n > 0) return fail_arg(1, "A");
+  if (n < 0) return fail_arg(2, "n");
+  if (lda < n) return fail_arg(3, "lda");
+  if (batch < 0) return fail_arg(5, "batch");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(launch_add_diag(A, n, lda, a_bstride, value, batch, s), "add_diagonal");
+  return 0;
+}
+
 int gpk_timing_enable(int on) {
   std::lock_guard<std::mutex> lk(g_timing.mu);
   g_timing.on = on != 0;

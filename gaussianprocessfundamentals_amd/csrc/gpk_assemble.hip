@@ -103,8 +103,10 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   for (int e = tid; e < kd.n_hyp; e += 256) hyp_s[e] = hyp_g[e];
   __syncthreads();
   const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
-  stage_points(kd, a, hyp_s, prow, gi0, b, true, slot_stride);
-  stage_points(kd, a, hyp_s, pcol, gj0, b, false, slot_stride);
+  if (a.A == nullptr) {
+    stage_points(kd, a, hyp_s, prow, gi0, b, true, slot_stride);
+    stage_points(kd, a, hyp_s, pcol, gj0, b, false, slot_stride);
+  }
   __syncthreads();
 
   const int c = tid & 63;
@@ -147,6 +149,11 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
       v = (ccls == CLS_TRAIN && gj == gi - a.n_pad) ? 1.0 : 0.0;
     } else if (a.E != nullptr && rcls == CLS_TEST) {
       v = (ccls == CLS_TRAIN) ? a.E[(int64_t)b * a.e_bs + (gi - a.n_pad) * a.n + gj] : 0.0;
+    } else if (a.A != nullptr && rcls == CLS_TRAIN && ccls == CLS_TRAIN) {
+      // dense mode: the caller's matrix (lower triangle, mirrored) + noise on the diagonal
+      const double* Ab = a.A + (int64_t)b * a.a_bs;
+      v = (gj <= gi) ? Ab[gi * a.a_ld + gj] : Ab[gj * a.a_ld + gi];
+      if (gi == gj) v += noise;
     } else if ((rcls == CLS_TRAIN || rcls == CLS_TEST) && col_kernel) {
 #ifndef GPK_ASM_ABLATE
 #define GPK_ASM_ABLATE 0  // timing-only: 1 skips the kernel evaluation (wrong results)

@@ -44,6 +44,11 @@ struct AsmArgs {
   // (rows nb[b] .. n_pad-1 become identity rows) and its first mb[b] test points (zero rows after)
   const int64_t* nb;
   const int64_t* mb;
+  // dense mode (gpk_assemble_dense): the training block is read from A (lower triangle, mirrored)
+  // instead of evaluated from the kernel program
+  const double* A;
+  int64_t a_ld;
+  int64_t a_bs;
 };
 
 struct GemmArgs {
@@ -150,6 +155,41 @@ hipError_t launch_trsv_diag(const TrsvArgs& a, int dtype, int32_t batch, hipStre
 hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x, double* y,
                        double alpha, double beta, hipStream_t s);
+
+// approximation paths (gpk_approx.hip)
+struct DgemmArgs {
+  int32_t ta, tb;
+  int64_t M, N, K;
+  const double* A;
+  int64_t lda, a_bs;
+  const double* B;
+  int64_t ldb, b_bs;
+  double* C;
+  int64_t ldc, c_bs;
+  double alpha, beta;
+};
+
+struct JacobiArgs {
+  const double* Ain;
+  double* Aout;
+  const double* Vin;
+  double* Vout;
+  int32_t m, mm;
+  int32_t* flag;
+};
+
+hipError_t launch_dgemm(const DgemmArgs& g, int32_t batch, hipStream_t s);
+hipError_t launch_jacobi_init(const double* A, int64_t lda, int64_t a_bs, int m, double* A0, double* V0,
+                              int32_t batch, hipStream_t s);
+hipError_t launch_jacobi_round(const JacobiArgs& a, int r, int32_t batch, hipStream_t s);
+hipError_t launch_jacobi_out(const double* Af, const double* Vf, int m, double* V, double* lam, int32_t batch,
+                             hipStream_t s);
+hipError_t launch_pinv_factor(const double* V, const double* lam, int m, double rcond, int mode, double* mu,
+                              double* U, int32_t* rank, int32_t batch, hipStream_t s);
+hipError_t launch_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int d, double* Wm,
+                              double* work, hipStream_t s);
+hipError_t launch_add_diag(double* A, int64_t n, int64_t lda, int64_t a_bs, double value, int32_t batch,
+                           hipStream_t s);
 
 enum { GEMM_UPDATE = 0, GEMM_TRSM = 1 };
 

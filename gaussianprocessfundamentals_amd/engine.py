@@ -493,3 +493,164 @@ def gemv(A: torch.Tensor, x: torch.Tensor, y: Optional[torch.Tensor] = None, alp
     nat.check(nat.lib().gpk_gemv(nat.ptr(A), n, m, int(A.stride(0)), nat.ptr(xv), nat.ptr(y), float(alpha),
                                  float(beta), nat.stream_handle(A.device)), "gpk_gemv")
     return y
+
+
+# ----------------------------------------------------------------------------- approximation paths
+# Dense device building blocks of the Nystroem / SKC / SKI matrices (include/gpk.h
+# "approximation paths").  Matrices are row-major fp64 device tensors, [n, m] or batched [B, n, m].
+def _mat_args(t: torch.Tensor, name: str):
+    if t.dtype != torch.float64 or t.device != device():
+        raise ValueError("%s must be a float64 tensor on %s" % (name, device()))
+    if t.dim() == 2:
+        t = t.unsqueeze(0)
+    if t.dim() != 3 or t.stride(2) != 1:
+        raise ValueError("%s must be a row-major [n, m] or [B, n, m] matrix" % name)
+    return t, int(t.stride(1)), int(t.stride(0)) if t.shape[0] > 1 else 0
+
+
+def dgemm(A: torch.Tensor, B: torch.Tensor, trans_a: bool = False, trans_b: bool = False, alpha: float = 1.0,
+          beta: float = 0.0, C: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C <- alpha op(A) op(B) + beta C on f64 MFMA (gpk_dgemm); the tf.matmul / tf.tensordot products
+    of gpbasics/Statistics/Nystroem_K.py and Metrics/StructuredKernelInterpolation.py."""
+    squeeze = A.dim() == 2 and B.dim() == 2 and (C is None or C.dim() == 2)
+    A3, lda, abs_ = _mat_args(A, "A")
+    B3, ldb, bbs = _mat_args(B, "B")
+    batch = max(A3.shape[0], B3.shape[0])
+    if A3.shape[0] not in (1, batch) or B3.shape[0] not in (1, batch):
+        raise ValueError("batch sizes of A and B differ")
+    M = A3.shape[2] if trans_a else A3.shape[1]
+    K = A3.shape[1] if trans_a else A3.shape[2]
+    Kb = B3.shape[2] if trans_b else B3.shape[1]
+    N = B3.shape[1] if trans_b else B3.shape[2]
+    if K != Kb:
+        raise ValueError("inner dimensions differ: %d vs %d" % (K, Kb))
+    if C is None:
+        C3 = torch.empty((batch, M, N), dtype=torch.float64, device=A.device)
+        beta = 0.0
+    else:
+        C3 = C.unsqueeze(0) if C.dim() == 2 else C
+        if tuple(C3.shape) != (batch, M, N) or not C3.is_contiguous():
+            raise ValueError("C must be a contiguous [%d, %d, %d] tensor" % (batch, M, N))
+    nat.check(nat.lib().gpk_dgemm(int(trans_a), int(trans_b), M, N, K, float(alpha), nat.ptr(A3), lda, abs_,
+                                  nat.ptr(B3), ldb, bbs, float(beta), nat.ptr(C3), N, M * N, batch,
+                                  nat.stream_handle(A.device)), "gpk_dgemm")
+    return C3[0] if squeeze else C3
+
+
+def syevj(A: torch.Tensor, max_sweeps: int = 60):
+    """Eigendecomposition of a symmetric [m, m] (or [B, m, m]) device matrix by two-sided Jacobi
+    (gpk_syevj): returns (lam [.., m], V [.., m, m] with the eigenvectors in its columns, sweeps)."""
+    A3, lda, abs_ = _mat_args(A, "A")
+    batch, m = A3.shape[0], A3.shape[1]
+    if A3.shape[2] != m:
+        raise ValueError("A must be square")
+    L = nat.lib()
+    V = torch.empty((batch, m, m), dtype=torch.float64, device=A.device)
+    lam = torch.empty((batch, m), dtype=torch.float64, device=A.device)
+    wb = int(L.gpk_syevj_workspace_bytes(m, batch))
+    work = torch.empty(max(1, (wb + 7) // 8), dtype=torch.float64, device=A.device)
+    sweeps = ctypes.c_int32(0)
+    nat.check(L.gpk_syevj(m, batch, nat.ptr(A3), lda, abs_, nat.ptr(V), nat.ptr(lam), nat.ptr(work), wb,
+                          int(max_sweeps), ctypes.byref(sweeps), nat.stream_handle(A.device)), "gpk_syevj")
+    if A.dim() == 2:
+        return lam[0], V[0], int(sweeps.value)
+    return lam, V, int(sweeps.value)
+
+
+def pinv_factor(lam: torch.Tensor, V: torch.Tensor, mode: int, rcond: float = -1.0):
+    """U = V diag(mu) with tf.linalg.pinv's cutoff (gpk_pinv_factor): mode 0 mu = 1/lam (pinv = U V^T),
+    mode 1 mu = lam^-1/2 (pinv = U U^T).  Returns (U, rank [B] int32 device tensor)."""
+    squeeze = V.dim() == 2
+    V3 = V.unsqueeze(0) if squeeze else V
+    lam2 = lam.unsqueeze(0) if lam.dim() == 1 else lam
+    batch, m = V3.shape[0], V3.shape[1]
+    U = torch.empty_like(V3)
+    mu = torch.empty((batch, m), dtype=torch.float64, device=V.device)
+    rank = torch.empty(batch, dtype=torch.int32, device=V.device)
+    nat.check(nat.lib().gpk_pinv_factor(m, batch, nat.ptr(V3.contiguous()), nat.ptr(lam2.contiguous()),
+                                        float(rcond), int(mode), nat.ptr(mu), nat.ptr(U), nat.ptr(rank),
+                                        nat.stream_handle(V.device)), "gpk_pinv_factor")
+    return (U[0] if squeeze else U), rank
+
+
+def pinv_sym(A: torch.Tensor, rcond: float = -1.0) -> torch.Tensor:
+    """tf.linalg.pinv of a symmetric matrix (gpbasics/Statistics/Nystroem_K.py:53): Jacobi
+    eigendecomposition, the reference's cutoff 10 m eps max|lam|, then V diag(1/lam) V^T on MFMA."""
+    lam, V, _ = syevj(A)
+    U, _ = pinv_factor(lam, V, 0, rcond)
+    return dgemm(U, V, trans_b=True)
+
+
+def ski_weights(X: torch.Tensor, Z: torch.Tensor) -> torch.Tensor:
+    """SKI interpolation weights [n, m] (gpk_ski_weights; StructuredKernelInterpolation.py:31-49)."""
+    X = as_device_f64(X)
+    Z = as_device_f64(Z)
+    n, d = X.shape
+    m = Z.shape[0]
+    Wm = torch.empty((n, m), dtype=torch.float64, device=X.device)
+    work = torch.empty(2 * n + 1, dtype=torch.float64, device=X.device)
+    nat.check(nat.lib().gpk_ski_weights(nat.ptr(X), n, nat.ptr(Z), m, d, nat.ptr(Wm), nat.ptr(work),
+                                        nat.stream_handle(X.device)), "gpk_ski_weights")
+    return Wm
+
+
+def add_diagonal(A: torch.Tensor, value: float) -> torch.Tensor:
+    """A += value * I in place (gpk_add_diagonal)."""
+    A3, lda, abs_ = _mat_args(A, "A")
+    n = min(A3.shape[1], A3.shape[2])
+    nat.check(nat.lib().gpk_add_diagonal(nat.ptr(A3), n, lda, abs_, A3.shape[0], float(value),
+                                         nat.stream_handle(A.device)), "gpk_add_diagonal")
+    return A
+
+
+class DenseFactorization(AugmentedFactorization):
+    """Augmented factorisation of a caller-supplied dense SPD matrix A + noise I (gpk_assemble_dense):
+    the approximate covariance matrices of the metrics (Nystroem, SKI) go through the same blocked
+    Cholesky as K.  ``inverse=True`` carries identity extra rows, so the corner holds -(A + noise I)^-1
+    (read out by :meth:`k_inv`); ``m`` > 0 with explicit rows E gives -E A^-1 E^T in the corner."""
+
+    def __init__(self, n: int, m: int = 0, batch: int = 1, inverse: bool = False):
+        self.inverse = bool(inverse)
+        super().__init__(n, 1, n if inverse else m, batch, torch.float64)
+
+    def run(self, A: torch.Tensor, noise, y: Optional[torch.Tensor] = None, E: Optional[torch.Tensor] = None):
+        A3, lda, abs_ = _mat_args(A, "A")
+        B, n = self.batch, self.n
+        if A3.shape[1] < n or A3.shape[2] < n or A3.shape[0] not in (1, B):
+            raise ValueError("A must hold [%d, %d] per member" % (n, n))
+        dev = self.W.device
+        noise_t = torch.as_tensor(noise, dtype=torch.float64).to(dev).reshape(-1).contiguous()
+        if noise_t.numel() not in (1, B):
+            raise ValueError("noise must be a scalar or one value per member")
+        ns = 1 if noise_t.numel() == B and B > 1 else 0
+        if y is None:
+            y = torch.zeros(n, dtype=torch.float64, device=dev)
+        y = y.to(device=dev, dtype=torch.float64).contiguous()
+        ybs = n if y.numel() == B * n and B > 1 else 0
+        _check_operand("y", y, ybs, n, B, dev)
+        ebs = 0
+        if self.m and not self.inverse:
+            if E is None:
+                raise ValueError("m = %d extra rows need E" % self.m)
+            E = E.to(device=dev, dtype=torch.float64).contiguous()
+            ebs = self.m * n if E.numel() == B * self.m * n and B > 1 else 0
+            _check_operand("E", E, ebs, self.m * n, B, dev)
+        s = nat.stream_handle(dev)
+        L = self.L
+        lay = self.layout
+        self.info.zero_()
+        nat.check(L.gpk_assemble_dense(ctypes.byref(lay), nat.ptr(A3), lda, abs_, nat.ptr(noise_t), ns,
+                                       nat.ptr(E) if E is not None else None, ebs, int(self.inverse),
+                                       nat.ptr(y), ybs, nat.ptr(self.W), s), "gpk_assemble_dense")
+        nat.check(L.gpk_potrf_aug_ex(ctypes.byref(lay), nat.ptr(self.W), nat.ptr(self.Winv), nat.ptr(self.info),
+                                     nat.AUG_EXTRA_IDENTITY if self.inverse else 0, s), "gpk_potrf_aug_ex")
+        nat.check(L.gpk_finalize(ctypes.byref(lay), nat.ptr(self.W), nat.ptr(self.info), nat.ptr(self.out),
+                                 nat.ptr(self.mu) if self.m else None, nat.ptr(self.var) if self.m else None, s),
+                  "gpk_finalize")
+        self.done = True
+        return self
+
+    def k_inv(self, b: int = 0) -> torch.Tensor:
+        if not self.inverse:
+            raise RuntimeError("DenseFactorization(..., inverse=True) carries the inverse")
+        return -self.corner(b)

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GPK_ABI_VERSION 3
+#define GPK_ABI_VERSION 4
 
 /* arithmetic types of the factorisation */
 enum { GPK_F64 = 0, GPK_F32 = 1 };
@@ -228,6 +228,53 @@ int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, 
  * get_alpha_strict_inverse (Metrics/Metrics.py:132-133).  Timed under class 5. */
 int gpk_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x, double* y, double alpha,
              double beta, void* stream);
+
+/* ---------------------------------------------------------------- approximation paths (§8f.4)
+ * Building blocks of the Nyström / SKC / SKI matrices of the reference
+ * (Statistics/Nystroem_K.py, Metrics/SkcLogLikelihood.py, Metrics/StructuredKernelInterpolation.py);
+ * the resulting dense matrices are factored through gpk_assemble_dense + gpk_potrf_aug. */
+
+/* Training block of the augmented matrix from a caller matrix A [n, lda] (fp64; the lower
+ * triangle is read and mirrored) + noise[b] on its diagonal, instead of a kernel evaluation
+ * (the metrics' get_covariance_matrix for an approximate K, Metrics/Metrics.py:113-126).  Extra
+ * rows: E [m, n] (corner 0: it becomes -E A^-1 E^T) or, with eye != 0 and a layout planned with
+ * m = n, the identity (corner -A^-1 after gpk_potrf_aug_ex(GPK_AUG_EXTRA_IDENTITY)). */
+int gpk_assemble_dense(const gpk_layout* lay, const double* A, int64_t lda, int64_t a_bstride,
+                       const double* noise_dev, int64_t noise_stride, const double* E, int64_t e_bstride,
+                       int32_t eye, const double* y, int64_t y_bstride, void* W, void* stream);
+
+/* C <- alpha op(A) op(B) + beta C, row-major fp64, op(A) [M, K], op(B) [K, N], batched by
+ * strides (f64 MFMA 16x16x4, 64 x 64 tiles): the tf.matmul / tf.tensordot products of
+ * Nystroem_K.py:62, :81-88, :98-104 and StructuredKernelInterpolation.py:25. */
+int gpk_dgemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, double alpha,
+              const double* A, int64_t lda, int64_t a_bstride, const double* B, int64_t ldb, int64_t b_bstride,
+              double beta, double* C, int64_t ldc, int64_t c_bstride, int32_t batch, void* stream);
+
+/* Symmetric eigendecomposition A = V diag(lam) V^T (V [m, m] row-major, eigenvectors in its
+ * columns) by two-sided cyclic Jacobi (round-robin pairs, one launch per round), batched.  The
+ * spectral half of tf.linalg.pinv (Nystroem_K.py:53).  Synchronises the stream once per sweep;
+ * *sweeps_out = sweeps run (the last one without rotations).  work: gpk_syevj_workspace_bytes. */
+size_t gpk_syevj_workspace_bytes(int64_t m, int32_t batch);
+int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
+              void* work, size_t work_bytes, int32_t max_sweeps, int32_t* sweeps_out, void* stream);
+
+/* U = V diag(mu) with mu_i = 1 / lam_i (mode 0; pinv = U V^T) or 1 / sqrt(lam_i) (mode 1;
+ * pinv = U U^T) for |lam_i| > rcond max|lam| and 0 otherwise -- tf.linalg.pinv's cutoff (rcond < 0:
+ * its default 10 m eps).  rank_dev[b] = kept eigenvalues, -1 if mode 1 keeps a negative one. */
+int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam, double rcond, int32_t mode,
+                    double* mu, double* U, int32_t* rank_dev, void* stream);
+
+/* SKI interpolation weights W [n, m] (row-major) of training points X [n, d] on inducing points
+ * Z [m, d]: get_weight_matrix (StructuredKernelInterpolation.py:31-49), expanded-norm euclidean
+ * distances, nearest (all ties) 1 - d1 / (d1 + d2), second nearest d1 / (d1 + d2).
+ * work: 2 n + 1 doubles. */
+int gpk_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int32_t d, double* Wm, double* work,
+                    void* stream);
+
+/* A[b] += value * I (the "+ tf.eye(n) * noise" of Nystroem_K.py:68-69 and
+ * StructuredKernelInterpolation.py:27). */
+int gpk_add_diagonal(double* A, int64_t n, int64_t lda, int64_t a_bstride, int32_t batch, double value,
+                     void* stream);
 
 /* Per-kernel-class timing with HIP events recorded on the launch stream.
  * class: 0 assemble, 1 diag, 2 trsm, 3 update, 4 finalize, 5 trsv, 6 grad */

@@ -415,3 +415,137 @@ def known_answers() -> List[Tuple[str, float, float]]:
         k2 = kernel_matrix((name, {"ard": False}), [1.0], xa / ls, xb / ls)
         out.append(("ard_" + name, float(np.max(np.abs(k1 - k2))), 0.0))
     return out
+
+
+# ----------------------------------------------------------------------------- approximations (§8f.4)
+def tf_pinv(A: np.ndarray) -> np.ndarray:
+    """tf.linalg.pinv with its default rcond = 10 max(rows, cols) eps: singular values s > rcond
+    max(s) inverted, the rest dropped (Statistics/Nystroem_K.py:53 calls it on K_mm)."""
+    rcond = 10.0 * max(A.shape) * np.finfo(np.float64).eps
+    return np.linalg.pinv(A, rcond=rcond)
+
+
+def nystroem_k_approx(tree, hyp, x, z, scaled=False, se_expanded=False):
+    """K_hat = (K_nm pinv(K_mm)) K_nm^T (Statistics/Nystroem_K.py:36-64); z are the inducing
+    inputs the reference passes as ``indices``."""
+    knm = kernel_matrix(tree, hyp, x, z, scaled, se_expanded)
+    kmm = kernel_matrix(tree, hyp, z, z, scaled, se_expanded)
+    return (knm @ tf_pinv(kmm)) @ knm.T, knm, kmm
+
+
+def nystroem_det(tree, hyp, noise, x, z, scaled=False, se_expanded=False) -> float:
+    """get_K_approx_det (Statistics/Nystroem_K.py:92-108): (n - m) log(noise) +
+    slogdet(noise I_m + K_nm^T (K_nm pinv(K_mm)))[1]."""
+    _, knm, kmm = nystroem_k_approx(tree, hyp, x, z, scaled, se_expanded)
+    n, m = knm.shape
+    phi_t = knm @ tf_pinv(kmm)
+    to_det = np.eye(m) * noise + knm.T @ phi_t
+    return float((n - m) * math.log(noise) + np.linalg.slogdet(to_det)[1])
+
+
+def nystroem_nlml(tree, hyp, noise, x, y, z, handling: str = "CHOLESKY_BASED", lower_bound: bool = False,
+                  jitter: float = 1e-8, scaled=False, se_expanded=False) -> float:
+    """LogLikelihood.get_metric with BASIC_NYSTROEM / SKC_LOWER_BOUND (Metrics/LogLikelihood.py:30-65,
+    Metrics/Metrics.py:77-150): the covariance matrix is K_hat + noise I, the log-determinant the
+    Nystroem one; CHOLESKY_BASED keeps the EXACT alpha (get_alpha_cholesky reads the holistic
+    covariance matrix), the other handlings solve with K_hat + noise I.  SKC_LOWER_BOUND subtracts
+    trace(K_hat + noise I - K) / (2 p_cov_matrix_jitter) (:51-60)."""
+    y = np.asarray(y, np.float64).reshape(-1, 1)
+    n = y.shape[0]
+    khat, _, _ = nystroem_k_approx(tree, hyp, x, z, scaled, se_expanded)
+    khat_n = khat + np.eye(n) * noise
+    if handling == "CHOLESKY_BASED":
+        L = cholesky_lower(k_noised(tree, hyp, noise, x, scaled, se_expanded))
+        alpha = l_alpha(L, y)
+    elif handling == "LINEAR_CONJUGATE_GRADIENT":
+        alpha = linear_cg(khat_n, y, np.zeros_like(y))
+    elif handling == "PSEUDO_INVERSE":
+        alpha = tf_pinv(khat_n) @ y
+    else:
+        alpha = np.linalg.inv(khat_n) @ y
+    logdet = nystroem_det(tree, hyp, noise, x, z, scaled, se_expanded)
+    ll = -0.5 * float(y.T @ alpha) - 0.5 * logdet - 0.5 * n * math.log(2 * math.pi)
+    if lower_bound:
+        k = kernel_matrix(tree, hyp, x, x, scaled, se_expanded)
+        ll -= (1.0 / (2.0 * jitter)) * float(np.trace(khat_n - k))
+    return -ll
+
+
+def vsgd_step(alpha: np.ndarray, grad: np.ndarray, batch_size: float = 10.0, total: float = 10.0,
+              decay: float = 0.95, max_lr: float = 1e-6) -> np.ndarray:
+    """One tfp.optimizer.VariationalSGD(10, 10) step from zero moments in burn-in (iteration 0 <
+    burnin = 25, so the learning-rate cap is burnin_max_learning_rate = 1e-6): first moment
+    m = (1 - decay) g, second moment v = (1 - decay) (g - m)^2, per-coordinate learning rate
+    min(2 batch_size / (total v), cap) (Mandt et al. 2017's preconditioned constant SGD), then
+    alpha - lr g.  Restated from the published algorithm (TFP is absent here): parity unpinned."""
+    m = (1.0 - decay) * grad
+    v = (1.0 - decay) * (grad - m) ** 2
+    with np.errstate(divide="ignore"):
+        lr = np.where(v > 0, 2.0 * batch_size / (total * v), np.inf)
+    lr = np.clip(lr, 0.0, max_lr)
+    return alpha - lr * grad
+
+
+def skc_upper_bound(tree, hyp, noise, x, y, z, scaled=False, se_expanded=False) -> float:
+    """LogLikelihoodUpperBound.get_metric (Metrics/SkcLogLikelihood.py:26-69): alpha starts at ones;
+    minimize(opt, alpha) differentiates the tuple (value, gradient) that opt returns, so the step
+    uses grad = (K alpha - y) + K 1 (K = exact K + noise I); the value is
+    1/2 alpha^T K alpha - alpha^T y - 1/2 nystroem_det - n/2 log 2 pi at the stepped alpha."""
+    y = np.asarray(y, np.float64).reshape(-1, 1)
+    n = y.shape[0]
+    K = k_noised(tree, hyp, noise, x, scaled, se_expanded)
+    a = np.ones((n, 1))
+    g = (K @ a - y) + K @ np.ones((n, 1))
+    a = vsgd_step(a, g)
+    fit = 0.5 * float(a.T @ K @ a) - float(a.T @ y)
+    det = nystroem_det(tree, hyp, noise, x, z, scaled, se_expanded)
+    return fit - 0.5 * det - 0.5 * n * math.log(2 * math.pi)
+
+
+def ski_inducing_indices(n: int, m: int) -> np.ndarray:
+    """np.linspace(0, n, num=m, endpoint=False, dtype=int) (StructuredKernelInterpolation.py:14-16)."""
+    return np.linspace(start=0, stop=n, num=m, endpoint=False, dtype=int)
+
+
+def ski_weight_matrix(x: np.ndarray, z: np.ndarray) -> np.ndarray:
+    """get_weight_matrix (Metrics/StructuredKernelInterpolation.py:31-49), op for op."""
+    distances = euclidian_distance(x, z)
+    reduce_min_1 = distances.min(axis=1).reshape(-1, 1)
+    min_1_condition = distances == reduce_min_1
+    mask_1_distances = distances.max() * min_1_condition.astype(np.float64)
+    distances_masked = distances + mask_1_distances
+    reduce_min_2 = distances_masked.min(axis=1).reshape(-1, 1)
+    min_2_condition = distances_masked == reduce_min_2
+    weight_i = 1 - reduce_min_1 / (reduce_min_1 + reduce_min_2)
+    return (np.zeros_like(distances) + weight_i * min_1_condition.astype(np.float64)
+            + (1 - weight_i) * min_2_condition.astype(np.float64))
+
+
+def ski_matrix(tree, hyp, noise, x, m: int, scaled=False, se_expanded=False) -> np.ndarray:
+    """get_ski_matrix (StructuredKernelInterpolation.py:10-28): W K_mm W^T + noise I with the
+    inducing points x[linspace indices]."""
+    idx = ski_inducing_indices(x.shape[0], m)
+    z = x[idx]
+    kmm = kernel_matrix(tree, hyp, z, z, scaled, se_expanded)
+    w = ski_weight_matrix(x, z)
+    return (w @ kmm) @ w.T + np.eye(x.shape[0]) * noise
+
+
+def ski_nlml(tree, hyp, noise, x, y, m: int, handling: str = "CHOLESKY_BASED", scaled=False,
+             se_expanded=False) -> float:
+    """LogLikelihood.get_metric with SKI: only get_covariance_matrix changes (Metrics/Metrics.py:104-105),
+    so CHOLESKY_BASED (alpha and log-det from the holistic covariance matrix) is the exact -LML and
+    the other handlings use W K_mm W^T + noise I with slogdet."""
+    y = np.asarray(y, np.float64).reshape(-1, 1)
+    n = y.shape[0]
+    if handling == "CHOLESKY_BASED":
+        return nlml(tree, hyp, noise, x, y, scaled, se_expanded)
+    K = ski_matrix(tree, hyp, noise, x, m, scaled, se_expanded)
+    if handling == "LINEAR_CONJUGATE_GRADIENT":
+        alpha = linear_cg(K, y, np.zeros_like(y))
+    elif handling == "PSEUDO_INVERSE":
+        alpha = tf_pinv(K) @ y
+    else:
+        alpha = np.linalg.inv(K) @ y
+    logdet = np.linalg.slogdet(K)[1]
+    return -(-0.5 * float(y.T @ alpha) - 0.5 * logdet - 0.5 * n * math.log(2 * math.pi))

@@ -114,17 +114,47 @@ def test_data_input_split_and_shapes():
         gp.p_device = "cuda"
 
 
-def test_metric_strategy_rejection_messages():
+def test_metric_approximation_binding():
+    """Metric.__init__ (gpbasics/Metrics/Metrics.py:45-107): approximations set n_inducting_train and
+    swap get_covariance_matrix / get_log_determinant; a subset as large as the data disables them."""
     from gaussianprocessfundamentals_amd.Metrics.Metrics import Metric, MetricType
 
     class Dummy:
         n_train = 10
+        n_test = 5
 
-    # Nystroem / SKC / SKI approximations are not provided by the device engine
-    for approx in (mht.MatrixApproximations.BASIC_NYSTROEM, mht.MatrixApproximations.SKI,
-                   mht.MatrixApproximations.SKC_LOWER_BOUND):
-        with pytest.raises(NotImplementedError):
-            Metric(Dummy(), None, MetricType.LL, approx, mht.NumericalMatrixHandlingType.CHOLESKY_BASED, subset_size=5)
+    class Cov:
+        kernel = None
+
+        def set_data_input(self, di):
+            self.di = di
+
+    A, H = mht.MatrixApproximations, mht.NumericalMatrixHandlingType
+    m = Metric(Dummy(), Cov(), MetricType.LL, A.BASIC_NYSTROEM, H.CHOLESKY_BASED, subset_size=4)
+    assert m.data_input.n_inducting_train == 4 and m.data_input.n_inducting_test == 2.0
+    assert m.get_covariance_matrix.__func__ is Metric.get_nystroem_matrix
+    assert m.get_log_determinant.__func__ is Metric.get_log_determinant_nystroem
+    assert m.get_alpha.__func__ is Metric.get_alpha_cholesky and m._approximate()
+    m = Metric(Dummy(), Cov(), MetricType.LL, A.SKC_UPPER_BOUND, H.LINEAR_CONJUGATE_GRADIENT, subset_size=4)
+    assert m.get_covariance_matrix.__func__ is Metric.get_default_covariance_matrix and not m._approximate()
+    assert m.get_log_determinant.__func__ is Metric.get_log_determinant_nystroem
+    m = Metric(Dummy(), Cov(), MetricType.LL, A.SKI, H.STRICT_INVERSE, subset_size=4)
+    assert m.get_covariance_matrix.__func__ is Metric.get_ski_matrix
+    assert m.get_log_determinant.__func__ is Metric.get_log_determinant_slodget
+    m = Metric(Dummy(), Cov(), MetricType.LL, A.SKI, H.CHOLESKY_BASED)         # subset = int(10 * 0.1)
+    assert m.subset_size == 1 and m.data_input.n_inducting_train == 1
+    m = Metric(Dummy(), Cov(), MetricType.LL, A.SKI, H.CHOLESKY_BASED, subset_size=10)
+    assert m.local_approx is A.NONE and not m._approximate()
+
+
+def test_variational_sgd_step_matches_oracle():
+    from oracle import gp_oracle as o
+    from gaussianprocessfundamentals_amd.Metrics.SkcLogLikelihood import variational_sgd_step
+    g = np.array([0.0, 1.0, -3.0, 5e3, 6.5e3, -7e3, 1e5]).reshape(-1, 1)
+    a = np.ones_like(g)
+    got = variational_sgd_step(torch.as_tensor(a), torch.as_tensor(g)).numpy()
+    assert np.array_equal(got, o.vsgd_step(a, g))
+    assert got[0, 0] == 1.0 and got[1, 0] == 1.0 - 1e-6
 
 
 @pytest.mark.parametrize("n,world", [(128, 1), (128, 2), (128, 8), (10, 3), (3, 8), (0, 4)])

@@ -70,3 +70,48 @@ def test_golden_inputs_are_reproducible():
     g = golden("c2_se_n4096")
     x, y = o.make_inputs("C2")
     np.testing.assert_array_equal(x, g["x"])
+
+
+# ------------------------------------------------------------------ approximations (§8f.4)
+def test_nystroem_with_all_points_is_exact():
+    """Inducing points = training points: K_hat = K, so the Nystroem determinant is logdet(K + s I)
+    and SKC's correction is n s / (2 jitter)."""
+    rng = np.random.default_rng(2)
+    x = np.linspace(0, 1, 12).reshape(-1, 1)
+    y = rng.standard_normal(12)
+    tree = ("SE", {"ard": False})
+    K = o.k_noised(tree, [0.1], 1e-2, x)
+    assert abs(o.nystroem_det(tree, [0.1], 1e-2, x, x) - np.linalg.slogdet(K)[1]) < 1e-9
+    exact = o.nlml(tree, [0.1], 1e-2, x, y)
+    for h in ("CHOLESKY_BASED", "STRICT_INVERSE", "PSEUDO_INVERSE"):
+        assert abs(o.nystroem_nlml(tree, [0.1], 1e-2, x, y, x, handling=h) - exact) < 1e-8 * abs(exact)
+    lb = o.nystroem_nlml(tree, [0.1], 1e-2, x, y, x, lower_bound=True, jitter=1e-8)
+    assert abs(lb - (exact + 12 * 1e-2 / (2 * 1e-8))) < 1e-6 * abs(lb)
+
+
+def test_ski_weights_on_inducing_points_and_midpoints():
+    z = np.array([[0.0], [1.0], [2.0]])
+    w = o.ski_weight_matrix(z, z)
+    assert np.array_equal(w, np.eye(3))
+    x = np.array([[0.25], [1.5]])
+    w = o.ski_weight_matrix(x, z)
+    # x = 1.5 is equidistant from 1 and 2: BOTH are "nearest" (weight 1 - 0.5 / (0.5 + 1.5) each, with
+    # the masking offset = the global max distance 1.5) and 0 becomes the second nearest -- the
+    # reference's tie behaviour, rows need not sum to 1
+    assert np.allclose(w, [[0.75, 0.25, 0.0], [0.25, 0.75, 0.75]])
+    # all points inducing: K_ski = K + s I, so every handling gives the exact -LML
+    xs = np.linspace(0, 1, 10).reshape(-1, 1)
+    y = np.cos(3 * xs[:, 0])
+    tree = ("SE", {"ard": False})
+    exact = o.nlml(tree, [0.2], 1e-2, xs, y)
+    assert abs(o.ski_nlml(tree, [0.2], 1e-2, xs, y, 10, handling="STRICT_INVERSE") - exact) < 1e-8 * abs(exact)
+    assert list(o.ski_inducing_indices(10, 4)) == [0, 2, 5, 7]
+
+
+def test_vsgd_step_burnin_cap():
+    g = np.array([[1.0], [-2.0], [0.0]])
+    a = o.vsgd_step(np.ones_like(g), g)
+    assert np.allclose(a, 1 - 1e-6 * g)
+    big = np.array([[1e6]])            # 2 / (0.05 * 0.9025 g^2) < 1e-6: the adaptive rate wins
+    lr = 2.0 / (0.05 * (0.95e6) ** 2)
+    assert np.allclose(o.vsgd_step(np.ones((1, 1)), big), 1 - lr * 1e6)
