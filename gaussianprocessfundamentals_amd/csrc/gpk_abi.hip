@@ -142,6 +142,7 @@ struct Tune {
   int64_t fuse_kbuild;    // gpk_nlml: K build fused into the first trailing update (single-node kernels)
   int64_t upd_band;       // trailing-update tile order: 0 row-major, B > 0 bands of B tile rows
   int64_t skip_zero_rows; // skip the MFMAs of the all-zero 16-row blocks below the y row
+  int64_t syevj_abs_tol_e3; // Jacobi: absolute rotation threshold in units of 1e-3 eps max|a_ii|
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -154,7 +155,7 @@ Tune& tune() {
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
-                         env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1)};
+                         env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 1000)};
   return t;
 }
 
@@ -852,7 +853,7 @@ int gpk_dgemm(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
 
 size_t gpk_syevj_workspace_bytes(int64_t m, int32_t batch) {
   if (m <= 0 || batch <= 0) return 8;
-  return (size_t)(4 * m * m * (int64_t)batch + 1) * sizeof(double);
+  return (size_t)(4 * m * m * (int64_t)batch + 2) * sizeof(double);
 }
 
 int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
@@ -875,12 +876,21 @@ int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
   double* Vb[2] = {buf + 2 * blk, buf + 3 * blk};
   int32_t* flag = reinterpret_cast<int32_t*>(buf + 4 * blk);
   GPK_HIP(launch_jacobi_init(A, lda, a_bstride, (int)m, Ab[0], Vb[0], batch, s), "syevj init");
+  // absolute threshold: off-diagonal elements below tol_scale eps max|a_ii| are rounding noise at the
+  // accuracy of any backward-stable eigensolver (and of tf.linalg.pinv's SVD); rotating them only
+  // shuffles the noise-level subspace sweep after sweep
+  double* dmax = reinterpret_cast<double*>(flag) + 1;
+  GPK_HIP(launch_diag_absmax(Ab[0], (int)m, batch, dmax, s), "syevj scale");
+  double host_dmax = 0.0;
+  GPK_HIP(hipMemcpyAsync(&host_dmax, dmax, sizeof(double), hipMemcpyDeviceToHost, s), "syevj scale read");
+  GPK_HIP(hipStreamSynchronize(s), "syevj sync");
+  const double tol_abs = (double)tune().syevj_abs_tol_e3 * 1e-3 * 2.220446049250313e-16 * host_dmax;
   const int mm = (int)(m + (m & 1));
   int cur = 0, sweeps = 0;
   for (; sweeps < (max_sweeps > 0 ? max_sweeps : 60); ++sweeps) {
     GPK_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s), "syevj flag");
     for (int r = 0; r < mm - 1; ++r) {
-      JacobiArgs ja{Ab[cur], Ab[cur ^ 1], Vb[cur], Vb[cur ^ 1], (int32_t)m, mm, flag};
+      JacobiArgs ja{Ab[cur], Ab[cur ^ 1], Vb[cur], Vb[cur ^ 1], (int32_t)m, mm, flag, tol_abs};
       GPK_HIP(launch_jacobi_round(ja, r, batch, s), "syevj round");
       cur ^= 1;
     }
@@ -958,6 +968,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "fuse_kbuild")) slot = &t.fuse_kbuild;
   else if (!strcmp(key, "upd_band")) slot = &t.upd_band;
   else if (!strcmp(key, "skip_zero_rows")) slot = &t.skip_zero_rows;
+  else if (!strcmp(key, "syevj_abs_tol_e3")) slot = &t.syevj_abs_tol_e3;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -98,8 +98,8 @@ __device__ __forceinline__ int jac_partner(int i, int r, int mm) {
 }
 
 // rotation seen from index i: new_i = cs x_i + cp x_partner (rows of J^T A, columns of A J)
-__device__ __forceinline__ void jac_rotation(const double* A, int m, int i, int j, int* part, double* cs,
-                                             double* cp, int* flag) {
+__device__ __forceinline__ void jac_rotation(const double* A, int m, int i, int j, double tol_abs, int* part,
+                                             double* cs, double* cp, int* flag) {
   *part = i;
   *cs = 1.0;
   *cp = 0.0;
@@ -107,7 +107,7 @@ __device__ __forceinline__ void jac_rotation(const double* A, int m, int i, int 
   const int p = i < j ? i : j, qq = i < j ? j : i;
   const double apq = A[(int64_t)p * m + qq];
   const double app = A[(int64_t)p * m + p], aqq = A[(int64_t)qq * m + qq];
-  if (apq == 0.0 || fabs(apq) <= 2.220446049250313e-16 * sqrt(fabs(app) * fabs(aqq))) return;
+  if (fabs(apq) <= tol_abs || fabs(apq) <= 2.220446049250313e-16 * sqrt(fabs(app) * fabs(aqq))) return;
   const double th = (aqq - app) / (2.0 * apq);
   double t;
   if (fabs(th) > 1e150) t = 0.5 / th;
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void jacobi_round_kernel(JacobiArgs a, int r) 
     const int idx = (tid < JT ? i0 : j0) + (tid % JT);
     int part, fl = 0;
     double cs, cp;
-    jac_rotation(A, a.m, idx, idx < a.mm ? jac_partner(idx, r, a.mm) : idx, &part, &cs, &cp, &fl);
+    jac_rotation(A, a.m, idx, idx < a.mm ? jac_partner(idx, r, a.mm) : idx, a.tol_abs, &part, &cs, &cp, &fl);
     if (fl) *a.flag = 1;
     if (tid < JT) { rpart[tid] = part; rcs[tid] = cs; rcp[tid] = cp; }
     else { cpart[tid - JT] = part; ccs[tid - JT] = cs; ccp[tid - JT] = cp; }
@@ -170,6 +170,21 @@ __global__ __launch_bounds__(256) void jacobi_init_kernel(const double* A, int64
   const int64_t i = e / m, j = e % m;
   A0[b * mm + e] = A[b * a_bs + i * lda + j];
   V0[b * mm + e] = (i == j) ? 1.0 : 0.0;
+}
+
+// max |A_ii| over every member (the absolute scale of the rotation threshold)
+__global__ __launch_bounds__(256) void diag_absmax_kernel(const double* A0, int m, int32_t batch, double* out) {
+  __shared__ double red[256];
+  const int64_t mm = (int64_t)m * m;
+  double mx = 0.0;
+  for (int64_t e = threadIdx.x; e < (int64_t)m * batch; e += 256) mx = fmax(mx, fabs(A0[(e / m) * mm + (e % m) * (m + 1)]));
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0];
 }
 
 __global__ __launch_bounds__(256) void jacobi_out_kernel(const double* Af, const double* Vf, int m, double* V,
@@ -321,6 +336,11 @@ hipError_t launch_jacobi_init(const double* A, int64_t lda, int64_t a_bs, int m,
   const int64_t mm = (int64_t)m * m;
   hipLaunchKernelGGL(jacobi_init_kernel, dim3((unsigned)((mm + 255) / 256), batch), dim3(256), 0, s, A, lda, a_bs,
                      m, A0, V0);
+  return hipGetLastError();
+}
+
+hipError_t launch_diag_absmax(const double* A0, int m, int32_t batch, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(diag_absmax_kernel, dim3(1), dim3(256), 0, s, A0, m, batch, out);
   return hipGetLastError();
 }
 

@@ -176,12 +176,14 @@ struct JacobiArgs {
   double* Vout;
   int32_t m, mm;
   int32_t* flag;
+  double tol_abs;  // pairs with |a_pq| <= tol_abs are not rotated (besides the relative criterion)
 };
 
 hipError_t launch_dgemm(const DgemmArgs& g, int32_t batch, hipStream_t s);
 hipError_t launch_jacobi_init(const double* A, int64_t lda, int64_t a_bs, int m, double* A0, double* V0,
                               int32_t batch, hipStream_t s);
 hipError_t launch_jacobi_round(const JacobiArgs& a, int r, int32_t batch, hipStream_t s);
+hipError_t launch_diag_absmax(const double* A0, int m, int32_t batch, double* out, hipStream_t s);
 hipError_t launch_jacobi_out(const double* Af, const double* Vf, int m, double* V, double* lam, int32_t batch,
                              hipStream_t s);
 hipError_t launch_pinv_factor(const double* V, const double* lam, int m, double rcond, int mode, double* mu,

@@ -1,5 +1,9 @@
-"""Diagnostics of gpk_syevj on an ill-conditioned kernel Gram matrix (sweeps, eigenvalue error)."""
+"""gpk_syevj convergence vs the absolute rotation threshold (tune key syevj_abs_tol_e3): sweeps,
+time and eigenvalue / pinv accuracy against numpy on kernel Gram matrices and a random symmetric one.
+
+usage: python tools/diag_syevj.py"""
 import sys
+import time
 
 import numpy as np
 import torch
@@ -8,31 +12,35 @@ sys.path.insert(0, ".")
 import gaussianprocessfundamentals_amd.global_parameters as gp  # noqa: E402
 
 gp.init(0)
+from gaussianprocessfundamentals_amd import _native as nat  # noqa: E402
 from gaussianprocessfundamentals_amd import engine  # noqa: E402
 from oracle import gp_oracle as o  # noqa: E402
 
+SE = ("SE", {"ard": False})
 rng = np.random.default_rng(2)
-x = np.sort(rng.uniform(0, 1, (250, 1)), axis=0)
-for name, z, l in (("clustered25", x[:25], 0.2), ("grid60", np.linspace(0, 1, 60).reshape(-1, 1), 0.3)):
-    K = o.kernel_matrix(("SE", {"ard": False}), [l], z, z)
-    lam, V, sweeps = engine.syevj(torch.tensor(K, device="cuda"))
-    lam = lam.cpu().numpy()
-    V = V.cpu().numpy()
-    ref = np.linalg.eigvalsh(K)
-    print(name, "sweeps", sweeps, "max eig err", np.max(np.abs(np.sort(lam) - ref)),
-          "recon", np.max(np.abs(V @ np.diag(lam) @ V.T - K)), "orth", np.max(np.abs(V.T @ V - np.eye(len(K)))))
-    print("  smallest dev", np.sort(lam)[:4], "ref", ref[:4])
-    t = 10 * np.log(10 * np.sort(lam) + 1e-2)
-    tr = 10 * np.log(10 * ref + 1e-2)
-    print("  logdet terms diff", np.max(np.abs(t - tr)), "sum diff", np.sum(t) - np.sum(tr))
-
-from gaussianprocessfundamentals_amd.Metrics import StructuredKernelInterpolation as ski  # noqa: E402
-kmm = o.kernel_matrix(("SE", {"ard": False}), [0.2], x[:25], x[:25])
-lam_np = np.linalg.eigvalsh(kmm)
-terms = 10 * np.log(10 * lam_np + 1e-2)
-got = float(ski.get_approx_logdet(torch.tensor(kmm), 250, 25, 1e-2))
-lam_d, _, sw = engine.syevj(torch.tensor(kmm, device="cuda"))
-print("approx_logdet", got, np.sum(terms), got - np.sum(terms), "sweeps", sw)
-print("dev lam", np.sort(lam_d.cpu().numpy())[:6])
-print("np  lam", lam_np[:6])
-print("torch-side", float((250 / 25) * torch.sum(torch.log((250 / 25) * lam_d + 1e-2))))
+G = rng.standard_normal((300, 300))
+mats = {
+    "grid409_l0.01": o.kernel_matrix(SE, [0.01], np.linspace(0, 1, 409).reshape(-1, 1), np.linspace(0, 1, 409).reshape(-1, 1)),
+    "grid409_l0.05": o.kernel_matrix(SE, [0.05], np.linspace(0, 1, 409).reshape(-1, 1), np.linspace(0, 1, 409).reshape(-1, 1)),
+    "rand300": (G + G.T) / 2,
+}
+for tol in (1000, 10000, 100000):
+    nat.tune("syevj_abs_tol_e3", tol)
+    for name, K in mats.items():
+        Kd = torch.tensor(K, device="cuda")
+        engine.syevj(Kd)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lam, V, sweeps = engine.syevj(Kd)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+        lam, V = lam.cpu().numpy(), V.cpu().numpy()
+        ref = np.linalg.eigvalsh(K)
+        scale = np.max(np.abs(ref))
+        P = engine.pinv_sym(Kd).cpu().numpy()
+        Pref = o.tf_pinv(K)
+        print("tol_e3 %5d %-14s sweeps %2d  %7.1f ms  eig err %.2e  recon %.2e  orth %.2e  pinv rel %.2e" % (
+            tol, name, sweeps, ms, np.max(np.abs(np.sort(lam) - ref)) / scale,
+            np.max(np.abs(V @ np.diag(lam) @ V.T - K)) / scale, np.max(np.abs(V.T @ V - np.eye(len(K)))),
+            np.max(np.abs(P - Pref)) / np.max(np.abs(Pref))))
+nat.tune("syevj_abs_tol_e3", 1000)
