@@ -326,3 +326,23 @@ def test_cross_validation_matches_oracle_folds(metric):
         else:
             vals.append(o.mse(SE, [0.15], NOISE, x[tr], y[tr], x[te], y[te]))
     assert rel(got, float(np.mean(vals))) < 1e-9
+
+
+@pytest.mark.parametrize("approx,handling", [
+    (mht.MatrixApproximations.NONE, mht.NumericalMatrixHandlingType.STRICT_INVERSE),
+    (mht.MatrixApproximations.SKI, mht.NumericalMatrixHandlingType.CHOLESKY_BASED),
+    (mht.MatrixApproximations.SKI, mht.NumericalMatrixHandlingType.STRICT_INVERSE)])
+def test_blockwise_log_likelihood_per_segment_strategies(approx, handling):
+    """Other strategies run one LogLikelihood per segment, as the reference always does
+    (M/LogLikelihood.py:86-104): STRICT_INVERSE and SKI + CHOLESKY (= exact) give the exact sum;
+    SKI + STRICT the sum of the per-segment SKI likelihoods (m = 10 % of each segment)."""
+    g, segs = blockwise_setup(n=900, n_test=60)
+    flat = [0.08, 0.3, 0.9, 0.45]
+    m = get_metric_by_type(MetricType.blockwise_LL, g, approx, handling)
+    got = float(m.get_metric(hyp_list(flat), T(NOISE)))
+    if approx is mht.MatrixApproximations.SKI and handling is mht.NumericalMatrixHandlingType.STRICT_INVERSE:
+        exp = sum(o.ski_nlml(t, h, NOISE, s[0], s[1], int(len(s[0]) * 0.1), handling="STRICT_INVERSE")
+                  for t, h, s in zip(CHILD_TREES, CHILD_HYPS, segs))
+    else:
+        exp = o.blockwise_nlml([(t, h, s[0], s[1]) for t, h, s in zip(CHILD_TREES, CHILD_HYPS, segs)], NOISE)
+    assert rel(got, exp) < 1e-9, (got, exp)
