@@ -257,6 +257,9 @@ __global__ __launch_bounds__(128 * WN, WN == 4 ? 4 : 2) void gemm_kernel(GemmArg
         glds16(src[i] + (int64_t)(kc) * GBK, smem + (stage) * STAGE + (wid * PW + i) * 1024);   \
   }
 
+#ifndef GPK_ABLATE_C
+#define GPK_ABLATE_C 0  // timing-only (wrong results): 1 = the C-first update starts from zero instead of C
+#endif
 #ifndef GPK_CFIRST
 #define GPK_CFIRST 1  // f64 update: C loaded into the accumulators before the K loop (A negated)
 #endif
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(128 * WN, WN == 4 ? 4 : 2) void gemm_kernel(GemmArg
     for (int m = 0; m < MB; ++m)
 #pragma unroll
       for (int n = 0; n < NBK; ++n) {
-        if (CFIRST) {
+        if (CFIRST && GPK_ABLATE_C == 0) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[m][n][r] = BufIO<T>::load(crs, cvo, GPK_CSOFF(m, n, r));
         } else {
