@@ -652,6 +652,80 @@ int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, 
   return gpk_finalize(lay, W, info_dev, out_dev, nullptr, nullptr, stream);
 }
 
+// ------------------------------------------------------------- workspace-style convenience entries
+// The flat signatures of SURVEY §8(b): the caller hands one scratch buffer instead of a layout and
+// W / Winv; the calls carve the augmented layout out of it and run the same kernels.
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+size_t gpk_workspace_bytes(int op, int dtype, int64_t n, int64_t m, int32_t batch) {
+  (void)m;
+  gpk_layout lay;
+  if (n <= 0 || batch <= 0) return 0;
+  if (op == GPK_WS_NLML) {
+    if (gpk_plan(dtype, batch, n, 0, 1, &lay)) return 0;
+    return align256(lay.w_bytes) + align256(lay.inv_bytes) + align256((size_t)batch * 4 * sizeof(double));
+  }
+  if (op == GPK_WS_POTRF) {
+    if (dtype != GPK_F64 || gpk_plan(GPK_F64, 1, n, 0, 1, &lay)) return 0;
+    return align256(lay.w_bytes) + align256(lay.inv_bytes) + align256(8 * sizeof(double)) +
+           align256((size_t)n * sizeof(double));
+  }
+  return 0;
+}
+
+int gpk_nlml_batched(const gpk_kdesc* kd, int32_t batch, const double* hyp_dev, const double* noise_dev, int dtype,
+                     const double* X, const double* y, int64_t n, int32_t d, void* work, size_t work_bytes,
+                     double* nlml_dev, int32_t* info_dev, void* stream) {
+  if (!kd) return fail_arg(1, "kd");
+  if (batch <= 0) return fail_arg(2, "batch");
+  if (!nlml_dev) return fail_arg(12, "nlml_dev");
+  gpk_layout lay;
+  if (int e = gpk_plan(dtype, batch, n, 0, d, &lay)) return e;
+  if (!work || work_bytes < gpk_workspace_bytes(GPK_WS_NLML, dtype, n, 0, batch)) return fail_arg(11, "work_bytes");
+  char* w = reinterpret_cast<char*>(work);
+  void* W = w;
+  void* Winv = w + align256(lay.w_bytes);
+  double* out = reinterpret_cast<double*>(w + align256(lay.w_bytes) + align256(lay.inv_bytes));
+  if (int e = gpk_nlml(kd, &lay, hyp_dev, kd->n_hyp, noise_dev, 1, X, 0, y, 0, W, Winv, info_dev, out, stream))
+    return e;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(hipMemcpy2DAsync(nlml_dev, sizeof(double), out, 4 * sizeof(double), sizeof(double), (size_t)batch,
+                           hipMemcpyDeviceToDevice, s),
+          "nlml_batched read-out");
+  return 0;
+}
+
+int gpk_potrf_lower(int dtype, void* A, int64_t n, int64_t lda, void* work, size_t work_bytes, int32_t* info_dev,
+                    double* logdet_dev, void* stream) {
+  if (dtype != GPK_F64) return fail_arg(1, "dtype (gpk_potrf_lower factors fp64)");
+  if (!A) return fail_arg(2, "A");
+  if (n <= 0) return fail_arg(3, "n");
+  if (lda < n) return fail_arg(4, "lda");
+  if (!info_dev) return fail_arg(7, "info_dev");
+  gpk_layout lay;
+  if (int e = gpk_plan(GPK_F64, 1, n, 0, 1, &lay)) return e;
+  if (!work || work_bytes < gpk_workspace_bytes(GPK_WS_POTRF, GPK_F64, n, 0, 1)) return fail_arg(6, "work_bytes");
+  char* w = reinterpret_cast<char*>(work);
+  double* W = reinterpret_cast<double*>(w);
+  void* Winv = w + align256(lay.w_bytes);
+  double* out = reinterpret_cast<double*>(w + align256(lay.w_bytes) + align256(lay.inv_bytes));
+  double* zeros = reinterpret_cast<double*>(w + align256(lay.w_bytes) + align256(lay.inv_bytes) +
+                                            align256(8 * sizeof(double)));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(hipMemsetAsync(out, 0, 8 * sizeof(double), s), "potrf_lower scratch");
+  GPK_HIP(hipMemsetAsync(zeros, 0, (size_t)n * sizeof(double), s), "potrf_lower scratch");
+  GPK_HIP(hipMemsetAsync(info_dev, 0, sizeof(int32_t), s), "memset info");
+  // noise 0 (out[4] is zero), y = 0: the augmented factorisation of A alone
+  if (int e = gpk_assemble_dense(&lay, reinterpret_cast<const double*>(A), lda, 0, out + 4, 0, nullptr, 0, 0, zeros, 0,
+                                 W, stream))
+    return e;
+  if (int e = gpk_potrf_aug(&lay, W, Winv, info_dev, stream)) return e;
+  if (int e = gpk_finalize(&lay, W, info_dev, out, nullptr, nullptr, stream)) return e;
+  GPK_HIP(launch_copy_lower(W, lay.ld, reinterpret_cast<double*>(A), lda, n, s), "potrf_lower copy");
+  if (logdet_dev) GPK_HIP(hipMemcpyAsync(logdet_dev, out + 2, sizeof(double), hipMemcpyDeviceToDevice, s), "logdet");
+  return 0;
+}
+
 size_t gpk_grad_workspace_bytes(const gpk_kdesc* kd, const gpk_layout* lay) {
   if (!kd || !lay || lay->n <= 0 || lay->batch <= 0) return 0;
   const int64_t nt = (lay->n + ATILE - 1) / ATILE;

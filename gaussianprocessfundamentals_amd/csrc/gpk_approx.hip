@@ -322,7 +322,21 @@ __global__ __launch_bounds__(256) void add_diag_kernel(double* A, int64_t n, int
   if (i < n) A[(int64_t)blockIdx.y * a_bs + i * lda + i] += value;
 }
 
+__global__ __launch_bounds__(256) void copy_lower_kernel(const double* src, int64_t lds, double* dst, int64_t ldd,
+                                                         int64_t n) {
+  const int64_t i = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j <= i && j < n) dst[i * ldd + j] = src[i * lds + j];
+}
+
 }  // namespace
+
+hipError_t launch_copy_lower(const double* src, int64_t lds, double* dst, int64_t ldd, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(copy_lower_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n), dim3(256), 0, s, src, lds, dst,
+                     ldd, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_dgemm(const DgemmArgs& g, int32_t batch, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || batch <= 0) return hipSuccess;

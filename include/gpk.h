@@ -229,6 +229,29 @@ int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, 
 int gpk_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x, double* y, double alpha,
              double beta, void* stream);
 
+/* ------------------------------------------------------ workspace-style entries
+ * The flat signatures of the survey's boundary sketch: one caller scratch buffer of
+ * gpk_workspace_bytes(op, ...) bytes replaces the layout and W / Winv.  (The single-problem
+ * gpk_nlml of that sketch is gpk_nlml_batched with batch = 1; the sketch's gpk_trsv_lower and
+ * gpk_posterior are served by gpk_trsv and by the test rows of the augmented factorisation --
+ * gpk_assemble with Xs + gpk_potrf_aug + gpk_finalize(mu, var) -- see INTEGRATION.md.) */
+enum { GPK_WS_NLML = 0, GPK_WS_POTRF = 1 };
+size_t gpk_workspace_bytes(int op, int dtype, int64_t n, int64_t m, int32_t batch);
+
+/* -LML of `batch` hyperparameter / noise candidates on shared X [n, d], y [n] (device):
+ * hyp_dev [batch][kd->n_hyp], noise_dev [batch], nlml_dev [batch] (+inf where info_dev[b] != 0).
+ * LogLikelihood.get_metric for each candidate (Metrics/LogLikelihood.py:30-65). */
+int gpk_nlml_batched(const gpk_kdesc* kd, int32_t batch, const double* hyp_dev, const double* noise_dev, int dtype,
+                     const double* X, const double* y, int64_t n, int32_t d, void* work, size_t work_bytes,
+                     double* nlml_dev, int32_t* info_dev, void* stream);
+
+/* In-place lower Cholesky of a row-major fp64 A [n, lda] (upper triangle untouched, LAPACK
+ * dpotrf semantics) through the blocked MFMA factorisation: tf.linalg.cholesky of get_L_K
+ * (Statistics/CovarianceMatrix.py:247-254).  *info_dev: 0 or the first non-positive pivot
+ * (1-based); *logdet_dev (may be NULL) = 2 sum log diag L (Metrics/Metrics.py:152-154). */
+int gpk_potrf_lower(int dtype, void* A, int64_t n, int64_t lda, void* work, size_t work_bytes, int32_t* info_dev,
+                    double* logdet_dev, void* stream);
+
 /* ---------------------------------------------------------------- approximation paths (§8f.4)
  * Building blocks of the Nyström / SKC / SKI matrices of the reference
  * (Statistics/Nystroem_K.py, Metrics/SkcLogLikelihood.py, Metrics/StructuredKernelInterpolation.py);
