@@ -6,13 +6,13 @@ The reference binds ``get_alpha`` / ``get_log_determinant`` per numerical handli
   CHOLESKY_BASED (default)   alpha = L^-T L^-1 y, logdet = 2 sum log diag L     (:138-139, :152-154)
   STRICT_INVERSE             alpha = inv(K) y: K^-1 from the identity-augmented factorisation,
                              one device GEMV; logdet = slogdet(K)                (:132-133, :148-149)
-  PSEUDO_INVERSE             alpha = pinv(K) y: equal to inv(K) y for the positive-definite K the
-                             kernels produce; a K that is not positive definite (where pinv's
-                             rank truncation would matter) raises NotImplementedError (:135-136)
+  PSEUDO_INVERSE             alpha = pinv(K) y: inv(K) y for a positive-definite K; otherwise the
+                             Jacobi eigendecomposition with tf.linalg.pinv's cutoff (:135-136)
   LINEAR_CONJUGATE_GRADIENT  alpha = linear_cg(K, y, 0) (device GEMV per iteration) (:141-144)
 
-slogdet(K)[1] is log|det K| = 2 sum log diag L for a positive-definite K (the device Cholesky);
-for any other K it raises NotImplementedError (the reference's LU-based slogdet is not provided).
+slogdet(K)[1] is log|det K| = 2 sum log diag L for a positive-definite K (the device Cholesky) and
+sum log|lam_i| from the Jacobi eigenvalues otherwise; STRICT_INVERSE of an indefinite nonsingular K
+(LU in the reference) is V diag(1/lam) V^T.  The eigendecomposition fallback is limited to n <= 2048.
 Subset-of-data approximations (SOD_GRID, SOD_RANDOM) evaluate the exact path on the subset
 (:60-68).  Matrix approximations (:77-126) swap get_covariance_matrix / get_log_determinant:
 
@@ -166,21 +166,51 @@ class Metric(AbstractMetric):
         """inv(K) y (Metrics.py:132-133): the explicit inverse, then one device GEMV."""
         from .. import engine
         self._require_plain()
+        if not self._positive_definite(hyper_parameter, noise, indices):
+            # tf.linalg.inv is LU-based: an indefinite but nonsingular K is inverted, a singular one raises
+            lam, V = self._eigen(hyper_parameter, noise, indices)
+            if bool((lam == 0).any()):
+                raise engine.CholeskyError("inv: the covariance matrix is singular")
+            U, _ = engine.pinv_factor(lam, V, 0, rcond=0.0)
+            return engine.dgemm(U, engine.dgemm(V, self._y(y), trans_a=True))
         if self._approximate():
             f = self._approx_factorization(hyper_parameter, noise, indices)
-            f.check_info()
             return engine.gemv(f.k_inv(0).contiguous(), self._y(y))
         return engine.gemv(self.covariance_matrix.get_K_inv(hyper_parameter, noise).contiguous(), self._y(y))
 
-    def get_alpha_pseudo_inverse(self, hyper_parameter: List, noise, y=None, indices=None):
-        """pinv(K) y (Metrics.py:135-136) = inv(K) y for a positive-definite K (raises otherwise)."""
-        from .. import engine
-        self._require_plain()
+    # largest n for the eigendecomposition fallback of a matrix that is not positive definite (the
+    # Jacobi sweeps cost O(n^3) each with n - 1 launches per sweep)
+    EIGEN_FALLBACK_MAX_N = 2048
+
+    def _positive_definite(self, hyper_parameter: List, noise, indices=None) -> bool:
         f = (self._approx_factorization(hyper_parameter, noise, indices) if self._approximate()
              else self.covariance_matrix.factorization(hyper_parameter, noise))
-        if int(f.info.abs().max()) != 0:
-            raise NotImplementedError("pinv of a matrix that is not positive definite is not provided")
-        return self.get_alpha_strict_inverse(hyper_parameter, noise, y, indices)
+        return int(f.info.abs().max()) == 0
+
+    def _eigen(self, hyper_parameter: List, noise, indices=None):
+        """Eigendecomposition (gpk_syevj) of the covariance matrix the handling works on, for the
+        handlings' non-positive-definite cases; cached with that matrix."""
+        from .. import engine
+        K = self.get_covariance_matrix(hyper_parameter, noise, indices)
+        if getattr(self, "_eig_src", None) is not K:
+            n = K.shape[0]
+            if n > self.EIGEN_FALLBACK_MAX_N:
+                raise NotImplementedError("the covariance matrix is not positive definite and n = %d exceeds the "
+                                          "eigendecomposition fallback (n <= %d)" % (n, self.EIGEN_FALLBACK_MAX_N))
+            lam, V, _ = engine.syevj(K.contiguous())
+            self._eig, self._eig_src = (lam, V), K
+        return self._eig
+
+    def get_alpha_pseudo_inverse(self, hyper_parameter: List, noise, y=None, indices=None):
+        """pinv(K) y (Metrics.py:135-136): inv(K) y for a positive-definite K; otherwise the
+        eigendecomposition route of tf.linalg.pinv (Jacobi, cutoff 10 n eps max|lam|)."""
+        from .. import engine
+        self._require_plain()
+        if self._positive_definite(hyper_parameter, noise, indices):
+            return self.get_alpha_strict_inverse(hyper_parameter, noise, y, indices)
+        lam, V = self._eigen(hyper_parameter, noise, indices)
+        U, _ = engine.pinv_factor(lam, V, 0)
+        return engine.dgemm(U, engine.dgemm(V, self._y(y), trans_a=True))
 
     def get_alpha_lcg(self, hyper_parameter: List, noise, y=None, indices=None):
         """linear_cg(K, y, 0) (Metrics.py:141-144; Auxiliary/LinearConjugateGradients.py)."""
@@ -197,11 +227,12 @@ class Metric(AbstractMetric):
         return torch.sum(f.logdet())
 
     def get_log_determinant_slodget(self, hyper_parameter: List, noise, indices=None):
-        """slogdet(K)[1] = log|det K| (Metrics.py:146-147), from the device Cholesky for a
-        positive-definite K; other K raise NotImplementedError."""
+        """slogdet(K)[1] = log|det K| (Metrics.py:146-147): 2 sum log diag L from the device Cholesky
+        for a positive-definite K, sum log|lam_i| from the eigenvalues otherwise (-inf if singular)."""
         self._require_plain()
         f = (self._approx_factorization(hyper_parameter, noise, indices) if self._approximate()
              else self.covariance_matrix.factorization(hyper_parameter, noise))
-        if int(f.info.abs().max()) != 0:
-            raise NotImplementedError("slogdet of a matrix that is not positive definite is not provided")
-        return torch.sum(f.logdet())
+        if int(f.info.abs().max()) == 0:
+            return torch.sum(f.logdet())
+        lam, _ = self._eigen(hyper_parameter, noise, indices)
+        return torch.sum(torch.log(torch.abs(lam)))

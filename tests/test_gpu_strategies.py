@@ -97,3 +97,39 @@ def test_subset_of_data_grid_is_exact_on_the_grid_subset():
     got_r = float(r.get_metric(hyp_list([0.12]), T(NOISE)))
     assert rel(got_r, o.nlml(SE, [0.12], NOISE, sub.data_x_train.cpu().numpy(),
                               sub.data_y_train.cpu().numpy().reshape(-1))) < 1e-9
+
+
+@pytest.mark.parametrize("handling", [H.STRICT_INVERSE, H.PSEUDO_INVERSE])
+def test_handlings_of_an_indefinite_covariance(handling):
+    """K + noise I with a negative noise is indefinite: the Cholesky reports it, and STRICT_INVERSE /
+    PSEUDO_INVERSE + slogdet fall back to the Jacobi eigendecomposition, as the reference's LU-based
+    tf.linalg.inv / SVD-based pinv / slogdet handle it.  NLL rel <= 1e-8 (cond(K) ~ 1e3 here)."""
+    g, x, y, _, _ = setup(n=300)
+    noise = -0.3
+    K = o.k_noised(SE, [0.1], noise, x)
+    assert np.min(np.linalg.eigvalsh(K)) < 0
+    met = get_metric_by_type(MetricType.LL, g, numerical_matrix_handling=handling)
+    got = float(met.get_metric(hyp_list([0.1]), T(noise)).reshape(-1)[0])
+    alpha = (np.linalg.inv(K) if handling is H.STRICT_INVERSE else o.tf_pinv(K)) @ y
+    ref = o.nlml_with_alpha(alpha, y, np.linalg.slogdet(K)[1], 300)
+    assert rel(got, ref) <= 1e-8, (got, ref)
+
+
+def test_pseudo_inverse_of_a_singular_covariance():
+    """Duplicated inputs and zero noise: K is singular (rank 150 of 300), pinv truncates below
+    10 n eps max|lam| exactly like tf.linalg.pinv.  alpha compared through K alpha (= the projection
+    of y on K's range, O(1)), max-abs <= 1e-6: the kept eigenvalues reach down to the cutoff, where
+    pinv amplifies the eigensolvers' rounding differences (alpha itself is O(1e3))."""
+    rng = np.random.default_rng(3)
+    xh = np.sort(rng.uniform(0, 1, (150, 1)), axis=0)
+    x = np.concatenate([xh, xh])
+    y = np.sin(6 * x[:, 0])
+    di = DataInput(x, y.reshape(-1, 1), x[:5], y[:5].reshape(-1, 1))
+    di.set_mean_function(ZeroMeanFunction(1))
+    g = GaussianProcess(make_kernel(SE, 1), ZeroMeanFunction(1))
+    g.set_data_input(di)
+    met = get_metric_by_type(MetricType.LL, g, numerical_matrix_handling=H.PSEUDO_INVERSE)
+    alpha = met.get_alpha(hyp_list([0.5]), T(0.0), None).cpu().numpy().reshape(-1)
+    K = o.k_noised(SE, [0.5], 0.0, x)
+    ref = o.tf_pinv(K) @ y
+    assert np.max(np.abs(K @ alpha - K @ ref)) <= 1e-6
