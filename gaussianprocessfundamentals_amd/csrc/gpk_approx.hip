@@ -11,15 +11,53 @@
 namespace gpk {
 namespace {
 
+typedef double d2 __attribute__((ext_vector_type(2)));
+
 // ============================================================================================ GEMM
 // C = alpha op(A) op(B) + beta C (row-major; op(A) M x K, op(B) K x N).  64 x 64 tiles, 256 threads
-// = 2 x 2 waves of 32 x 32 (2 x 2 f64 MFMA 16x16x4 blocks), K staged 16 at a time through LDS in
-// k-major order so that a lane's operand (row lane & 15, k lane >> 4) is one conflict-free LDS read.
-constexpr int GT = 64, GKC = 16;
+// = 2 x 2 waves of 32 x 32 (2 x 2 f64 MFMA 16x16x4 blocks).  K is staged 16 at a time in LDS as
+// [row][k] (row stride 18 doubles: the 16 rows a quarter-wave reads sit on distinct banks), and the
+// MFMA k-step s of lane group q = lane >> 4 takes k = 4 q + s -- the same permutation for both
+// operands -- so two ds_read_b128 per 16-row block feed all four k-steps.  Two LDS stages; the next
+// chunk's global loads are issued before the current chunk's MFMAs (one barrier per chunk).
+constexpr int GT = 64, GKC = 16, GLD = GKC + 2;
+
+struct GemmStage {
+  double a[4], b[4];
+};
+
+__device__ __forceinline__ void dgemm_fetch(const DgemmArgs& g, const double* A, const double* B, int64_t i0,
+                                            int64_t j0, int64_t k0, int tid, GemmStage& st) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid * 4 + u;  // 1024 elements of each operand chunk
+    int ii, kk;
+    if (g.ta) { kk = e / GT; ii = e % GT; } else { ii = e / GKC; kk = e % GKC; }
+    const int64_t gi = i0 + ii, gk = k0 + kk;
+    st.a[u] = (gi < g.M && gk < g.K) ? (g.ta ? A[gk * g.lda + gi] : A[gi * g.lda + gk]) : 0.0;
+    int jj, kb;
+    if (g.tb) { jj = e / GKC; kb = e % GKC; } else { kb = e / GT; jj = e % GT; }
+    const int64_t gj = j0 + jj, gkb = k0 + kb;
+    st.b[u] = (gj < g.N && gkb < g.K) ? (g.tb ? B[gj * g.ldb + gkb] : B[gkb * g.ldb + gj]) : 0.0;
+  }
+}
+
+__device__ __forceinline__ void dgemm_store(const DgemmArgs& g, int tid, const GemmStage& st, double* As, double* Bs) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid * 4 + u;
+    int ii, kk;
+    if (g.ta) { kk = e / GT; ii = e % GT; } else { ii = e / GKC; kk = e % GKC; }
+    As[ii * GLD + kk] = st.a[u];
+    int jj, kb;
+    if (g.tb) { jj = e / GKC; kb = e % GKC; } else { kb = e / GT; jj = e % GT; }
+    Bs[jj * GLD + kb] = st.b[u];
+  }
+}
 
 __global__ __launch_bounds__(256) void dgemm_kernel(DgemmArgs g) {
-  __shared__ double As[GKC][GT + 1];
-  __shared__ double Bs[GKC][GT + 1];
+  __shared__ __attribute__((aligned(16))) double As[2][GT * GLD];
+  __shared__ __attribute__((aligned(16))) double Bs[2][GT * GLD];
   const int b = blockIdx.z;
   const int64_t i0 = (int64_t)blockIdx.y * GT, j0 = (int64_t)blockIdx.x * GT;
   const double* A = g.A + (int64_t)b * g.a_bs;
@@ -34,36 +72,36 @@ __global__ __launch_bounds__(256) void dgemm_kernel(DgemmArgs g) {
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
 
-  for (int64_t k0 = 0; k0 < g.K; k0 += GKC) {
+  GemmStage st;
+  dgemm_fetch(g, A, B, i0, j0, 0, tid, st);
+  dgemm_store(g, tid, st, As[0], Bs[0]);
+  __syncthreads();
+  const int nk = (int)((g.K + GKC - 1) / GKC);
+  for (int c = 0; c < nk; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nk) dgemm_fetch(g, A, B, i0, j0, (int64_t)(c + 1) * GKC, tid, st);
+    d2 fa[2][2], fb[2][2];
 #pragma unroll
-    for (int e = tid; e < GT * GKC; e += 256) {
-      int ii, kk;
-      if (g.ta) { kk = e / GT; ii = e % GT; } else { ii = e / GKC; kk = e % GKC; }
-      const int64_t gi = i0 + ii, gk = k0 + kk;
-      double v = 0.0;
-      if (gi < g.M && gk < g.K) v = g.ta ? A[gk * g.lda + gi] : A[gi * g.lda + gk];
-      As[kk][ii] = v;
-      int jj, kb;
-      if (g.tb) { jj = e / GKC; kb = e % GKC; } else { kb = e / GT; jj = e % GT; }
-      const int64_t gj = j0 + jj, gkb = k0 + kb;
-      double u = 0.0;
-      if (gj < g.N && gkb < g.K) u = g.tb ? B[gj * g.ldb + gkb] : B[gkb * g.ldb + gj];
-      Bs[kb][jj] = u;
+    for (int mi = 0; mi < 2; ++mi) {
+      const d2* src = reinterpret_cast<const d2*>(&As[cur][(wr * 32 + mi * 16 + lr) * GLD + 4 * q]);
+      fa[mi][0] = src[0];
+      fa[mi][1] = src[1];
     }
-    __syncthreads();
 #pragma unroll
-    for (int s = 0; s < GKC / 4; ++s) {
-      double fa[2], fb[2];
+    for (int ni = 0; ni < 2; ++ni) {
+      const d2* src = reinterpret_cast<const d2*>(&Bs[cur][(wc * 32 + ni * 16 + lr) * GLD + 4 * q]);
+      fb[ni][0] = src[0];
+      fb[ni][1] = src[1];
+    }
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) fa[mi] = As[4 * s + q][wr * 32 + mi * 16 + lr];
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) fb[ni] = Bs[4 * s + q][wc * 32 + ni * 16 + lr];
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
-    }
+          acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[mi][s >> 1][s & 1], fb[ni][s >> 1][s & 1],
+                                                             acc[mi][ni], 0, 0, 0);
+    if (c + 1 < nk) dgemm_store(g, tid, st, As[cur ^ 1], Bs[cur ^ 1]);
     __syncthreads();
   }
 #pragma unroll
