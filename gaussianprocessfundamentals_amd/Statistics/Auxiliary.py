@@ -162,4 +162,20 @@ class BlockwiseAuxiliaryGpProperties(HolisticAuxiliaryGpProperties):
         return torch.diagonal(self.get_posterior_var(hyper_parameter, noise)).clone()
 
     def get_inverse_cholesky_k_times_k_s(self, hyper_parameter: List, noise):
-        raise NotImplementedError("inv(L) K_s of a segmented GP: use get_posterior_var (block-diagonal)")
+        """inv(L) K_s over a SegmentedCovarianceMatrix (Auxiliary.py:57-66 inherited): block-diagonal
+        [sum n_i, sum m_i] of the segments' V_i = L_i^-1 K_s,i, read (transposed) from the extra rows of
+        the one ragged factorisation; a segment without training (test) points has an n_i x 0
+        (0 x m_i) block."""
+        if self.data_input is None:
+            return None
+        if self.inv_L_K_dot_K_s is None:
+            f, index = self._segments(hyper_parameter, noise)
+            blocks = []
+            for i, di in enumerate(self.data_input.data_inputs):
+                if i in index:
+                    blocks.append(f.extra_rows(index.index(i)).to(torch.float64).transpose(0, 1))
+                else:
+                    blocks.append(torch.zeros((int(di.n_train), int(di.n_test)), dtype=torch.float64,
+                                              device=engine.device()))
+            self.inv_L_K_dot_K_s = torch.block_diag(*blocks).contiguous()
+        return self.inv_L_K_dot_K_s

@@ -250,6 +250,12 @@ def test_segmented_covariance_matrix_getters():
     assert np.max(np.abs(var - block_diag(*[p[1] for p in post]))) < 1e-8
     full, mean_mu, post_mu = g.predict(hyp, noise=nz)
     assert np.max(np.abs(post_mu.cpu().numpy() - np.concatenate([p[0] for p in post]))) < 1e-8
+    # inv(L) K_s: block-diagonal of the segments' L_i^-1 K_s,i (Auxiliary.py:57-66 over the segments)
+    Vs = [np.linalg.solve(L, o.kernel_matrix(t, h, s[0], s[2])) for L, t, h, s in zip(Ls, CHILD_TREES, CHILD_HYPS, segs)]
+    g.aux.reset()
+    V = g.aux.get_inverse_cholesky_k_times_k_s(hyp, nz).cpu().numpy()
+    assert V.shape == (sum(v.shape[0] for v in Vs), sum(v.shape[1] for v in Vs))
+    assert np.max(np.abs(V - block_diag(*Vs))) < 1e-8
 
 
 def test_partitioned_gp_predict_and_empty_training_segment():
