@@ -176,8 +176,6 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
     def _inverse_factorization(self, hyper_parameter, noise):
         """Augment with identity rows: extra rows -> L^-T, corner -> -K^-1 (one factorisation)."""
         self._require_data()
-        if self.data_input.data_x_train.dim() == 3:
-            raise NotImplementedError("explicit inverses are not provided for BatchDataInput")
         if self._inv_fact is None:
             self._inv_fact = self.inverse_factorization(hyper_parameter, noise, gradient=False)
             self._inv_fact.check_info()
@@ -206,14 +204,20 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
         the augmented matrix come out as L^-T."""
         if self.L_inv_K is None:
             f = self._inverse_factorization(hyper_parameter, noise)
-            self.L_inv_K = f.l_inv(0).to(torch.float64).contiguous()
+            if self.data_input.data_x_train.dim() == 3:   # BatchDataInput: [B, N, N]
+                self.L_inv_K = torch.stack([f.l_inv(b).to(torch.float64) for b in range(f.batch)])
+            else:
+                self.L_inv_K = f.l_inv(0).to(torch.float64).contiguous()
         return self.L_inv_K
 
     def get_K_inv(self, hyper_parameter: List, noise) -> torch.Tensor:
         """inv(K + noise I) (CovarianceMatrix.py:208-216) from the Schur complement corner."""
         if self.K_inv is None:
             f = self._inverse_factorization(hyper_parameter, noise)
-            self.K_inv = f.k_inv(0).to(torch.float64)
+            if self.data_input.data_x_train.dim() == 3:   # BatchDataInput: [B, N, N]
+                self.K_inv = torch.stack([f.k_inv(b).to(torch.float64) for b in range(f.batch)])
+            else:
+                self.K_inv = f.k_inv(0).to(torch.float64)
         return self.K_inv
 
     def get_K_s(self, hyper_parameter: List) -> torch.Tensor:

@@ -418,3 +418,25 @@ def test_schedule_variants_match_oracle(group, group_first, lookahead):
         nat.tune("group", old_g)
         nat.tune("group_first", old_f)
         nat.tune("lookahead", old_l)
+
+
+def test_batch_explicit_inverses():
+    """get_K_inv / get_L_inv_K of a BatchDataInput: one identity-augmented batched factorisation,
+    [B, N, N] (tf.linalg.inv / inv(L) broadcast over the batch, CovarianceMatrix.py:208-216, :267-275).
+    Tolerance max-abs <= 1e-9 relative to the largest entry."""
+    rng = np.random.default_rng(12)
+    B, n = 3, 200
+    x = np.sort(rng.uniform(0, 1, (B, n, 1)), axis=1)
+    y = np.sin(5 * x[..., 0])
+    g = build_gp(SE, x, y, x[:, :10], y[:, :10, None])
+    cm = g.covariance_matrix
+    nz = torch.tensor(1e-2, dtype=torch.float64)
+    kinv = cm.get_K_inv(hyp_list([0.2]), nz).cpu().numpy()
+    linv = cm.get_L_inv_K(hyp_list([0.2]), nz).cpu().numpy()
+    assert kinv.shape == (B, n, n) and linv.shape == (B, n, n)
+    for b in range(B):
+        K = o.k_noised(SE, [0.2], 1e-2, x[b])
+        ref = np.linalg.inv(K)
+        assert np.max(np.abs(kinv[b] - ref)) <= 1e-9 * np.max(np.abs(ref))
+        Lref = np.linalg.inv(np.linalg.cholesky(K))
+        assert np.max(np.abs(linv[b] - Lref)) <= 1e-9 * np.max(np.abs(Lref))
