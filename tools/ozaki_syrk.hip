@@ -7,7 +7,7 @@
 // (v_mfma_i32_16x16x64_i8); the pairs of one d share one int32 accumulator (|sum| <= S K 64^2 < 2^31),
 // converted to fp64 once per d.  Operands are read straight from global memory (L2): no LDS staging.
 //
-// build+run (GPU box): hipcc --offload-arch=gfx950 -O3 tools/ozaki_syrk.hip -o /tmp/oz && /tmp/oz [rows] [S]
+// build+run (GPU box): hipcc --offload-arch=gfx950 -O3 tools/ozaki_syrk.hip -o /tmp/oz && /tmp/oz [rows] [S] [staged 0/1]
 // Prints the max relative error of sampled tiles against an fp64 host product and the emulated
 // rate (2 K x lower elements / kernel time, the f64 update's algorithmic count).
 #include <hip/hip_runtime.h>
@@ -108,6 +108,69 @@ __global__ __launch_bounds__(512) void syrk_i8(const signed char* Q, const doubl
       }
 }
 
+// LDS-staged variant: per 64-byte K chunk the (d + 1) slices of the tile's A rows and B rows needed by
+// the digit pairs of d are staged once (row stride 80 B: a quarter-wave's 16-B reads hit distinct banks)
+// and shared by the 8 waves; one workgroup per CU at S = 6 (123 KB of LDS).
+constexpr int RS = 80;  // LDS row stride (bytes)
+
+__global__ __launch_bounds__(512) void syrk_i8_lds(const signed char* Q, const double* sc, int rows, int S, double* C) {
+  extern __shared__ __attribute__((aligned(16))) signed char lds[];
+  signed char* La = lds;                          // [S][128][RS]
+  signed char* Lb = lds + (size_t)S * 128 * RS;   // [S][128][RS]
+  const int t = blockIdx.x;
+  int ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while (ti * (ti + 1) / 2 > t) --ti;
+  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+  const int tj = t - ti * (ti + 1) / 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int lr = lane & 15, q = lane >> 4;
+  const int lrow = tid >> 2, lpc = tid & 3;  // loader: row 0..127, 16-B piece 0..3
+  d4 accd[4][2];
+  for (int m = 0; m < 4; ++m)
+    for (int n = 0; n < 2; ++n) accd[m][n] = d4{0, 0, 0, 0};
+  for (int d = 0; d < S; ++d) {
+    i4 acci[4][2];
+    for (int m = 0; m < 4; ++m)
+      for (int n = 0; n < 2; ++n) acci[m][n] = i4{0, 0, 0, 0};
+    for (int k0 = 0; k0 < KD; k0 += 64) {
+      for (int s = 0; s <= d; ++s) {
+        const signed char* qa = Q + ((size_t)s * rows + ti * 128 + lrow) * KD + k0 + 16 * lpc;
+        const signed char* qb = Q + ((size_t)s * rows + tj * 128 + lrow) * KD + k0 + 16 * lpc;
+        *reinterpret_cast<i4*>(La + ((size_t)s * 128 + lrow) * RS + 16 * lpc) = *reinterpret_cast<const i4*>(qa);
+        *reinterpret_cast<i4*>(Lb + ((size_t)s * 128 + lrow) * RS + 16 * lpc) = *reinterpret_cast<const i4*>(qb);
+      }
+      __syncthreads();
+      for (int s = 0; s <= d; ++s) {
+        const int tt = d - s;
+        i4 fa[4], fb[2];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          fa[m] = *reinterpret_cast<const i4*>(La + ((size_t)s * 128 + wr * 64 + m * 16 + lr) * RS + 16 * q);
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          fb[n] = *reinterpret_cast<const i4*>(Lb + ((size_t)tt * 128 + wc * 32 + n * 16 + lr) * RS + 16 * q);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) acci[m][n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[m], fb[n], acci[m][n], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+    const double f = ldexp(1.0, -7 * (d + 2));
+    for (int m = 0; m < 4; ++m)
+      for (int n = 0; n < 2; ++n)
+        for (int r = 0; r < 4; ++r) accd[m][n][r] += f * (double)acci[m][n][r];
+  }
+  for (int m = 0; m < 4; ++m)
+    for (int n = 0; n < 2; ++n)
+      for (int r = 0; r < 4; ++r) {
+        const int gi = ti * 128 + wr * 64 + m * 16 + 4 * q + r;
+        const int gj = tj * 128 + wc * 32 + n * 16 + lr;
+        C[(size_t)gi * rows + gj] = sc[gi] * sc[gj] * accd[m][n][r];
+      }
+}
+
 int main(int argc, char** argv) {
   const int rows = argc > 1 ? atoi(argv[1]) : 4096;
   const int S = argc > 2 ? atoi(argv[2]) : 6;
@@ -133,12 +196,24 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   CHECK(hipEventCreate(&e2));
+  const bool staged = argc > 3 && atoi(argv[3]) == 1;
+  const size_t lds = (size_t)2 * S * 128 * RS;
+  if (staged)
+    CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(syrk_i8_lds), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds));
+  auto syrk = [&]() {
+    if (staged)
+      hipLaunchKernelGGL(syrk_i8_lds, dim3(tiles), dim3(512), lds, 0, dQ, dsc, rows, S, dC);
+    else
+      hipLaunchKernelGGL(syrk_i8, dim3(tiles), dim3(512), 0, 0, dQ, dsc, rows, S, dC);
+  };
   hipLaunchKernelGGL(slice_rows, dim3(rows), dim3(256), 0, 0, dP, rows, S, dQ, dsc);
-  hipLaunchKernelGGL(syrk_i8, dim3(tiles), dim3(512), 0, 0, dQ, dsc, rows, S, dC);  // warm
+  syrk();  // warm
+  CHECK(hipGetLastError());
   CHECK(hipEventRecord(e0));
   hipLaunchKernelGGL(slice_rows, dim3(rows), dim3(256), 0, 0, dP, rows, S, dQ, dsc);
   CHECK(hipEventRecord(e1));
-  hipLaunchKernelGGL(syrk_i8, dim3(tiles), dim3(512), 0, 0, dQ, dsc, rows, S, dC);
+  syrk();
   CHECK(hipEventRecord(e2));
   CHECK(hipEventSynchronize(e2));
   float ms_slice, ms_syrk;
@@ -163,9 +238,9 @@ int main(int argc, char** argv) {
       }
   }
   const double lower = (double)tiles * 128.0 * 128.0;
-  printf("rows %d K %d S %d (int8 GEMMs %d): max err / sum|p p| %.3e; slice %.3f ms, emulated syrk %.3f ms = %.1f TF/s "
+  printf("%s rows %d K %d S %d (int8 GEMMs %d): max err / sum|p p| %.3e; slice %.3f ms, emulated syrk %.3f ms = %.1f TF/s "
          "fp64-equivalent (%.0f int8 TOP/s issued)\n",
-         rows, KD, S, S * (S + 1) / 2, worst, ms_slice, ms_syrk, 2.0 * KD * lower / (ms_syrk * 1e-3) / 1e12,
+         staged ? "lds " : "l2  ", rows, KD, S, S * (S + 1) / 2, worst, ms_slice, ms_syrk, 2.0 * KD * lower / (ms_syrk * 1e-3) / 1e12,
          2.0 * KD * lower * (S * (S + 1) / 2) / (ms_syrk * 1e-3) / 1e12);
   return worst < 1e-10 || S < 5 ? 0 : 3;
 }
