@@ -153,7 +153,7 @@ __device__ __forceinline__ double kbuild_value(const FastNode& fn, const double*
 }
 
 template <typename T, int MODE, int TM, int TN, int WN, int KB = 0>
-__global__ __launch_bounds__(128 * WN, WN == 4 ? 4 : 2) void gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2) void gemm_kernel(GemmArgs a) {
   constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B piece
   constexpr int GBK = ROWB / (int)sizeof(T); // K depth per stage (16 f64, 32 f32)
   constexpr int KS = GBK / 4;                // MFMA k-steps per stage
@@ -564,6 +564,10 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 
 }  // namespace
 
+#ifndef GPK_TRSM_WN
+#define GPK_TRSM_WN 2  // waves along N of the f64 128-tile TRSM (4: the update's 8-wave 64 x 32 layout)
+#endif
+
 hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s) {
   if (a.kbuild) {  // first trailing update with the fused K build (SE / MAT32 / MAT52 nodes)
     if (mode != GEMM_UPDATE || dtype != GPK_F64) return hipErrorInvalidValue;
@@ -585,7 +589,7 @@ hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t
     if (mode == GEMM_UPDATE)
       return tile == 128 ? launch_gemm_t<double, GEMM_UPDATE, 128, 128, GPK_UPD_WN>(a, batch, s)
                          : launch_gemm_t<double, GEMM_UPDATE, 64, 64>(a, batch, s);
-    return tile == 128 ? launch_gemm_t<double, GEMM_TRSM, 128, 128>(a, batch, s)
+    return tile == 128 ? launch_gemm_t<double, GEMM_TRSM, 128, 128, GPK_TRSM_WN>(a, batch, s)
                        : launch_gemm_t<double, GEMM_TRSM, 64, 128>(a, batch, s);
   }
   if (mode == GEMM_UPDATE)
