@@ -66,6 +66,10 @@ class LogLikelihood(AbstractLogLikelihood):
     def _get_metric_by_strategy(self, hyper_parameter: List, noise, indices=None) -> torch.Tensor:
         """The reference's formula with the bound get_alpha / get_log_determinant (LogLikelihood.py:36-49)
         for the STRICT / PSEUDO inverse and linear-CG handlings."""
+        H = mht.NumericalMatrixHandlingType
+        if (self.data_input.data_x_train.dim() == 3 and self.local_approx is mht.MatrixApproximations.NONE
+                and self.numerical_matrix_handling in (H.STRICT_INVERSE, H.PSEUDO_INVERSE)):
+            return self._batch_inverse_metric(hyper_parameter, noise)
         y = self.data_input.get_detrended_y_train().reshape(-1, 1).to(torch.float64)
         alpha = self.get_alpha(hyper_parameter, noise, y, indices).reshape(-1, 1)
         fit = torch.sum(y * alpha)
@@ -78,6 +82,27 @@ class LogLikelihood(AbstractLogLikelihood):
                 torch.diagonal(self.covariance_matrix.get_K(hyper_parameter))
             ll = ll - (1.0 / (2.0 * float(global_param.p_cov_matrix_jitter))) * torch.sum(diff)
         return -ll.reshape(1, 1)
+
+    def _batch_inverse_metric(self, hyper_parameter: List, noise) -> torch.Tensor:
+        """STRICT / PSEUDO inverse over a BatchDataInput.  In the reference the data fit is [B, 1, 1]
+        (one y^T alpha per member) and slogdet gives [B], so their sum broadcasts to [B, 1, B] before
+        p_batch_metric_aggregator reduces it (LogLikelihood.py:39-63) -- with the default mean: the
+        mean data fit plus the MEAN log-determinant (the Cholesky path sums the log-determinants, Q7).
+        K^-1 of every member comes from one batched identity-augmented factorisation; members must be
+        positive definite (pinv = inv there)."""
+        from .. import engine
+        cm = self.covariance_matrix
+        f = cm._inverse_factorization(hyper_parameter, noise)
+        y = self.data_input.get_detrended_y_train().to(torch.float64)
+        B = f.batch
+        yb = y.reshape(B, -1)
+        fit = torch.stack([torch.dot(yb[b], engine.gemv(f.k_inv(b).contiguous(), yb[b].contiguous()))
+                           for b in range(B)])
+        logdet = f.logdet()
+        n = float(self.data_input.n_train)
+        T = (-0.5 * fit).reshape(B, 1, 1) + (-0.5 * logdet).reshape(1, 1, B) + (-0.5 * (n * LOG_2PI))
+        agg = global_param.p_batch_metric_aggregator or torch.mean
+        return -agg(T)
 
     def get_metric_and_gradient(self, hyper_parameter: List, noise, reset: bool = True):
         """(-LML [1, 1], [d(-LML)/d h for h in hyper_parameter] (each shaped like h), d(-LML)/d noise).
