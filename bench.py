@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events")
     ap.add_argument("--roofline-steps", type=int, default=3, help="steps of the look-ahead-off roofline pass")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the multi-GPU code path (RCCL process group, per-step all-gather, barriers, MAX "
+                         "over ranks) even at world size 1: the rehearsal of the N > 1 bench on a 1-GPU box")
     return ap.parse_args()
 
 
@@ -182,7 +185,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        if world == 1:  # no launcher: a one-rank group of our own (127.0.0.1 rendezvous)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import gaussianprocessfundamentals_amd.global_parameters as gp
@@ -235,7 +244,7 @@ def main():
     # --pipeline P: P factorisation buffers on P streams, consecutive steps round-robin over them,
     # so that one batch's exposed panel chain (start and tail of the factorisation) overlaps the
     # trailing updates of the next (the batches are independent candidate sets of the sweep)
-    P = max(1, args.pipeline if args.pipeline is not None else (3 if world == 1 else 2))
+    P = max(1, args.pipeline if args.pipeline is not None else (2 if use_dist else 3))
     la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 1)
     nat.tune("lookahead", la)
     if grad_mode:
@@ -245,7 +254,7 @@ def main():
     fact = facts[0]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(P - 1)]
     step_no = [0]
-    gathered = [torch.empty(2 * chunk * world, dtype=torch.float64, device=dev) if world > 1 else None
+    gathered = [torch.empty(2 * chunk * world, dtype=torch.float64, device=dev) if use_dist else None
                 for _ in range(P)]
     mine = [torch.full((2 * chunk,), float("nan"), dtype=torch.float64, device=dev) for _ in range(P)]
 
@@ -258,7 +267,7 @@ def main():
                 f.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0, gradient=True)
             else:
                 f.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
-            if world > 1:
+            if use_dist:
                 mine[i][:batch] = f.nlml()
                 mine[i][chunk:chunk + batch] = f.info.to(torch.float64)
                 dist.all_gather_into_tensor(gathered[i], mine[i])
@@ -267,7 +276,7 @@ def main():
         step()
     torch.cuda.synchronize()
     # timed region: no per-launch HIP events (they would add a marker packet to every launch)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -275,10 +284,10 @@ def main():
         step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     el = t1 - t0
-    if world > 1:
+    if use_dist:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
@@ -311,6 +320,15 @@ def main():
         nat.tune("lookahead", old_la)
     nl = float(fact.nlml()[0].item())
     info = int(fact.info.abs().max().item())
+    gathered_ok = None
+    if use_dist:
+        # one more step on slot 0: every rank's (nlml, info) pairs must have arrived through RCCL
+        step(slot=0)
+        torch.cuda.synchronize()
+        g = gathered[0].view(world, 2 * chunk).cpu()
+        total = len(c4_candidates()) if sweep else world * batch
+        vals = g[:, :chunk].reshape(-1)
+        gathered_ok = bool(int(torch.isfinite(vals).sum()) == total and float(g[:, chunk:].nan_to_num(0).abs().max()) == 0.0)
 
     if rank == 0:
         evals = args.steps * (len(c4_candidates()) if sweep else world * batch)
@@ -377,12 +395,12 @@ def main():
             "lml_tflops": round(f_lml * value / 1e12, 3),
             "lml_frac_of_peak": round(f_lml * value / 1e12 / PEAK[dtn], 4),
             "kernel_ms_per_step": breakdown,
-            "check": {"nlml": nl, "info": info},
+            "check": {"nlml": nl, "info": info, **({"allgather_ok": gathered_ok} if use_dist else {})},
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
