@@ -57,8 +57,7 @@ def parse():
                          "(default: %d for the metric config, 1 otherwise)" % DEFAULT_BATCH)
     ap.add_argument("--pipeline", type=int, default=None,
                     help="factorisation buffers / streams that consecutive steps rotate over (overlap of batches); "
-                         "default 3 on one GPU, 2 with --gpus > 1 (RCCL's stream then keeps the process within "
-                         "GPU_MAX_HW_QUEUES = 4 hardware queues)")
+                         "default 3")
     ap.add_argument("--lookahead", type=int, default=None,
                     help="panel look-ahead on side streams (default: on, off when --pipeline > 1)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
@@ -176,8 +175,19 @@ def cpu_baseline(cfg_name, n, budget_s):
                       "1-thread evaluation (%.1f s)" % (len(times), cfg_name, n, threads, blas, cpu_model, t1)}
 
 
+# Hardware queues per process: HIP multiplexes streams onto GPU_MAX_HW_QUEUES in-order hardware queues
+# (4 by default). P pipelined factorisation streams + torch's default stream + RCCL's stream exceed 4,
+# and two streams sharing a queue serialise: the all-gather of one batch then waits behind another
+# batch's updates. Measured with the RCCL path on (--dist, N = 8192, P = 3): 321.7 evals/s with 4
+# queues, 338.1 with 8 (P = 2: 302.1 / 329.5); without RCCL 8 queues change nothing (339.0 vs 339.5).
+HW_QUEUES = 8
+
+
 def main():
     args = parse()
+    # before the first HIP call of the process (torch initialises HIP lazily)
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
     import torch
     import torch.distributed as dist
 
@@ -244,7 +254,7 @@ def main():
     # --pipeline P: P factorisation buffers on P streams, consecutive steps round-robin over them,
     # so that one batch's exposed panel chain (start and tail of the factorisation) overlaps the
     # trailing updates of the next (the batches are independent candidate sets of the sweep)
-    P = max(1, args.pipeline if args.pipeline is not None else (2 if use_dist else 3))
+    P = max(1, args.pipeline if args.pipeline is not None else 3)
     la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 1)
     nat.tune("lookahead", la)
     if grad_mode:
