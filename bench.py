@@ -180,13 +180,13 @@ def cpu_baseline(cfg_name, n, budget_s):
 # and two streams sharing a queue serialise: the all-gather of one batch then waits behind another
 # batch's updates. Measured with the RCCL path on (--dist, N = 8192, P = 3): 321.7 evals/s with 4
 # queues, 338.1 with 8 (P = 2: 302.1 / 329.5); without RCCL 8 queues change nothing (339.0 vs 339.5).
-HW_QUEUES = 8
+HW_QUEUES = int(os.environ.get("GPK_BENCH_HW_QUEUES", "8"))  # 0: leave the runtime default
 
 
 def main():
     args = parse()
     # before the first HIP call of the process (torch initialises HIP lazily)
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES:
+    if HW_QUEUES and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES:
         os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
     import torch
     import torch.distributed as dist
