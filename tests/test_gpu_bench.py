@@ -1,0 +1,51 @@
+"""bench.py's multi-GPU code path at world size 1 (`--dist`: RCCL process group, per-step
+all-gather of every rank's (nlml, info), barriers, MAX over ranks) and its JSON contract, run as a
+child process at small N.  The reported nlml of the first candidate is checked against the oracle
+(rel <= 1e-9, the C2 tolerance of SURVEY §8d)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from oracle import gp_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(*args, timeout=100):
+    env = dict(os.environ)
+    env.setdefault("MASTER_PORT", "29563")
+    cp = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+                        capture_output=True, text=True, timeout=timeout)
+    assert cp.returncode == 0, cp.stdout[-2000:] + cp.stderr[-4000:]
+    lines = [l for l in cp.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, cp.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_dist_rehearsal_metric():
+    n = 1024
+    d = run_bench("--dist", "--n", str(n), "--batch", "4", "--steps", "2", "--warmup", "1",
+                  "--roofline-steps", "1", "--no-cpu-baseline")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["scaling"] == "weak" and d["dtype"] == "f64"
+    assert d["value"] > 0 and d["config"]["batches_in_flight"] == 3
+    assert d["check"]["info"] == 0 and d["check"]["allgather_ok"] is True
+    r = d["roofline"]
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1.0
+    x, y = o.make_inputs("metric", n=n)
+    exp = o.nlml(("SE", {}), [0.1], 1e-2, x, y)
+    assert abs(d["check"]["nlml"] - exp) <= 1e-9 * abs(exp)
+
+
+def test_bench_dist_rehearsal_sweep():
+    d = run_bench("--dist", "--config", "C4", "--n", "512", "--steps", "1", "--warmup", "1",
+                  "--roofline-steps", "1", "--no-cpu-baseline")
+    assert d["scaling"] == "strong" and d["config"]["candidates_per_rank_step"] == 128
+    assert d["check"]["info"] == 0 and d["check"]["allgather_ok"] is True
