@@ -10,6 +10,9 @@ from __future__ import annotations
 import logging
 from typing import List, Tuple
 
+import torch
+
+from .. import engine
 from .. import global_parameters as global_param
 from . import Auxiliary as ax
 from . import CovarianceMatrix as cm
@@ -71,6 +74,33 @@ class AbstractGaussianProcess:
         else:
             post_mu = self.aux.get_posterior_mu(kernel_hyper_param, noise)
         return mean_mu + post_mu, mean_mu, post_mu
+
+    def get_n_prior_functions(self, n: int, hyper_param, noise, generator=None):
+        """n prior function draws at the test points, [n_test, n] (GaussianProcess.py:87-95):
+        L_K_ss N, N ~ normal(mean(y_train), std(y_train)) -- the reference's draw, whose mean and
+        spread come from the training targets (np.mean / np.std, population std), not N(0, 1).
+        L_K_ss is the device Cholesky of K_ss + noise I, the product the f64 MFMA dgemm;
+        ``generator`` (a torch.Generator on the device) only makes the draw reproducible."""
+        L = self.covariance_matrix.get_L_K_ss(hyper_param, noise)
+        y = engine.as_device_f64(self.data_input.data_y_train)
+        z = torch.randn((int(L.shape[0]), int(n)), dtype=torch.float64, device=L.device, generator=generator)
+        z = z * torch.std(y, unbiased=False) + torch.mean(y)
+        return engine.dgemm(L.contiguous(), z)
+
+    def get_n_posterior_functions(self, n: int, hyper_param, noise, generator=None):
+        """n posterior function draws, [n_test, n] (GaussianProcess.py:97-110): mu + chol(Sigma +
+        p_cov_matrix_jitter I) N(0, 1), Sigma the full posterior covariance (Auxiliary.py:83-93),
+        its Cholesky on the device (DenseFactorization; CholeskyError if Sigma + jitter I is not PD,
+        where the reference's tf.linalg.cholesky raises InvalidArgumentError)."""
+        sigma = self.aux.get_posterior_var(hyper_param, noise).to(torch.float64).contiguous()
+        m = int(sigma.shape[0])
+        f = engine.DenseFactorization(m)
+        f.run(sigma, float(torch.as_tensor(global_param.p_cov_matrix_jitter)))
+        f.check_info()
+        L = f.cholesky(0).to(torch.float64).contiguous()
+        z = torch.randn((m, int(n)), dtype=torch.float64, device=L.device, generator=generator)
+        mu = self.aux.get_posterior_mu(hyper_param, noise).to(torch.float64).reshape(-1, 1)
+        return engine.dgemm(L, z, beta=1.0, C=mu.expand(m, int(n)).contiguous())
 
     def copy(self):
         raise NotImplementedError

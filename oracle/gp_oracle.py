@@ -249,6 +249,23 @@ def posterior(tree, hyp, noise, x, y, xs, scaled=False, se_expanded=False):
     return mu, var
 
 
+def n_prior_functions(tree, hyp, noise, xs, y_train, z, scaled=False, se_expanded=False):
+    """get_n_prior_functions (S/GaussianProcess.py:87-95) for a given standard-normal draw z
+    [M, n]: L_K_ss (z std(y) + mean(y)), L_K_ss = chol(K_ss + noise I) (S/CovarianceMatrix.py:238-245),
+    mean / population std of the training targets (np.mean / np.std, :90-92)."""
+    y = np.asarray(y_train, dtype=np.float64).reshape(-1)
+    L = cholesky_lower(k_noised(tree, hyp, noise, xs, scaled, se_expanded))
+    return L @ (np.asarray(z, dtype=np.float64) * np.std(y) + np.mean(y))
+
+
+def n_posterior_functions(tree, hyp, noise, x, y, xs, z, jitter, scaled=False, se_expanded=False):
+    """get_n_posterior_functions (S/GaussianProcess.py:97-110) for a given standard-normal draw
+    z [M, n]: mu + chol(Sigma + jitter I) z, (mu, Sigma) from :func:`posterior`."""
+    mu, var = posterior(tree, hyp, noise, x, y, xs, scaled, se_expanded)
+    L = cholesky_lower(var + jitter * np.eye(var.shape[0]))
+    return mu.reshape(-1, 1) + L @ np.asarray(z, dtype=np.float64)
+
+
 # ---------------------------------------------------------------- segmented models (SURVEY §8f.2-3)
 def cp_indicator(x, cp, mode: str = "INDICATOR"):
     """Change-point masks of ChangePointOperator (K/Operators.py:379-408) on 1-D inputs:

@@ -115,3 +115,16 @@ def test_vsgd_step_burnin_cap():
     big = np.array([[1e6]])            # 2 / (0.05 * 0.9025 g^2) < 1e-6: the adaptive rate wins
     lr = 2.0 / (0.05 * (0.95e6) ** 2)
     assert np.allclose(o.vsgd_step(np.ones((1, 1)), big), 1 - lr * 1e6)
+
+
+def test_function_draw_restatements():
+    # prior draw with z = I and standardised targets is L itself: L L^T = K_ss + noise I
+    xt = np.linspace(0.0, 1.0, 9).reshape(9, 1)
+    y = np.array([-1.0, 1.0])  # mean 0, population std 1
+    L = o.n_prior_functions(SE, [0.2], 1e-2, xt, y, np.eye(9))
+    assert np.allclose(L @ L.T, o.k_noised(SE, [0.2], 1e-2, xt), atol=1e-14)
+    # posterior draw with z = 0 is the posterior mean
+    x, yy = o.make_inputs("C1", n=64)
+    mu, _ = o.posterior(SE, [0.1], 1e-2, x, yy, xt)
+    f = o.n_posterior_functions(SE, [0.1], 1e-2, x, yy, xt, np.zeros((9, 2)), 1e-8)
+    assert np.array_equal(f, np.repeat(mu.reshape(-1, 1), 2, axis=1))
