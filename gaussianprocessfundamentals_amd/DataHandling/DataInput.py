@@ -33,6 +33,31 @@ def _f64(x) -> torch.Tensor:
     return t.to(device=_dev(), dtype=torch.float64)
 
 
+def is_equidistant(input_vector) -> bool:
+    """Consecutive differences within 1 / (100 len) of their mean (DataInput.py:17-23), over every
+    element of the [N, D] array (numpy's flat mean / max / min)."""
+    v = _f64(input_vector)
+    diff = v[:len(v) - 1] - v[1:]
+    mean = torch.mean(diff)
+    allowed_error = 1 / (100 * len(v))
+    return bool(torch.abs(torch.max(diff) - mean) < allowed_error) and \
+        bool(torch.abs(torch.min(diff) - mean) < allowed_error)
+
+
+def is_equidistant_batch(input_data) -> torch.Tensor:
+    """BatchDataInput.py:14-21 as written: the mean over the BATCH axis [N-1, D] against the per-member
+    max / min over the points [B, D] (the two broadcast only when B or N - 1 is 1 or they are equal,
+    as in TensorFlow); returns the boolean tensor."""
+    x = _f64(input_data)
+    length = x.shape[1]
+    diff = x[:, :length - 1, :] - x[:, 1:, :]
+    mean = torch.mean(diff, dim=0)
+    diff_max = torch.abs(torch.max(diff, dim=1).values - mean)
+    diff_min = torch.abs(torch.min(diff, dim=1).values - mean)
+    allowed_error = 1 / (100 * length)
+    return torch.logical_and(diff_max < allowed_error, diff_min < allowed_error)
+
+
 class AbstractDataInput:
     def __init__(self, data_x_train, data_y_train, data_x_test=None, data_y_test=None,
                  test_ratio: float = -1, seed: int = 3061941):
@@ -125,6 +150,19 @@ class AbstractDataInput:
             self.detrended_y_test = self._detrend(self.data_x_test, self.data_y_test)
         return self.detrended_y_test
 
+    def get_detrended_y_test_individual(self, data_x_test, data_y_test) -> torch.Tensor:
+        """Detrended targets of a caller-given test set (DataInput.py:108-124): y itself (fp64) for the
+        zero mean, else y - m(X) with the mean function's last hyperparameters; not memoised."""
+        y = _f64(data_y_test)
+        if isinstance(self.mean_function, bmf.ZeroMeanFunction):
+            return y
+        mf = self.mean_function
+        return y - mf.get_tf_tensor(mf.get_last_hyper_parameter(), _f64(data_x_test)).reshape(-1, 1)
+
+    def get_independent_smoothed_grid_subset(self, subset_size: int, smoothing_kernel=None):
+        """Declared without a body in the reference (AbstractDataInput.py:138-139): None."""
+        return None
+
     def get_x_range(self) -> List[List[float]]:
         """[min, max] per input dimension over train and test (DataInput.py:229-242)."""
         d = self.get_input_dimensionality()
@@ -192,6 +230,10 @@ class DataInput(AbstractDataInput):
         idx = torch.as_tensor(np.linspace(start=0, stop=self.n_train, num=int(subset_size), endpoint=False, dtype=int))
         return self._subset(idx)
 
+    def is_equidistant_input_x(self) -> bool:
+        """DataInput.py:169-170."""
+        return is_equidistant(self.data_x_train)
+
     def get_subset(self, subset_size: int, subset_of_data_approach):
         from ..Metrics import MatrixHandlingTypes as mht
         if subset_of_data_approach is mht.SubsetOfDataApproaches.SOD_GRID:
@@ -209,6 +251,23 @@ class BatchDataInput(AbstractDataInput):
         if data_x_test is not None and data_y_test is not None:
             data_x_test, data_y_test = _f64(data_x_test), _f64(data_y_test)
         super().__init__(_f64(data_x_train), _f64(data_y_train), data_x_test, data_y_test, test_ratio, seed)
+
+    def is_equidistant_input_x(self):
+        """BatchDataInput.py:97-98."""
+        return is_equidistant_batch(self.data_x_train)
+
+    # not implemented for batches in the reference either (BatchDataInput.py:30-34, :94-95, :100-101)
+    def get_inducting_x_train(self, *args):
+        raise Exception("get_inducting_x_train -- Not implemented for BatchDataInput.")
+
+    def get_inducting_x_test(self, *args):
+        raise Exception("get_inducting_x_test -- Not implemented for BatchDataInput.")
+
+    def get_independent_smoothed_grid_subset(self, subset_size: int, smoothing_kernel=None):
+        raise Exception("get_independent_smoothed_grid_subset -- Not implemented for BatchDataInput.")
+
+    def get_subset(self, subset_size: int, subset_of_data_approach):
+        raise Exception("get_subset -- Not implemented for BatchDataInput.")
 
 
 class PartitionedDataInput(DataInput):

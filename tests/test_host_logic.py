@@ -175,3 +175,29 @@ def test_ensure_init_exits_when_not_initialised():
         assert e.value.code == -100
     finally:
         gp.initiated = True
+
+
+def test_is_equidistant_and_individual_detrending():
+    import numpy as np
+    import torch
+    from gaussianprocessfundamentals_amd.DataHandling import DataInput as dim
+    from gaussianprocessfundamentals_amd.DataHandling.BatchDataInput import BatchDataInput, is_equidistant as eq_b
+    from gaussianprocessfundamentals_amd.MeanFunctionBasics.BaseMeanFunctions import ZeroMeanFunction
+    grid = np.linspace(0.0, 1.0, 50).reshape(-1, 1)
+    assert dim.is_equidistant(grid)
+    jitter = grid.copy()
+    jitter[10, 0] += 1e-3  # > 1 / (100 * 50) off the mean spacing
+    assert not dim.is_equidistant(jitter)
+    di = dim.DataInput(grid, np.sin(grid), grid[:5], np.cos(grid[:5]))
+    assert di.is_equidistant_input_x()
+    di.set_mean_function(ZeroMeanFunction(1))
+    y = di.get_detrended_y_test_individual(grid[:3], np.ones((3, 1)))
+    assert y.dtype == torch.float64 and torch.equal(y.cpu(), torch.ones(3, 1, dtype=torch.float64))
+    # batched form: B = 1 broadcasts; a non-uniform member fails
+    xb = np.stack([grid])
+    assert bool(eq_b(xb).all())
+    assert not bool(eq_b(np.stack([jitter])).all())
+    bdi = BatchDataInput(xb, np.sin(xb), xb, np.sin(xb))
+    assert bool(bdi.is_equidistant_input_x().all())
+    with pytest.raises(Exception, match="Not implemented for BatchDataInput"):
+        bdi.get_subset(10, None)
