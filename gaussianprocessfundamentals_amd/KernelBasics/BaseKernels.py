@@ -130,6 +130,14 @@ class BaseKernel(k.Kernel):
             out.append(torch.tensor(0.1, dtype=torch.float64))
         return out
 
+    def get_default_hyper_parameter_fixed(self, xrange: List[List[float]], n: int) -> List:
+        """The fixed branch of get_default_hyper_parameter (e.g. BaseKernels.py:323-332)."""
+        return self.get_default_hyper_parameter(xrange, n, from_distribution=False)
+
+    def get_default_hyper_parameter_distribution(self, xrange: List[List[float]], n: int) -> List:
+        """The random branch of get_default_hyper_parameter (e.g. BaseKernels.py:334-350)."""
+        return self.get_default_hyper_parameter(xrange, n, from_distribution=True)
+
     def get_hyper_parameter_distribution_definition(self, xrange: List[List[float]], n: int) -> List[dict]:
         width = xrange[0][1] - xrange[0][0]
         out = []

@@ -238,6 +238,50 @@ class ChangePointOperator(Operator):
             return 1.0 / (1.0 + torch.exp(-100.0 * (xv - c)))
         return (xv < c).to(torch.float64)
 
+    # the reference's mask functions on [N, 1] inputs (Operators.py:379-408), device tensors in and out
+    @staticmethod
+    def approx_indicator(x, cp) -> torch.Tensor:
+        """1 / (1 + exp(-100 (x - cp))) (:379-385)."""
+        return 1.0 / (1.0 + torch.exp(-100.0 * (x - cp)))
+
+    @staticmethod
+    def sigmoid(x, cp) -> torch.Tensor:
+        """0.5 (1 + tanh((cp - x) / 0.0025)) (:387-394)."""
+        return 0.5 * (1 + torch.tanh((cp - x) / 0.0025))
+
+    @staticmethod
+    def indicator_function_tf_less(x, cp) -> torch.Tensor:
+        """[x < cp] as fp64, shape [N, 1] (:396-400)."""
+        c = torch.as_tensor(cp, dtype=torch.float64, device=x.device).reshape(())
+        return (x.reshape(-1) < c).to(torch.float64).reshape(-1, 1)
+
+    @staticmethod
+    def indicator_function_relu_sign(x, cp) -> torch.Tensor:
+        """relu(sign(x - cp)) (:402-404; unused by the reference's operator)."""
+        return torch.relu(torch.sign(x - cp))
+
+    def indicator_function(self, x, cp) -> torch.Tensor:
+        return self.indicator_function_tf_less(x, cp)
+
+    def get_cp_encapsulated_kernel(self, kernel, x_vector, x_vector_, hyper_param, previous_sigmoid, cp):
+        """(K * previous_sigmoid * ind ind'^T, (1 - ind)(1 - ind')^T) for one child (:410-440): its
+        matrix from the device kernel build, masked by this change point's outer indicator; the second
+        value is the complement mask the next child starts from (0 when cp is None, as in the reference)."""
+        from .. import engine
+        x, x_ = engine.as_device_f64(x_vector), engine.as_device_f64(x_vector_)
+        K = kernel.get_tf_tensor(hyper_param, x, x_) * previous_sigmoid
+        if cp is None:
+            return K, torch.zeros((), dtype=torch.float64, device=K.device)
+        cp = torch.as_tensor(cp, dtype=torch.float64, device=K.device)
+        t = global_param.p_cp_operator_type
+        if t == global_param.ChangePointOperatorType.SIGMOID:
+            ind, ind_ = self.sigmoid(x, cp), self.sigmoid(x_, cp)
+        elif t == global_param.ChangePointOperatorType.APPROX_INDICATOR:
+            ind, ind_ = self.approx_indicator(x, cp), self.approx_indicator(x_, cp)
+        else:
+            ind, ind_ = self.indicator_function(x, cp), self.indicator_function(x_, cp)
+        return K * (ind @ ind_.transpose(-1, -2)), (1.0 - ind) @ (1.0 - ind_).transpose(-1, -2)
+
     def get_tf_tensor(self, hyper_parameter: List, x_vector, x_vector_) -> torch.Tensor:
         assert x_vector is not None and x_vector_ is not None, "Input vectors x and x_ uninitialized: " + str(self)
         assert len(hyper_parameter) == self.get_number_of_hyper_parameter(), "Invalid hyper_param size: %s" % str(self)

@@ -352,3 +352,18 @@ def test_blockwise_log_likelihood_per_segment_strategies(approx, handling):
     else:
         exp = o.blockwise_nlml([(t, h, s[0], s[1]) for t, h, s in zip(CHILD_TREES, CHILD_HYPS, segs)], NOISE)
     assert rel(got, exp) < 1e-9, (got, exp)
+
+
+def test_cp_encapsulated_kernel_matches_oracle():
+    # one child through get_cp_encapsulated_kernel (Operators.py:410-440): K * prev * ind ind'^T and
+    # the complement mask; chaining both children reproduces the operator's matrix
+    x = np.sort(np.random.default_rng(3).uniform(0, 1, 70)).reshape(-1, 1)
+    a, b = bk.SquaredExponentialKernel(1), bk.MaternKernel5_2(1)
+    cpo = ops.ChangePointOperator(1, [a, b], [0.4])
+    K0, prev = cpo.get_cp_encapsulated_kernel(a, x, x, [0.2], 1.0, 0.4)
+    K1, none = cpo.get_cp_encapsulated_kernel(b, x, x, [0.3], prev, None)
+    ref = o.change_point_matrix([("SE", {}), ("MAT52", {})], [[0.2], [0.3]], [0.4], x, x)
+    assert float(torch.max(torch.abs((K0 + K1).cpu() - torch.as_tensor(ref)))) <= 1e-13
+    assert float(none) == 0.0
+    full = cpo.get_tf_tensor([0.4, 0.2, 0.3], x, x)
+    assert float(torch.max(torch.abs(full - (K0 + K1)))) <= 1e-14
