@@ -27,12 +27,12 @@ __version__ = "0.1.0"
 
 _SUBMODULES = (
     "global_parameters", "engine", "sweep",
-    "Auxiliary", "Auxiliary.BasicGPComponent",
+    "Auxiliary", "Auxiliary.BasicGPComponent", "Auxiliary.Distances", "Auxiliary.LinearConjugateGradients",
     "KernelBasics", "KernelBasics.Kernel", "KernelBasics.BaseKernels", "KernelBasics.Operators",
     "KernelBasics.PartitioningModel", "KernelBasics.PartitionOperator",
     "MeanFunctionBasics", "MeanFunctionBasics.MeanFunction", "MeanFunctionBasics.BaseMeanFunctions",
     "DataHandling", "DataHandling.DataInput", "DataHandling.AbstractDataInput", "DataHandling.BatchDataInput",
-    "Statistics", "Statistics.CovarianceMatrix", "Statistics.Auxiliary", "Statistics.GaussianProcess",
+    "Statistics", "Statistics.CovarianceMatrix", "Statistics.Auxiliary", "Statistics.GaussianProcess", "Statistics.ApproximationType",
     "Metrics", "Metrics.MatrixHandlingTypes", "Metrics.Metrics", "Metrics.LogLikelihood", "Metrics.Auxiliary",
     "Metrics.BayesianInformationCriterion", "Metrics.MeanSquaredError", "Metrics.CrossValidation",
 )

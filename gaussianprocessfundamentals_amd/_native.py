@@ -31,7 +31,7 @@ EXPORTS = (
     "gpk_grad_workspace_bytes", "gpk_nlml_grad", "gpk_assemble_ragged", "gpk_potrf_aug_ragged",
     "gpk_finalize_ragged", "gpk_nlml_ragged", "gpk_gemv",
     "gpk_assemble_dense", "gpk_dgemm", "gpk_syevj_workspace_bytes", "gpk_syevj", "gpk_pinv_factor",
-    "gpk_ski_weights", "gpk_add_diagonal", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower",
+    "gpk_ski_weights", "gpk_add_diagonal", "gpk_distance_matrix", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower",
 )
 
 
@@ -105,6 +105,8 @@ def _declare(lib):
         "gpk_pinv_factor": (c_int, [c_int64, c_int32, P, P, c_double, c_int32, P, P, P, P]),
         "gpk_ski_weights": (c_int, [P, c_int64, P, c_int64, c_int32, P, P, P]),
         "gpk_add_diagonal": (c_int, [P, c_int64, c_int64, c_int64, c_int32, c_double, P]),
+        "gpk_distance_matrix": (c_int, [c_int, P, c_int64, c_int64, P, c_int64, c_int64, c_int32, c_int32, P,
+                                        c_int64, c_int64, P]),
         "gpk_workspace_bytes": (c_size_t, [c_int, c_int, c_int64, c_int64, c_int32]),
         "gpk_nlml_batched": (c_int, [POINTER(GpkKdesc), c_int32, P, P, c_int, P, P, c_int64, c_int32, P, c_size_t,
                                      P, P, P]),

@@ -1011,6 +1011,24 @@ int gpk_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int3
   return 0;
 }
 
+int gpk_distance_matrix(int mode, const double* A, int64_t n, int64_t a_bstride, const double* B, int64_t m,
+                        int64_t b_bstride, int32_t d, int32_t batch, double* out, int64_t ldo, int64_t o_bstride,
+                        void* stream) {
+  if (mode < 0 || mode > 2) return fail_arg(1, "mode (0 expanded-norm euclidean, 1 manhattan, 2 euclidean)");
+  if (!A && n > 0) return fail_arg(2, "A");
+  if (n < 0) return fail_arg(3, "n");
+  if (!B && m > 0) return fail_arg(5, "B");
+  if (m < 0) return fail_arg(6, "m");
+  if (d <= 0) return fail_arg(8, "d");
+  if (batch < 0) return fail_arg(9, "batch");
+  if (!out && n > 0 && m > 0) return fail_arg(10, "out");
+  if (ldo < m) return fail_arg(11, "ldo");
+  if (n > 65535) return fail_arg(3, "n (at most 65535 rows per call)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(launch_distance(mode, A, n, a_bstride, B, m, b_bstride, d, batch, out, ldo, o_bstride, s), "distance");
+  return 0;
+}
+
 int gpk_add_diagonal(double* A, int64_t n, int64_t lda, int64_t a_bstride, int32_t batch, double value,
                      void* stream) {
   if (!A && n > 0) return fail_arg(1, "A");

@@ -367,7 +367,50 @@ __global__ __launch_bounds__(256) void copy_lower_kernel(const double* src, int6
   if (j <= i && j < n) dst[i * ldd + j] = src[i * lds + j];
 }
 
+// Pairwise distances of Auxiliary/Distances.py, one thread per output element (threads along the
+// row of the output: coalesced stores; the row's A point and the B points come through L1 / L2).
+// mode 0: euclidian_distance (:4-7), sqrt((|a|^2 - 2 a.b) + |b|^2) unclamped -- NaN where rounding
+// makes the argument negative, as the reference; 1: manhattan_distance (:10-12); 2: sqrt(sum (a-b)^2).
+__global__ __launch_bounds__(256) void distance_kernel(int mode, const double* __restrict__ A, int64_t a_bs,
+                                                       const double* __restrict__ B, int64_t m, int64_t b_bs, int d,
+                                                       double* __restrict__ out, int64_t ldo, int64_t o_bs) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= m) return;
+  const int64_t i = blockIdx.y;
+  const double* a = A + (int64_t)blockIdx.z * a_bs + i * d;
+  const double* b = B + (int64_t)blockIdx.z * b_bs + j * d;
+  double r;
+  if (mode == 0) {
+    double na = 0.0, nb = 0.0, ab = 0.0;
+    for (int k = 0; k < d; ++k) {
+      na += a[k] * a[k];
+      nb += b[k] * b[k];
+      ab += a[k] * b[k];
+    }
+    r = sqrt((na - 2.0 * ab) + nb);
+  } else if (mode == 1) {
+    r = 0.0;
+    for (int k = 0; k < d; ++k) r += fabs(a[k] - b[k]);
+  } else {
+    r = 0.0;
+    for (int k = 0; k < d; ++k) {
+      const double t = a[k] - b[k];
+      r += t * t;
+    }
+    r = sqrt(r);
+  }
+  out[(int64_t)blockIdx.z * o_bs + i * ldo + j] = r;
+}
+
 }  // namespace
+
+hipError_t launch_distance(int mode, const double* A, int64_t n, int64_t a_bs, const double* B, int64_t m,
+                           int64_t b_bs, int d, int32_t batch, double* out, int64_t ldo, int64_t o_bs, hipStream_t s) {
+  if (n <= 0 || m <= 0 || batch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(distance_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)n, (unsigned)batch), dim3(256), 0, s,
+                     mode, A, a_bs, B, m, b_bs, d, out, ldo, o_bs);
+  return hipGetLastError();
+}
 
 hipError_t launch_copy_lower(const double* src, int64_t lds, double* dst, int64_t ldd, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;

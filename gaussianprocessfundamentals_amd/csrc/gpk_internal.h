@@ -191,6 +191,8 @@ hipError_t launch_pinv_factor(const double* V, const double* lam, int m, double 
 hipError_t launch_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int d, double* Wm,
                               double* work, hipStream_t s);
 hipError_t launch_copy_lower(const double* src, int64_t lds, double* dst, int64_t ldd, int64_t n, hipStream_t s);
+hipError_t launch_distance(int mode, const double* A, int64_t n, int64_t a_bs, const double* B, int64_t m,
+                           int64_t b_bs, int d, int32_t batch, double* out, int64_t ldo, int64_t o_bs, hipStream_t s);
 hipError_t launch_add_diag(double* A, int64_t n, int64_t lda, int64_t a_bs, double value, int32_t batch,
                            hipStream_t s);
 

@@ -294,6 +294,14 @@ int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam
 int gpk_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int32_t d, double* Wm, double* work,
                     void* stream);
 
+/* Pairwise distance matrices out[b] [n, m] (row stride ldo) of A[b] [n, d] and B[b] [m, d] (row-major),
+ * replacing gpbasics/Auxiliary/Distances.py: mode 0 euclidian_distance (:4-7, the expanded norm
+ * sqrt(|a|^2 - 2 a.b + |b|^2), unclamped: NaN where rounding makes it negative), 1 manhattan_distance
+ * (:10-12), 2 the direct euclidean sqrt(sum (a - b)^2).  Batch strides 0 broadcast one operand. */
+int gpk_distance_matrix(int mode, const double* A, int64_t n, int64_t a_bstride, const double* B, int64_t m,
+                        int64_t b_bstride, int32_t d, int32_t batch, double* out, int64_t ldo, int64_t o_bstride,
+                        void* stream);
+
 /* A[b] += value * I (the "+ tf.eye(n) * noise" of Nystroem_K.py:68-69 and
  * StructuredKernelInterpolation.py:27). */
 int gpk_add_diagonal(double* A, int64_t n, int64_t lda, int64_t a_bstride, int32_t batch, double value,
