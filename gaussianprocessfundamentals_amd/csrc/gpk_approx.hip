@@ -381,11 +381,15 @@ __global__ __launch_bounds__(256) void distance_kernel(int mode, const double* _
   const double* b = B + (int64_t)blockIdx.z * b_bs + j * d;
   double r;
   if (mode == 0) {
+#pragma clang fp contract(off)
+    // the reference's arithmetic shape: the norms as reduce_sum of rounded squares (no FMA), the cross
+    // term as a matmul (fused multiply-add chain), so that they round differently and a == b can give
+    // a slightly negative argument (NaN), as in TensorFlow -- with one shared FMA form it never would
     double na = 0.0, nb = 0.0, ab = 0.0;
     for (int k = 0; k < d; ++k) {
-      na += a[k] * a[k];
+      na += a[k] * a[k];  // contraction off in this block: rounded square, then the add
       nb += b[k] * b[k];
-      ab += a[k] * b[k];
+      ab = fma(a[k], b[k], ab);
     }
     r = sqrt((na - 2.0 * ab) + nb);
   } else if (mode == 1) {

@@ -36,7 +36,9 @@ def test_expanded_euclidean_quirk(d):
     if d == 1:
         assert np.all(np.isfinite(got))  # exact for D = 1
     else:
-        assert np.isnan(got).any()        # the reference's unclamped sqrt reaches NaN on the diagonal
+        # the reference's unclamped sqrt reaches NaN on the diagonal (the norms and the matmul round
+        # differently); where exactly depends on the summation order, so only its presence is pinned
+        assert np.isnan(np.diag(got)).any() and np.isnan(np.diag(ref)).any()
 
 
 def test_batched_and_broadcast():
