@@ -6,6 +6,12 @@ D = 1, NaN on parts of the diagonal for D > 1); ``manhattan_distance`` is the L1
 [n, d] / [m, d] or batched [B, n, d] / [B, m, d] (a batch of 1 broadcasts, as TensorFlow's matmul
 and broadcasting subtraction do); outputs [n, m] / [B, n, m] fp64 on the device.  The kernel
 matrices never go through these: the kernel build evaluates its distances in registers.
+
+Parity note: for D > 1 WHERE the expanded norm turns NaN is parity unpinned -- the reference ships
+no fixture for it, and the rounding shape used here (norms from rounded squares, the cross term as
+an FMA chain, the shape TensorFlow's reduce_sum / matmul are assumed to have) is this build's
+restatement; only the D = 1 result (exact, no NaN) is guaranteed.  Callers that need finite
+distances use ``euclidean_distance_direct``.
 """
 from __future__ import annotations
 

@@ -48,8 +48,13 @@ class LogLikelihood(AbstractLogLikelihood):
         if approx and _wants_grad(hyper_parameter, noise):
             raise NotImplementedError("gradients through the %s approximation are not provided" % self.local_approx)
         if _wants_grad(hyper_parameter, noise):
+            if self.numerical_matrix_handling is mht.NumericalMatrixHandlingType.LINEAR_CONJUGATE_GRADIENT:
+                # the reference's tape differentiates the CG iterations (tolerance 1e-2); the analytic
+                # gradient is the exact one, which would not belong to the CG value
+                raise NotImplementedError("gradients through LINEAR_CONJUGATE_GRADIENT are not provided")
             # differentiable form: what the reference's tf.GradientTape sees through get_metric
-            # (Optimizer/Fitter.py:104-158); backward() uses the analytic device gradient
+            # (Optimizer/Fitter.py:104-158); backward() uses the analytic device gradient.  The value
+            # comes from the selected handling (STRICT / PSEUDO inverse: the exact gradient is theirs)
             return _NegLogLikelihood.apply(self, _as_tensor(noise), *[_as_tensor(h) for h in hyper_parameter])
         if approx or self.numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
             return self._get_metric_by_strategy(hyper_parameter, noise, indices)
@@ -58,10 +63,14 @@ class LogLikelihood(AbstractLogLikelihood):
             n = float(self.data_input.n_train)
             logdet_total = torch.sum(f.logdet())
             ll = (-0.5 * f.fit() + -0.5 * logdet_total) + (-0.5 * (n * LOG_2PI))
-            ll = torch.where(f.info == 0, ll, torch.full_like(ll, -math.inf))
             agg = global_param.p_batch_metric_aggregator or torch.mean
-            return -agg(ll)
-        return f.nlml().reshape(1, 1)
+            res = -agg(ll)
+            # one member that is not positive definite makes the whole aggregate +inf (its NaN
+            # log-determinant would otherwise reach every member through the summed penalty, Q7);
+            # the reference raises from tf.linalg.cholesky (get_metric_checked does)
+            return torch.where(torch.any(f.info != 0), torch.full_like(res, math.inf), res)
+        # a copy: f.out is the factorisation's buffer, overwritten by the next evaluation
+        return f.nlml().reshape(1, 1).clone()
 
     def _get_metric_by_strategy(self, hyper_parameter: List, noise, indices=None) -> torch.Tensor:
         """The reference's formula with the bound get_alpha / get_log_determinant (LogLikelihood.py:36-49)
@@ -118,8 +127,8 @@ class LogLikelihood(AbstractLogLikelihood):
         if self.data_input.data_x_train.dim() == 3:
             raise NotImplementedError("gradients of the BatchDataInput aggregate (Q7) are not provided")
         f = self.covariance_matrix.inverse_factorization(hyper_parameter, noise, gradient=True)
-        g = f.gradient()[0]
-        return f.nlml().reshape(1, 1), _split_like(g[:-1], hyper_parameter), g[-1]
+        g = f.gradient()[0].clone()
+        return f.nlml().reshape(1, 1).clone(), _split_like(g[:-1], hyper_parameter), g[-1]
 
     def get_metric_checked(self, hyper_parameter: List, noise, reset: bool = True) -> torch.Tensor:
         """get_metric that raises CholeskyError when K + noise I is not positive definite
@@ -160,6 +169,8 @@ class _NegLogLikelihood(torch.autograd.Function):
     @staticmethod
     def forward(ctx, metric, noise, *hyper_parameter):
         nl, grads, gnoise = metric.get_metric_and_gradient(list(hyper_parameter), noise, reset=False)
+        if metric.numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
+            nl = metric._get_metric_by_strategy(list(hyper_parameter), noise).reshape(1, 1)
         ctx.save_for_backward(gnoise, *grads)
         ctx.meta = [(h.device, h.dtype) for h in (noise,) + hyper_parameter]
         return nl.clone()

@@ -1023,7 +1023,6 @@ int gpk_distance_matrix(int mode, const double* A, int64_t n, int64_t a_bstride,
   if (batch < 0) return fail_arg(9, "batch");
   if (!out && n > 0 && m > 0) return fail_arg(10, "out");
   if (ldo < m) return fail_arg(11, "ldo");
-  if (n > 65535) return fail_arg(3, "n (at most 65535 rows per call)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   GPK_HIP(launch_distance(mode, A, n, a_bstride, B, m, b_bstride, d, batch, out, ldo, o_bstride, s), "distance");
   return 0;

@@ -411,9 +411,21 @@ __global__ __launch_bounds__(256) void distance_kernel(int mode, const double* _
 hipError_t launch_distance(int mode, const double* A, int64_t n, int64_t a_bs, const double* B, int64_t m,
                            int64_t b_bs, int d, int32_t batch, double* out, int64_t ldo, int64_t o_bs, hipStream_t s) {
   if (n <= 0 || m <= 0 || batch <= 0) return hipSuccess;
-  hipLaunchKernelGGL(distance_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)n, (unsigned)batch), dim3(256), 0, s,
-                     mode, A, a_bs, B, m, b_bs, d, out, ldo, o_bs);
-  return hipGetLastError();
+  // rows go to gridDim.y and members to gridDim.z (each at most 65535): larger inputs are split into
+  // launches over row / member ranges with offset pointers
+  constexpr int64_t kMaxGrid = 65535;
+  for (int64_t b0 = 0; b0 < batch; b0 += kMaxGrid) {
+    const int64_t nb = batch - b0 < kMaxGrid ? batch - b0 : kMaxGrid;
+    for (int64_t i0 = 0; i0 < n; i0 += kMaxGrid) {
+      const int64_t ni = n - i0 < kMaxGrid ? n - i0 : kMaxGrid;
+      hipLaunchKernelGGL(distance_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)ni, (unsigned)nb), dim3(256),
+                         0, s, mode, A + b0 * a_bs + i0 * d, a_bs, B + b0 * b_bs, m, b_bs, d,
+                         out + b0 * o_bs + i0 * ldo, ldo, o_bs);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_copy_lower(const double* src, int64_t lds, double* dst, int64_t ldd, int64_t n, hipStream_t s) {

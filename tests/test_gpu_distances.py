@@ -50,3 +50,11 @@ def test_batched_and_broadcast():
         assert np.allclose(got[i], o.manhattan_distance(a[i], b[0]), rtol=1e-14, atol=1e-15)
     with pytest.raises(ValueError):
         dist.manhattan_distance(a, rng.uniform(0, 1, (2, 40, 2)))
+
+
+def test_more_rows_than_one_grid_dimension():
+    """n > 65535 rows (the kernel's gridDim.y bound): split into launches over row ranges."""
+    rng = np.random.default_rng(11)
+    a, b = rng.uniform(0, 1, (70000, 2)), rng.uniform(0, 1, (5, 2))
+    got = dist.manhattan_distance(a, b).cpu().numpy()
+    assert got.shape == (70000, 5) and np.allclose(got, o.manhattan_distance(a, b), rtol=1e-14, atol=1e-15)
