@@ -143,6 +143,7 @@ struct Tune {
   int64_t upd_band;       // trailing-update tile order: 0 row-major, B > 0 bands of B tile rows
   int64_t skip_zero_rows; // skip the MFMAs of the all-zero 16-row blocks below the y row
   int64_t syevj_abs_tol_e3; // Jacobi: absolute rotation threshold in units of 1e-3 eps max|a_ii|
+  int64_t diag_version;   // diagonal-block kernel: 2 look-ahead schedule, 1 phase-serial
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -155,7 +156,8 @@ Tune& tune() {
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
-                         env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0)};
+                         env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0),
+                         env_i64("GPK_DIAG_VERSION", 2)};
   return t;
 }
 
@@ -393,6 +395,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
     da.kblk = k;
     da.info = info_dev;
     da.dbg = (int32_t)tn.diag_dbg;
+    da.version = (int32_t)tn.diag_version;
     return timed(1, (double)lay->batch * NB * NB * NB / 3.0, 0.0, sp,
                  [&] { return launch_diag(da, dt, lay->batch, sp); });
   };
@@ -1060,6 +1063,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "upd_band")) slot = &t.upd_band;
   else if (!strcmp(key, "skip_zero_rows")) slot = &t.skip_zero_rows;
   else if (!strcmp(key, "syevj_abs_tol_e3")) slot = &t.syevj_abs_tol_e3;
+  else if (!strcmp(key, "diag_version")) slot = &t.diag_version;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

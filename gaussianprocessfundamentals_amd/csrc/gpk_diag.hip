@@ -88,9 +88,10 @@ __device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf
     bad = (bad == 0 && !(piv > 0.0)) ? j + 1 : bad;
     const double ri = rsqrt_refined(piv);      // 1 / L[j][j]
     const double aj = w[j] * ri;
+    const double g = aj * ri;  // w[c] -= (w[j] / L[j][j]) (u[c] / L[j][j]): one FMA per entry
     w[j] = aj;
 #pragma unroll
-    for (int c = j + 1; c < DB; ++c) w[c] = fma(-aj, u[c] * ri, w[c]);
+    for (int c = j + 1; c < DB; ++c) w[c] = fma(-g, u[c], w[c]);
   }
   if (bad != 0 && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + bad);
   if (lane < DB) {
@@ -235,22 +236,225 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Look-ahead form (diag_version 2).  The same tile algebra, scheduled so that the potf2 chain -- the
+// only inherently sequential part -- is the critical path and everything else runs beside it:
+//
+//   P_s  wave 0     : potf2 + inverse of tile (s, s)
+//        waves 1..7 : trailing update of step s-1 for tile columns j >= s + 1; block row I = s - 1
+//                     of L^-1; L's block row s - 1 and L^-1's block row s - 2 to HBM
+//   ---- barrier
+//   QR_s wave w     : row i = s + 1 + w: X_i = A_{i,s} Dinv_s^T and X_{s+1}, both computed transposed
+//                     (Dinv_s A^T), which puts X[r][k = lk + 4q] in the registers of lane (r, lk) --
+//                     the MFMA operand layout -- then A_{i,s+1} -= X_i X_{s+1}^T: tile column s + 1
+//                     is up to date for potf2(s + 1) without waiting for the rest of the update
+//   ---- barrier
+// L^-1 lives in the block's upper tiles, which the factorisation never touches: tile (I, J) of L^-1
+// (J < I) is stored transposed as tile (J, I), its diagonal tiles stay in Dinv -- so block rows of
+// L^-1 are written as soon as they are computed and L stays intact for its own store.  Two barriers
+// per step instead of three, the inverse and every HBM store off the critical path, and 16-B loads of
+// the lower tiles only (the upper tiles of the block are never read).
+template <typename T>
+__device__ __forceinline__ void store_l_rows(const double* A, T* Wb, int64_t ld, int I, int t, int nt) {
+  // rows 16 I .. 16 I + 15 of L, columns 0 .. row (lower triangle only, as the phase-serial kernel)
+  constexpr int EPC = 16 / (int)sizeof(T);
+  typedef T vT __attribute__((ext_vector_type(EPC)));
+  const int ppr = (I + 1) * DB / EPC;  // pieces of a row up to the end of its diagonal tile
+  for (int e = t; e < DB * ppr; e += nt) {
+    const int r = I * DB + e / ppr, pc = e % ppr, c0 = pc * EPC;
+    if (c0 + EPC - 1 <= r) {
+      vT v;
+#pragma unroll
+      for (int u = 0; u < EPC; ++u) v[u] = (T)A[r * LDA + c0 + u];
+      *reinterpret_cast<vT*>(Wb + (int64_t)r * ld + c0) = v;
+    } else {
+#pragma unroll
+      for (int u = 0; u < EPC; ++u)
+        if (c0 + u <= r) Wb[(int64_t)r * ld + c0 + u] = (T)A[r * LDA + c0 + u];
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_inv_rows(const double* A, const double* Dinv, T* Ib, int I, int t, int nt) {
+  // rows 16 I .. 16 I + 15 of L^-1, all 128 columns: tiles J < I transposed from the upper tiles,
+  // the diagonal tile from Dinv (zeros above its diagonal), zeros right of it
+  constexpr int EPC = 16 / (int)sizeof(T);
+  typedef T vT __attribute__((ext_vector_type(EPC)));
+  constexpr int PPR = NB / EPC;
+  for (int e = t; e < DB * PPR; e += nt) {
+    const int rr = e / PPR, c0 = (e % PPR) * EPC;
+    const int J = c0 / DB;
+    vT v;
+#pragma unroll
+    for (int u = 0; u < EPC; ++u) {
+      const int cc = (c0 + u) % DB;
+      v[u] = J < I ? (T)A[(J * DB + cc) * LDA + I * DB + rr] : (J == I ? (T)Dinv[I * DB * DB + rr * DB + cc] : (T)0);
+    }
+    *reinterpret_cast<vT*>(Ib + (I * DB + rr) * NB + c0) = v;
+  }
+}
+
+// tile (I, J) of L^-1, J < I: -Dinv_I sum_{K=J}^{I-1} L_{I,K} Linv_{K,J}, stored transposed in tile (J, I)
+__device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, int I, int J, int lr, int lk) {
+  d4 tacc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s)  // K = J: the diagonal tile Dinv_J
+    tacc = mfma64(A[(I * DB + lr) * LDA + J * DB + 4 * s + lk], Dinv[J * DB * DB + (4 * s + lk) * DB + lr], tacc);
+  for (int K = J + 1; K < I; ++K) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      tacc = mfma64(A[(I * DB + lr) * LDA + K * DB + 4 * s + lk], A[(J * DB + lr) * LDA + K * DB + 4 * s + lk], tacc);
+  }
+  const double* Di = Dinv + I * DB * DB;
+  d4 out = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) out = mfma64(-Di[lr * DB + 4 * s + lk], tacc[s], out);
+  // out[q] = Linv_{I,J}[lk + 4q][lr]  ->  tile (J, I) [lr][lk + 4q]
+#pragma unroll
+  for (int q = 0; q < 4; ++q) A[(J * DB + lr) * LDA + I * DB + lk + 4 * q] = out[q];
+}
+
+template <typename T>
+__global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* A = sm;
+  double* Dinv = A + LDS_A;
+  double* colbuf = Dinv + LDS_DINV;
+  int* flag = reinterpret_cast<int*>(colbuf + LDS_COL);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15;
+  const int lk = lane >> 4;
+  const int b = blockIdx.x;
+  T* Wb = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs + a.j0 * a.ld + a.j0;
+  T* Ib = reinterpret_cast<T*>(a.Winv) + (int64_t)b * a.inv_bs + a.kblk * NB * NB;
+  {
+    // the lower 16-tiles of the block, 16 B per load, every load of a thread in flight at once
+    constexpr int EPC = 16 / (int)sizeof(T);
+    typedef T vT __attribute__((ext_vector_type(EPC)));
+    constexpr int PPR = NB / EPC, RPP = DT / PPR, NPASS = NB / RPP;
+    const int pc = tid % PPR, r0 = tid / PPR;
+    vT v[NPASS];
+#pragma unroll
+    for (int q = 0; q < NPASS; ++q) {
+      const int r = r0 + q * RPP;
+      if (pc * EPC <= (r | (DB - 1))) v[q] = *reinterpret_cast<const vT*>(Wb + (int64_t)r * a.ld + pc * EPC);
+    }
+#pragma unroll
+    for (int q = 0; q < NPASS; ++q) {
+      const int r = r0 + q * RPP;
+      if (pc * EPC <= (r | (DB - 1))) {
+#pragma unroll
+        for (int u = 0; u < EPC; ++u) A[r * LDA + pc * EPC + u] = (double)v[q][u];
+      }
+    }
+  }
+  if (tid == 0) *flag = 0;
+  __syncthreads();
+
+  d4 xs = {0.0, 0.0, 0.0, 0.0};  // wave 0: X_{s+1} (operand layout) from QR_s, stored in P_{s+1}
+#pragma unroll 1
+  for (int s = 0; s < NTL; ++s) {
+    // ---------------------------------------------------------------- P_s
+    if (wave == 0) {
+      if (s > 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[(s * DB + lr) * LDA + (s - 1) * DB + lk + 4 * q] = xs[q];
+      }
+      potf2_tile(A, Dinv + s * DB * DB, colbuf, s, lane, flag, a.j0);
+    } else if (s >= 1) {
+      const int w = wave - 1;
+      const int I = s - 1;
+      if (w < I) inverse_tile(A, Dinv, I, w, lr, lk);
+      // trailing update of step s - 1 for tile columns j >= s + 1 (column s was done in QR_{s-1});
+      // the last waves take the first tiles (waves 1..I hold an inverse tile)
+      const int m = NTL - 1 - s;
+      const int ntri = m * (m + 1) / 2;
+      for (int t = (NTL - 2) - w; t < ntri; t += NTL - 1) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+        const int tj = t - ti * (ti + 1) / 2;
+        const int i = s + 1 + ti, j = s + 1 + tj;
+        d4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = A[(i * DB + lk + 4 * q) * LDA + j * DB + lr];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          acc = mfma64(-A[(i * DB + lr) * LDA + (s - 1) * DB + 4 * k + lk],
+                       A[(j * DB + lr) * LDA + (s - 1) * DB + 4 * k + lk], acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + j * DB + lr] = acc[q];
+      }
+      store_l_rows(A, Wb, a.ld, I, tid - 64, DT - 64);
+      if (I >= 1) store_inv_rows(A, Dinv, Ib, I - 1, tid - 64, DT - 64);
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- QR_s
+    xs = d4{0.0, 0.0, 0.0, 0.0};  // (the old value is dead: nothing keeps it alive across potf2)
+    if (s < NTL - 1 && wave < NTL - 1 - s) {
+      const int i = s + 1 + wave;
+      const double* Dk = Dinv + s * DB * DB;
+      d4 xi = {0.0, 0.0, 0.0, 0.0}, x1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double dv = Dk[lr * DB + 4 * k + lk];
+        xi = mfma64(dv, A[(i * DB + lr) * LDA + s * DB + 4 * k + lk], xi);
+        if (wave != 0) x1 = mfma64(dv, A[((s + 1) * DB + lr) * LDA + s * DB + 4 * k + lk], x1);
+      }
+      if (wave == 0) x1 = xi;
+      // xi[q] = X_i[lr][lk + 4q]: the A operand of k-step q; x1 likewise the B operand
+      d4 acc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = A[(i * DB + lk + 4 * q) * LDA + (s + 1) * DB + lr];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = mfma64(-xi[q], x1[q], acc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + (s + 1) * DB + lr] = acc[q];
+      xs = xi;  // wave 0: tile (s + 1, s) is read by every wave of this phase, stored in P_{s+1}
+      if (wave != 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[(i * DB + lr) * LDA + s * DB + lk + 4 * q] = xi[q];
+      }
+    }
+    __syncthreads();
+  }
+  // after P_7: block row 7 of L to HBM, rows 6 and 7 of L^-1
+  store_l_rows(A, Wb, a.ld, NTL - 1, tid, DT);
+  if (wave >= 1) inverse_tile(A, Dinv, NTL - 1, wave - 1, lr, lk);
+  if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
+  __syncthreads();
+  store_inv_rows(A, Dinv, Ib, NTL - 2, tid, DT);
+  store_inv_rows(A, Dinv, Ib, NTL - 1, tid, DT);
+}
+
 }  // namespace
 
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s) {
-  static bool attr_done[2] = {false, false};
-  const void* fn = dtype == GPK_F64 ? reinterpret_cast<const void*>(diag_kernel<double>)
-                                    : reinterpret_cast<const void*>(diag_kernel<float>);
-  bool& done = attr_done[dtype == GPK_F64 ? 0 : 1];
+  static bool attr_done[4] = {false, false, false, false};
+  const bool v2 = a.version != 1;
+  const void* fn = v2 ? (dtype == GPK_F64 ? reinterpret_cast<const void*>(diag2_kernel<double>)
+                                          : reinterpret_cast<const void*>(diag2_kernel<float>))
+                      : (dtype == GPK_F64 ? reinterpret_cast<const void*>(diag_kernel<double>)
+                                          : reinterpret_cast<const void*>(diag_kernel<float>));
+  bool& done = attr_done[(dtype == GPK_F64 ? 0 : 1) + (v2 ? 2 : 0)];
   if (!done) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DIAG_LDS_BYTES);
     if (e != hipSuccess) return e;
     done = true;
   }
-  if (dtype == GPK_F64)
+  if (v2) {
+    if (dtype == GPK_F64)
+      hipLaunchKernelGGL(diag2_kernel<double>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+    else
+      hipLaunchKernelGGL(diag2_kernel<float>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+  } else if (dtype == GPK_F64) {
     hipLaunchKernelGGL(diag_kernel<double>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
-  else
+  } else {
     hipLaunchKernelGGL(diag_kernel<float>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+  }
   return hipGetLastError();
 }
 
