@@ -102,6 +102,17 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   const double* hyp_g = a.hyp + (int64_t)b * a.hyp_stride;
   for (int e = tid; e < kd.n_hyp; e += 256) hyp_s[e] = hyp_g[e];
   __syncthreads();
+  // per-node constants of a tree (reciprocals of the hyperparameters; single nodes keep theirs in
+  // registers below)
+  FastNode* fns = reinterpret_cast<FastNode*>(pcol + (1 + kd.n_ard) * slot_stride);
+  if (kd.n_nodes > 1 && tid < kd.n_nodes) {
+    const gpk_node nd = kd.nodes[tid];
+    if (nd.op != GPK_OP_ADD && nd.op != GPK_OP_MUL) {
+      FastNode f = make_fast_node(nd, hyp_s, a.d);
+      f.off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
+      fns[tid] = f;
+    }
+  }
   const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
   if (a.A == nullptr) {
     stage_points(kd, a, hyp_s, prow, gi0, b, true, slot_stride);
@@ -121,7 +132,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
       double v = (kd.n_nodes == 1)
                      ? fast_value(make_fast_node(kd.nodes[0], hyp_s, a.d), prow + rr * a.dp + fast_off(kd, slot_stride),
                                   pcol + c * a.dp + fast_off(kd, slot_stride))
-                     : eval_tree(kd, hyp_s, prow + rr * a.dp, pcol + c * a.dp, slot_stride, a.d);
+                     : eval_tree_fast(kd, fns, prow + rr * a.dp, pcol + c * a.dp);
       if (gi == gj) v += a.diag_add;
       W[gi * a.ld + gj] = (TOut)v;
     }
@@ -160,7 +171,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
 #endif
       if (!GPK_ASM_ABLATE)
         v = fast ? fast_value(fn, prow + fn.off + rr * a.dp, pcol + fn.off + c * a.dp)
-                 : eval_tree(kd, hyp_s, prow + rr * a.dp, pcol + c * a.dp, slot_stride, a.d);
+                 : eval_tree_fast(kd, fns, prow + rr * a.dp, pcol + c * a.dp);
       if (rcls == CLS_TRAIN && ccls == CLS_TRAIN && gi == gj) v += noise;
     } else if (rcls == CLS_Y && ccls == CLS_TRAIN) {
       v = yv;
@@ -481,7 +492,8 @@ hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_
 
 hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
                            hipStream_t s) {
-  const size_t lds = sizeof(double) * (GPK_MAX_HYP + 2 * (size_t)(1 + kd.n_ard) * ATILE * a.dp);
+  const size_t lds = sizeof(double) * (GPK_MAX_HYP + 2 * (size_t)(1 + kd.n_ard) * ATILE * a.dp) +
+                     sizeof(FastNode) * GPK_MAX_NODES;
   dim3 grid;
   if (a.plain) {
     const int64_t tr = (a.n + ATILE - 1) / ATILE, tc = (a.m + ATILE - 1) / ATILE;

@@ -148,27 +148,6 @@ struct Stack {
   }
 };
 
-__device__ __forceinline__ double eval_tree(const gpk_kdesc& kd, const double* hyp, const double* pa,
-                                            const double* pb, int slot_stride, int d) {
-  Stack st;
-  st.s0 = 0.0;
-  int sp = 0;
-  for (int q = 0; q < kd.n_nodes; ++q) {
-    const gpk_node nd = kd.nodes[q];
-    if (nd.op == GPK_OP_ADD || nd.op == GPK_OP_MUL) {
-      const double top = st.get(sp - 1);
-      const double below = st.get(sp - 2);
-      st.set(sp - 2, nd.op == GPK_OP_ADD ? below + top : below * top);
-      sp -= 1;
-    } else {
-      const int off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
-      st.set(sp, base_value(nd, hyp, pa + off, pb + off, d));
-      sp += 1;
-    }
-  }
-  return st.s0;
-}
-
 // Single-base-node trees (the common case, e.g. every SURVEY config but C5): the node's constants
 // are computed once per thread into registers and every division by a hyperparameter becomes a
 // multiplication by its reciprocal (|error| <= ~1e-14 relative in K; the generic postfix path keeps
@@ -208,6 +187,29 @@ __device__ __forceinline__ FastNode make_fast_node(const gpk_node& nd, const dou
   return f;
 }
 
+// sin^2(pi t), t >= 0 (the periodic kernel's sin^2(pi d / p) with t = d / p).  sin^2 has period 1 in
+// t, so t is reduced to its fraction (exact in floating point), folded onto [0, 1/2] by
+// sin(pi g) = sin(pi (1 - g)) (1 - g exact there), and sin(pi g) is its Taylor series to x^19 on
+// [0, pi/2] (truncation <= 2.6e-16): about a third of the library sin's work, with no quadrant
+// branches.  The phase error of t itself, |t| ulp, is the reference formula's as well.
+__device__ __forceinline__ double sin2_pi(double t) {
+  const double f = t - floor(t);
+  const double g = fmin(f, 1.0 - f);
+  const double x = PI * g;
+  const double x2 = x * x;
+  double p = -1.0 / 121645100408832000.0;     // -1/19!
+  p = fma(p, x2, 1.0 / 355687428096000.0);    //  1/17!
+  p = fma(p, x2, -1.0 / 1307674368000.0);     // -1/15!
+  p = fma(p, x2, 1.0 / 6227020800.0);         //  1/13!
+  p = fma(p, x2, -1.0 / 39916800.0);          // -1/11!
+  p = fma(p, x2, 1.0 / 362880.0);             //  1/9!
+  p = fma(p, x2, -1.0 / 5040.0);              // -1/7!
+  p = fma(p, x2, 1.0 / 120.0);                //  1/5!
+  p = fma(p, x2, -1.0 / 6.0);                 // -1/3!
+  const double sv = fma(x * x2, p, x);
+  return sv * sv;
+}
+
 // fast_value over coordinate accessors: a(k), b(k) return coordinate k of the two points
 template <typename PA, typename PB>
 __device__ __forceinline__ double fast_value_at(const FastNode& f, PA a, PB b) {
@@ -234,15 +236,11 @@ __device__ __forceinline__ double fast_value_at(const FastNode& f, PA a, PB b) {
   } else if (f.op == GPK_OP_PER) {
     double sn = 0.0;
     if (f.flags & GPK_NODE_STANDARD) {
-      for (int k = 0; k < d; ++k) {
-        const double t = sin(PI * (fabs(a(k) - b(k)) * f.iper));
-        sn += t * t;
-      }
+      for (int k = 0; k < d; ++k) sn += sin2_pi(fabs(a(k) - b(k)) * f.iper);
     } else {
       double dist = 0.0;
       for (int k = 0; k < d; ++k) dist += fabs(a(k) - b(k));
-      const double t = sin(PI * (dist * f.iper));
-      sn = t * t;
+      sn = sin2_pi(dist * f.iper);
     }
     r = exp((-2.0 * sn) * f.il2);
   } else {
@@ -269,6 +267,30 @@ __device__ __forceinline__ double fast_value_at(const FastNode& f, PA a, PB b) {
 
 __device__ __forceinline__ double fast_value(const FastNode& f, const double* a, const double* b) {
   return fast_value_at(f, [a](int k) { return a[k]; }, [b](int k) { return b[k]; });
+}
+
+// The postfix program with every base node's constants precomputed (fns[q] = make_fast_node of
+// node q, fns[q].off its ARD slot offset): the tree form of the single-node fast path -- no division
+// by a hyperparameter per element, the periodic nodes through sin2_pi.
+__device__ __forceinline__ double eval_tree_fast(const gpk_kdesc& kd, const FastNode* fns, const double* pa,
+                                                 const double* pb) {
+  Stack st;
+  st.s0 = 0.0;
+  int sp = 0;
+  for (int q = 0; q < kd.n_nodes; ++q) {
+    const int op = kd.nodes[q].op;
+    if (op == GPK_OP_ADD || op == GPK_OP_MUL) {
+      const double top = st.get(sp - 1);
+      const double below = st.get(sp - 2);
+      st.set(sp - 2, op == GPK_OP_ADD ? below + top : below * top);
+      sp -= 1;
+    } else {
+      const FastNode f = fns[q];
+      st.set(sp, fast_value(f, pa + f.off, pb + f.off));
+      sp += 1;
+    }
+  }
+  return st.s0;
 }
 
 }  // namespace
