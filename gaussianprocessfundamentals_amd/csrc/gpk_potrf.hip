@@ -360,57 +360,70 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
   const int64_t wrow0 = R + wr * (TM / WM);
   const int mact = a.row_end <= 0 ? MB
                  : (int)(a.row_end <= wrow0 ? 0 : ((a.row_end - wrow0 + 15) / 16 < MB ? (a.row_end - wrow0 + 15) / 16 : MB));
-  for (int kc = 0; kc < NK; ++kc) {
-    const int st = kc & 1;
-    // one barrier per chunk, at the top: it retires the chunk kc glds (vmcnt(0), issued a whole
-    // MFMA phase earlier) and frees stage st ^ 1, read during chunk kc - 1.  (At the bottom
-    // hipcc hoists it above the MFMAs, exposing the load latency.)  The vmcnt(0) is explicit:
-    // hipcc's wait insertion does not always see the LDS write of global_load_lds across the
-    // loop back edge (it dropped it once the C loads were issued ahead of the loop).
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt(7), lgkmcnt(15)
-    __syncthreads();
-    if (kc + 1 < NK) GPK_GLDS(st ^ 1, (kc + 1) % NK0);
-    const char* sb = smem + st * STAGE;
-    vec_t fa[MB][2], fb[NBK][2];
-#ifndef GPK_SPLIT_READ
-#define GPK_SPLIT_READ 1
+  // The K loop is instantiated per MFMA row count (MB, 1, 0 live 16-row blocks) so that each form is
+  // one basic block per chunk.  Order inside a chunk: barrier, all fragment reads, the MFMAs of the
+  // first half of the k-steps, THEN the next chunk's global_load_lds, then the second half.  hipcc's
+  // wait insertion treats an outstanding LDS DMA as pending LDS traffic and waits lgkmcnt(0) for any
+  // ds_read issued while one is in flight; with the DMA issued after the first half, the first MFMAs
+  // wait only for their own two fragment reads instead of all of them (the second half's lgkmcnt(0)
+  // falls on reads long completed), and the DMA still has half a chunk plus the next barrier to land.
+  // sched_barrier keeps the scheduler from hoisting the DMA back above the first half.
+#ifndef GPK_GLDS_MID
+#define GPK_GLDS_MID 1
 #endif
-    // the first-half pieces (k-steps 0 .. KS/2-1) of every fragment are read before any second-half
-    // piece, so the first half of the MFMAs waits for half of the reads only
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int m = 0; m < MB; ++m)
-        if (GPK_SPLIT_READ || h == 0) {
-          fa[m][0 + (GPK_SPLIT_READ ? h : 0)] =
-              *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + ((GPK_SPLIT_READ ? h : 0) ? p1 : p0));
-          if (!GPK_SPLIT_READ) fa[m][1] = *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + p1);
-        }
-#pragma unroll
-      for (int n = 0; n < NBK; ++n)
-        if (GPK_SPLIT_READ || h == 0) {
-          fb[n][0 + (GPK_SPLIT_READ ? h : 0)] =
-              *reinterpret_cast<const vec_t*>(sb + boff + n * 16 * ROWB + ((GPK_SPLIT_READ ? h : 0) ? p1 : p0));
-          if (!GPK_SPLIT_READ) fb[n][1] = *reinterpret_cast<const vec_t*>(sb + boff + n * 16 * ROWB + p1);
-        }
-    }
-
-#define GPK_MFMA_CHUNK(MLIM)                                                                           \
-  _Pragma("unroll") for (int s = 0; s < KS; ++s)                                                       \
-  _Pragma("unroll") for (int n = 0; n < NBK; ++n) {                                                    \
-    /* TRSM against the lower-triangular inverse: K chunk kc feeds output columns >= kc GBK only */    \
-    if (MODE == GEMM_TRSM && kc * GBK > wc * (TN / WN) + n * 16 + 15) continue;                        \
-    _Pragma("unroll") for (int m = 0; m < (MLIM); ++m)                                                 \
-      acc[m][n] = CFIRST ? Mfma<T>::op_neg(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]) \
-                         : Mfma<T>::op(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]);   \
+#ifndef GPK_GLDS_MID_F32
+#define GPK_GLDS_MID_F32 0  // f32 (8 k-steps per chunk): the DMA at the top measured faster (116 vs 112 TF)
+#endif
+  constexpr bool GMID = sizeof(T) == 8 ? GPK_GLDS_MID : GPK_GLDS_MID_F32;
+#define GPK_MFMA_STEPS(S0, S1, MLIM)                                                                     \
+  _Pragma("unroll") for (int s = (S0); s < (S1); ++s)                                                    \
+  _Pragma("unroll") for (int n = 0; n < NBK; ++n) {                                                      \
+    /* TRSM against the lower-triangular inverse: K chunk kc feeds output columns >= kc GBK only */      \
+    if (MODE == GEMM_TRSM && kc * GBK > wc * (TN / WN) + n * 16 + 15) continue;                          \
+    _Pragma("unroll") for (int m = 0; m < (MLIM); ++m)                                                   \
+      acc[m][n] = CFIRST ? Mfma<T>::op_neg(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n])   \
+                         : Mfma<T>::op(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]);     \
   }
-    if (mact > 1) {
-      GPK_MFMA_CHUNK(MB)
-    } else if (mact == 1) {
-      GPK_MFMA_CHUNK(1)
-    }
-#undef GPK_MFMA_CHUNK
+#define GPK_KLOOP(MLIM)                                                                                  \
+  for (int kc = 0; kc < NK; ++kc) {                                                                      \
+    const int st = kc & 1;                                                                               \
+    /* one barrier per chunk, at the top: it retires the chunk kc glds (vmcnt(0)) and frees stage       \
+       st ^ 1, read during chunk kc - 1.  The vmcnt(0) is explicit: hipcc's wait insertion does not     \
+       always see the LDS write of global_load_lds across the loop back edge. */                       \
+    __builtin_amdgcn_s_waitcnt(0x0F70); /* gfx9 encoding: vmcnt(0), expcnt(7), lgkmcnt(15) */          \
+    __syncthreads();                                                                                     \
+    if (!GMID && kc + 1 < NK) GPK_GLDS(st ^ 1, (kc + 1) % NK0);                                  \
+    if ((MLIM) > 0) {                                                                                    \
+      const char* sb = smem + st * STAGE;                                                                \
+      vec_t fa[MB][2], fb[NBK][2];                                                                       \
+      /* first-half pieces (k-steps 0 .. KS/2-1) of every fragment first, A0 and B0 leading */          \
+      _Pragma("unroll") for (int h = 0; h < 2; ++h) {                                                    \
+        fa[0][h] = *reinterpret_cast<const vec_t*>(sb + aoff + (h ? p1 : p0));                           \
+        _Pragma("unroll") for (int n = 0; n < NBK; ++n)                                                  \
+          fb[n][h] = *reinterpret_cast<const vec_t*>(sb + boff + n * 16 * ROWB + (h ? p1 : p0));         \
+        _Pragma("unroll") for (int m = 1; m < (MLIM); ++m)                                               \
+          fa[m][h] = *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + (h ? p1 : p0));         \
+      }                                                                                                  \
+      GPK_MFMA_STEPS(0, KS / 2, MLIM)                                                                    \
+      if (GMID) {                                                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+        if (kc + 1 < NK) GPK_GLDS(st ^ 1, (kc + 1) % NK0);                                               \
+        __builtin_amdgcn_sched_barrier(0);                                                               \
+      }                                                                                                  \
+      GPK_MFMA_STEPS(KS / 2, KS, MLIM)                                                                   \
+    } else if (GMID && kc + 1 < NK) {                                                                    \
+      GPK_GLDS(st ^ 1, (kc + 1) % NK0);                                                                  \
+    }                                                                                                    \
   }
+  if (mact > 1) {
+    GPK_KLOOP(MB)
+  } else if (mact == 1) {
+    GPK_KLOOP(1)
+  } else {
+    GPK_KLOOP(0)
+  }
+#undef GPK_KLOOP
+#undef GPK_MFMA_STEPS
 #undef GPK_GLDS
 
   if (GPK_ABLATE == 2 && acc[0][0][0] != (T)12345.678) return;
