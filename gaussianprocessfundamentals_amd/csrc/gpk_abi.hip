@@ -144,6 +144,8 @@ struct Tune {
   int64_t skip_zero_rows; // skip the MFMAs of the all-zero 16-row blocks below the y row
   int64_t syevj_abs_tol_e3; // Jacobi: absolute rotation threshold in units of 1e-3 eps max|a_ii|
   int64_t diag_version;   // diagonal-block kernel: 2 look-ahead schedule, 1 phase-serial
+  int64_t ingroup;        // in-group updates: 1 left-looking, 2 right-looking, 0 auto (by batch)
+  int64_t rl_max_tiles;   // auto: right-looking while batch x (block rows) stays below this
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -157,7 +159,8 @@ Tune& tune() {
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
                          env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0),
-                         env_i64("GPK_DIAG_VERSION", 2)};
+                         env_i64("GPK_DIAG_VERSION", 2), env_i64("GPK_INGROUP", 0),
+                         env_i64("GPK_RL_MAX_TILES", 256)};
   return t;
 }
 
@@ -505,16 +508,22 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
     GPK_HIP(hipStreamWaitEvent(sp, ss->fork, 0), "event");
     GPK_HIP(hipStreamWaitEvent(sb, ss->fork, 0), "event");
   }
+  // In-group updates.  Left-looking (throughput): block column k receives the group's earlier
+  // panels in ONE update of depth 128 (k - g0) right before its diagonal block is factored
+  // (right-looking updates read and write the group's columns once per panel).  Right-looking
+  // (latency, small batches whose thin launches cannot fill the chip): after panel k, the group's
+  // remaining columns receive panel k at depth 128 -- the chain to diag(k + 1) then carries one
+  // short update instead of one of depth up to 128 (G - 1).
+  const int64_t rows128 = lay->p / NB;
+  const bool right_looking = tn.ingroup == 2 || (tn.ingroup == 0 && lay->batch * rows128 < tn.rl_max_tiles);
   bool bulk_pending = false;
   for (int64_t g0 = 0, gsize = G0; g0 < nblk; g0 += gsize, gsize = G) {
     const int64_t gend = std::min(g0 + gsize, nblk);
     for (int64_t k = g0; k < gend; ++k) {
-      // left-looking inside the group: block column k receives the group's earlier panels in ONE
-      // update of depth 128 (k - g0) right before its diagonal block is factored (right-looking
-      // thin updates would read and write the group's columns once per panel)
-      if (k > g0) GPK_HIP(update(g0 * NB, (int)((k - g0) * NB), 0, 1, sp), "update thin");
+      if (!right_looking && k > g0) GPK_HIP(update(g0 * NB, (int)((k - g0) * NB), 0, 1, sp), "update thin");
       GPK_HIP(diag(k), "diag");
       GPK_HIP(trsm(k), "trsm");
+      if (right_looking && k + 1 < gend) GPK_HIP(update(k * NB, NB, 0, gend - k - 1, sp), "update thin");
     }
     const int kd = (int)((gend - g0) * NB);
     if (!la) {
@@ -1064,6 +1073,8 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "skip_zero_rows")) slot = &t.skip_zero_rows;
   else if (!strcmp(key, "syevj_abs_tol_e3")) slot = &t.syevj_abs_tol_e3;
   else if (!strcmp(key, "diag_version")) slot = &t.diag_version;
+  else if (!strcmp(key, "ingroup")) slot = &t.ingroup;
+  else if (!strcmp(key, "rl_max_tiles")) slot = &t.rl_max_tiles;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -15,7 +15,7 @@ import sys
 def klass(name):
     if "assemble_kernel" in name:
         return "assemble"
-    if "diag_kernel" in name:
+    if "diag_kernel" in name or "diag2_kernel" in name:
         return "diag"
     m = re.search(r"gemm_kernel<\w+, (\d)", name)
     if m:

@@ -14,7 +14,7 @@ import sys
 def klass(name):
     if "assemble_kernel" in name:
         return "assemble"
-    if "diag_kernel" in name:
+    if "diag_kernel" in name or "diag2_kernel" in name:
         return "diag"
     if "gemm_kernel<double, 1" in name or "gemm_kernel<float, 1" in name:
         return "trsm"

@@ -47,3 +47,35 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def thin_by_depth(path, n, batch, G):
+    """Per-depth average rate of the thin (left-looking in-group) launches of the last step."""
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                  for r in csv.DictReader(open(path)))
+    starts = [i for i, r in enumerate(rows) if "assemble_kernel" in r[2]]
+    step = rows[starts[-1]:]
+    nb = n // 128
+    upd = [(s, e) for s, e, k in step if "gemm_kernel<double, 0" in k or "gemm_kernel<float, 0" in k]
+    i = 0
+    acc = {}
+    for g0 in range(0, nb, G):
+        gend = min(g0 + G, nb)
+        for k in range(g0 + 1, gend):
+            rows_ = (nb - k) * 128
+            elems = sum(rows_ - r for r in range(128))
+            s, e = upd[i]
+            d = k - g0
+            a = acc.setdefault(d, [0.0, 0.0, 0])
+            a[0] += (e - s) * 1e-9
+            a[1] += 2.0 * 128 * d * elems * batch
+            a[2] += 1
+            i += 1
+        i += 1
+    for d in sorted(acc):
+        sec, fl, cnt = acc[d]
+        print("   thin depth %4d: %2d launches, avg %.1f us, %.1f TF/s" % (128 * d, cnt, sec / cnt * 1e6, fl / sec / 1e12))
+
+
+if __name__ == "__main__" and len(sys.argv) > 5 and sys.argv[5] == "depth":
+    thin_by_depth(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
