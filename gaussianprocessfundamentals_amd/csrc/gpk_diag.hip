@@ -250,8 +250,9 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
 //                     is up to date for potf2(s + 1) without waiting for the rest of the update
 //   ---- barrier
 // L^-1 lives in the block's upper tiles, which the factorisation never touches: tile (I, J) of L^-1
-// (J < I) is stored transposed as tile (J, I), its diagonal tiles stay in Dinv -- so block rows of
-// L^-1 are written as soon as they are computed and L stays intact for its own store.  Two barriers
+// (J < I) is stored transposed as tile (J, I), its diagonal tiles stay in Dinv -- so no in-place
+// hazard, and each tile of L^-1 goes to HBM from the registers that computed it (the zero tiles in
+// P_0, where waves 1..7 are idle).  Two barriers
 // per step instead of three, the inverse and every HBM store off the critical path, and 16-B loads of
 // the lower tiles only (the upper tiles of the block are never read).
 template <typename T>
@@ -276,27 +277,32 @@ __device__ __forceinline__ void store_l_rows(const double* A, T* Wb, int64_t ld,
 }
 
 template <typename T>
-__device__ __forceinline__ void store_inv_rows(const double* A, const double* Dinv, T* Ib, int I, int t, int nt) {
-  // rows 16 I .. 16 I + 15 of L^-1, all 128 columns: tiles J < I transposed from the upper tiles,
-  // the diagonal tile from Dinv (zeros above its diagonal), zeros right of it
+__device__ __forceinline__ void store_inv_zeros(T* Ib, int t, int nt) {
+  // the tiles right of L^-1's diagonal tiles: zeros (read as such by the panel solve's MFMA chunks)
   constexpr int EPC = 16 / (int)sizeof(T);
   typedef T vT __attribute__((ext_vector_type(EPC)));
-  constexpr int PPR = NB / EPC;
-  for (int e = t; e < DB * PPR; e += nt) {
-    const int rr = e / PPR, c0 = (e % PPR) * EPC;
-    const int J = c0 / DB;
-    vT v;
+  constexpr int PPT = DB / EPC;  // pieces per tile row
+  for (int e = t; e < NB * NB / EPC; e += nt) {
+    const int r = e / (NB / EPC), c0 = (e % (NB / EPC)) * EPC;
+    if (c0 / DB > r / DB) {
+      vT v;
 #pragma unroll
-    for (int u = 0; u < EPC; ++u) {
-      const int cc = (c0 + u) % DB;
-      v[u] = J < I ? (T)A[(J * DB + cc) * LDA + I * DB + rr] : (J == I ? (T)Dinv[I * DB * DB + rr * DB + cc] : (T)0);
+      for (int u = 0; u < EPC; ++u) v[u] = (T)0;
+      *reinterpret_cast<vT*>(Ib + r * NB + c0) = v;
     }
-    *reinterpret_cast<vT*>(Ib + (I * DB + rr) * NB + c0) = v;
   }
+  (void)PPT;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_inv_diag(const double* Dinv, T* Ib, int I, int t, int nt) {
+  // diagonal tile I of L^-1 (Dinv_I, zeros above its diagonal)
+  for (int e = t; e < DB * DB; e += nt) Ib[(I * DB + e / DB) * NB + I * DB + e % DB] = (T)Dinv[I * DB * DB + e];
 }
 
 // tile (I, J) of L^-1, J < I: -Dinv_I sum_{K=J}^{I-1} L_{I,K} Linv_{K,J}, stored transposed in tile (J, I)
-__device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, int I, int J, int lr, int lk) {
+template <typename T>
+__device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, T* Ib, int I, int J, int lr, int lk) {
   d4 tacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 4; ++s)  // K = J: the diagonal tile Dinv_J
@@ -310,9 +316,13 @@ __device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, int 
   d4 out = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 4; ++s) out = mfma64(-Di[lr * DB + 4 * s + lk], tacc[s], out);
-  // out[q] = Linv_{I,J}[lk + 4q][lr]  ->  tile (J, I) [lr][lk + 4q]
+  // out[q] = Linv_{I,J}[lk + 4q][lr]  ->  tile (J, I) [lr][lk + 4q] for the later rows, and straight
+  // from the registers to HBM (16 lanes of a row store 128 contiguous bytes)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) A[(J * DB + lr) * LDA + I * DB + lk + 4 * q] = out[q];
+  for (int q = 0; q < 4; ++q) {
+    A[(J * DB + lr) * LDA + I * DB + lk + 4 * q] = out[q];
+    Ib[(I * DB + lk + 4 * q) * NB + J * DB + lr] = (T)out[q];
+  }
 }
 
 template <typename T>
@@ -364,16 +374,18 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) A[(s * DB + lr) * LDA + (s - 1) * DB + lk + 4 * q] = xs[q];
       }
-      potf2_tile(A, Dinv + s * DB * DB, colbuf, s, lane, flag, a.j0);
-    } else if (s >= 1) {
+      if (!(a.dbg & 2)) potf2_tile(A, Dinv + s * DB * DB, colbuf, s, lane, flag, a.j0);  // timing ablation
+    } else if (s == 0) {
+      if (!(a.dbg & 8)) store_inv_zeros(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
+    } else {
       const int w = wave - 1;
       const int I = s - 1;
-      if (w < I) inverse_tile(A, Dinv, I, w, lr, lk);
+      if (w < I && !(a.dbg & 1)) inverse_tile(A, Dinv, Ib, I, w, lr, lk);
       // trailing update of step s - 1 for tile columns j >= s + 1 (column s was done in QR_{s-1});
       // the last waves take the first tiles (waves 1..I hold an inverse tile)
       const int m = NTL - 1 - s;
       const int ntri = m * (m + 1) / 2;
-      for (int t = (NTL - 2) - w; t < ntri; t += NTL - 1) {
+      for (int t = (NTL - 2) - w; t < ((a.dbg & 4) ? 0 : ntri); t += NTL - 1) {
         int ti = 0;
         while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
         const int tj = t - ti * (ti + 1) / 2;
@@ -388,13 +400,15 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + j * DB + lr] = acc[q];
       }
-      store_l_rows(A, Wb, a.ld, I, tid - 64, DT - 64);
-      if (I >= 1) store_inv_rows(A, Dinv, Ib, I - 1, tid - 64, DT - 64);
+      if (!(a.dbg & 8)) {
+        store_l_rows(A, Wb, a.ld, I, tid - 64, DT - 64);
+        store_inv_diag(Dinv, Ib, I, tid - 64, DT - 64);
+      }
     }
     __syncthreads();
     // ---------------------------------------------------------------- QR_s
     xs = d4{0.0, 0.0, 0.0, 0.0};  // (the old value is dead: nothing keeps it alive across potf2)
-    if (s < NTL - 1 && wave < NTL - 1 - s) {
+    if (s < NTL - 1 && wave < NTL - 1 - s && !(a.dbg & 4)) {
       const int i = s + 1 + wave;
       const double* Dk = Dinv + s * DB * DB;
       d4 xi = {0.0, 0.0, 0.0, 0.0}, x1 = {0.0, 0.0, 0.0, 0.0};
@@ -422,12 +436,13 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
     __syncthreads();
   }
   // after P_7: block row 7 of L to HBM, rows 6 and 7 of L^-1
+  if (wave >= 1) {
+    inverse_tile(A, Dinv, Ib, NTL - 1, wave - 1, lr, lk);
+  } else {
+    store_inv_diag(Dinv, Ib, NTL - 1, lane, 64);
+  }
   store_l_rows(A, Wb, a.ld, NTL - 1, tid, DT);
-  if (wave >= 1) inverse_tile(A, Dinv, NTL - 1, wave - 1, lr, lk);
   if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
-  __syncthreads();
-  store_inv_rows(A, Dinv, Ib, NTL - 2, tid, DT);
-  store_inv_rows(A, Dinv, Ib, NTL - 1, tid, DT);
 }
 
 }  // namespace

@@ -1,0 +1,48 @@
+"""diag2_kernel ablation: per-launch HIP-event span with and without the potf2 chain
+(gpk_tune("diag_debug", 2): timing only, wrong results), look-ahead off.
+
+usage: python tools/exp_diag2.py [batch] [n]
+"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+import gaussianprocessfundamentals_amd.global_parameters as gp  # noqa: E402
+
+gp.init(0)
+from gaussianprocessfundamentals_amd import _native as nat  # noqa: E402
+from gaussianprocessfundamentals_amd import engine  # noqa: E402
+from gaussianprocessfundamentals_amd.KernelBasics import BaseKernels as bk  # noqa: E402
+
+
+def main():
+    batch = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    dev = torch.device("cuda", 0)
+    f = engine.AugmentedFactorization(n, 1, 0, batch)
+    kd = engine.kernel_descriptor(bk.SquaredExponentialKernel(1), 1)
+    X = torch.sort(torch.rand(n, 1, dtype=torch.float64, device=dev), dim=0).values.contiguous()
+    Y = torch.rand(1, n, dtype=torch.float64, device=dev)
+    H = torch.full((batch, 1), 0.1, dtype=torch.float64, device=dev)
+    NZ = torch.tensor([1e-2], dtype=torch.float64, device=dev)
+    nat.tune("lookahead", 0)
+    for dbg in (0, 2, 0):
+        nat.tune("diag_debug", dbg)
+        f.run(kd, H, 1, NZ, 0, X, 0, Y, 0)
+        torch.cuda.synchronize()
+        nat.timing_reset()
+        nat.timing_enable(True)
+        for _ in range(3):
+            f.run(kd, H, 1, NZ, 0, X, 0, Y, 0)
+        torch.cuda.synchronize()
+        nat.timing_enable(False)
+        t = nat.timing_read()
+        print("diag_debug %d: diag %.1f us x %d" % (dbg, t["diag"]["ms"] * 1e3 / max(1, t["diag"]["launches"]),
+                                                   t["diag"]["launches"] // 3))
+    nat.tune("diag_debug", 0)
+    nat.tune("lookahead", 1)
+
+
+if __name__ == "__main__":
+    main()
