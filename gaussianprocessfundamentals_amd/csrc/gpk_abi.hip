@@ -514,13 +514,22 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // (latency, small batches whose thin launches cannot fill the chip): after panel k, the group's
   // remaining columns receive panel k at depth 128 -- the chain to diag(k + 1) then carries one
   // short update instead of one of depth up to 128 (G - 1).
+  // Two-level left-looking (ingroup 3): the group is split in halves; each half is left-looking
+  // within itself, and between the halves ONE update of the second half's columns with the first
+  // half's panels (depth 128 G/2) -- the thin launches re-read the half's panels instead of the
+  // group's, 36 instead of 42 panel-column reads + writes per group of 8 (they are HBM-bound).
   const int64_t rows128 = lay->p / NB;
   const bool right_looking = tn.ingroup == 2 || (tn.ingroup == 0 && lay->batch * rows128 < tn.rl_max_tiles);
+  const bool two_level = !right_looking && (tn.ingroup == 3 || tn.ingroup == 0) && G >= 4;
   bool bulk_pending = false;
   for (int64_t g0 = 0, gsize = G0; g0 < nblk; g0 += gsize, gsize = G) {
     const int64_t gend = std::min(g0 + gsize, nblk);
+    const int64_t gmid = two_level ? std::min(g0 + (gend - g0 + 1) / 2, gend) : gend;
     for (int64_t k = g0; k < gend; ++k) {
-      if (!right_looking && k > g0) GPK_HIP(update(g0 * NB, (int)((k - g0) * NB), 0, 1, sp), "update thin");
+      const int64_t h0 = k < gmid ? g0 : gmid;  // first panel of k's half
+      if (two_level && k == gmid && gmid > g0)
+        GPK_HIP(update(g0 * NB, (int)((gmid - g0) * NB), 0, gend - gmid, sp), "update half");
+      if (!right_looking && k > h0) GPK_HIP(update(h0 * NB, (int)((k - h0) * NB), 0, 1, sp), "update thin");
       GPK_HIP(diag(k), "diag");
       GPK_HIP(trsm(k), "trsm");
       if (right_looking && k + 1 < gend) GPK_HIP(update(k * NB, NB, 0, gend - k - 1, sp), "update thin");

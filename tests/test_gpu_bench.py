@@ -35,7 +35,7 @@ def test_bench_dist_rehearsal_metric():
               "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["scaling"] == "weak" and d["dtype"] == "f64"
-    assert d["value"] > 0 and d["config"]["batches_in_flight"] == 3
+    assert d["value"] > 0 and d["config"]["batches_in_flight"] == 2  # bench.DEFAULT_PIPELINE_METRIC
     assert d["check"]["info"] == 0 and d["check"]["allgather_ok"] is True
     r = d["roofline"]
     assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1.0

@@ -68,13 +68,14 @@ def _nlml_with(knob, value, n, batch, m=0):
 
 @pytest.mark.parametrize("n,batch,m", [(1100, 1, 0), (1100, 3, 21), (3000, 2, 0)])
 def test_in_group_schedules_agree(n, batch, m):
-    """Right-looking (latency) and left-looking (throughput) in-group updates: the same factorisation
-    up to summation order -- -LML rel <= 1e-12, the factor's lower triangle max-abs <= 1e-12 max|L|."""
+    """Right-looking (latency), left-looking and two-level left-looking (throughput) in-group updates:
+    the same factorisation up to summation order -- -LML rel <= 1e-12, the factor's lower triangle max-abs <= 1e-12 max|L|."""
     a = _nlml_with("ingroup", 1, n, batch, m)
-    b = _nlml_with("ingroup", 2, n, batch, m)
-    la, lb = a[0], b[0]
-    assert float((la - lb).abs().max()) <= 1e-12 * float(la.abs().max())
-    na, nb_ = a[3].view(batch, 4)[:, 0], b[3].view(batch, 4)[:, 0]
-    assert float(((na - nb_).abs() / na.abs()).max()) <= 1e-12
-    if m:
-        assert float((a[4] - b[4]).abs().max()) <= 1e-10 and float((a[5] - b[5]).abs().max()) <= 1e-10
+    for mode in (2, 3):  # right-looking, two-level left-looking
+        b = _nlml_with("ingroup", mode, n, batch, m)
+        la, lb = a[0], b[0]
+        assert float((la - lb).abs().max()) <= 1e-12 * float(la.abs().max())
+        na, nb_ = a[3].view(batch, 4)[:, 0], b[3].view(batch, 4)[:, 0]
+        assert float(((na - nb_).abs() / na.abs()).max()) <= 1e-12
+        if m:
+            assert float((a[4] - b[4]).abs().max()) <= 1e-10 and float((a[5] - b[5]).abs().max()) <= 1e-10
