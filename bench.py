@@ -87,6 +87,22 @@ def pmc_traffic(cfg, batch):
     return rec
 
 
+def synthetic_inputs(cfg, n):
+    """SURVEY §8(d) synthetic inputs (numpy default_rng): the generator the golden vectors and the oracle
+    use (oracle.gp_oracle.make_inputs), restated here so that the measured path imports nothing from oracle/
+    (only the cpu_baseline leg does)."""
+    import numpy as np
+    if cfg in ("C2", "C4", "metric"):
+        seed = {"C2": 1, "C4": 3, "metric": 5}[cfg]
+        rng = np.random.default_rng(seed)
+        x = np.sort(rng.uniform(0.0, 1.0, n)).reshape(n, 1)
+        return x, np.sin(4.0 * math.pi * x[:, 0]) + 0.1 * rng.standard_normal(n)
+    d, seed = {"C3": (4, 2), "C5": (8, 4)}[cfg]
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(0.0, 1.0, (n, d))
+    return x, np.sum(np.sin(2.0 * math.pi * x), axis=1) + 0.1 * rng.standard_normal(n)
+
+
 def c4_candidates():
     """lengthscale geomspace(0.02, 0.5, 16) x signal variance geomspace(0.25, 4, 8)
     (the grid of tests/golden/make_golden.py)."""
@@ -214,7 +230,6 @@ def main():
         gp.p_scaled_base_kernel = True  # hyp = [lengthscale, signal variance]
     from gaussianprocessfundamentals_amd import _native as nat
     from gaussianprocessfundamentals_amd import engine
-    from oracle import gp_oracle as o  # input generator only (same seeds as the golden vectors)
 
     kname, d, n, noise, dtn, hyp = CONFIGS[args.config]
     n = args.n or n
@@ -223,7 +238,7 @@ def main():
     elif hyp is None:
         hyp = [[0.4 + 0.1 * i for i in range(d)], 1.0, 0.5]
     dt = torch.float64 if dtn == "f64" else torch.float32
-    x, y = o.make_inputs("metric" if args.config == "metric" else args.config, n=n)
+    x, y = synthetic_inputs(args.config, n)
     dev = torch.device("cuda", local)
     X = torch.as_tensor(x, dtype=torch.float64, device=dev).contiguous()
     Y = torch.as_tensor(y, dtype=torch.float64, device=dev).reshape(1, n).contiguous()

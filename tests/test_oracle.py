@@ -128,3 +128,12 @@ def test_function_draw_restatements():
     mu, _ = o.posterior(SE, [0.1], 1e-2, x, yy, xt)
     f = o.n_posterior_functions(SE, [0.1], 1e-2, x, yy, xt, np.zeros((9, 2)), 1e-8)
     assert np.array_equal(f, np.repeat(mu.reshape(-1, 1), 2, axis=1))
+
+
+def test_bench_inputs_match_the_oracle_generator():
+    """bench.py restates the SURVEY §8(d) generator (the measured path imports nothing from oracle/):
+    it must produce the golden vectors' inputs bit for bit."""
+    import bench
+    for cfg, n in (("C2", 4096), ("C4", 512), ("metric", 8192), ("C3", 777), ("C5", 300)):
+        a, b = bench.synthetic_inputs(cfg, n), o.make_inputs(cfg, n=n)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), cfg
