@@ -68,6 +68,9 @@ KERNEL_CASES = [
     (("MAT52", {"ard": True, "standard": True}), [[0.25, 0.5, 0.75, 1.0]], 4),
     (("MAT32", {"standard": True}), [0.4], 3),
     (("ADD", [("SE", {"ard": True}), ("PER", {"standard": True})]), [[0.4, 0.6, 0.8], 1.0, 0.5], 3),
+    # GPK_MAX_DIM = 16 input dimensions
+    (("SE", {"ard": True}), [[0.6 + 0.05 * i for i in range(16)]], 16),
+    (("MUL", [("MAT32", {"standard": True}), ("PER", {"standard": True})]), [1.3, 1.1, 0.8], 16),
 ]
 
 
