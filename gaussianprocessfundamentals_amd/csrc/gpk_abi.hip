@@ -144,7 +144,7 @@ struct Tune {
   int64_t skip_zero_rows; // skip the MFMAs of the all-zero 16-row blocks below the y row
   int64_t syevj_abs_tol_e3; // Jacobi: absolute rotation threshold in units of 1e-3 eps max|a_ii|
   int64_t diag_version;   // diagonal-block kernel: 2 look-ahead schedule, 1 phase-serial
-  int64_t ingroup;        // in-group updates: 1 left-looking, 2 right-looking, 0 auto (by batch)
+  int64_t ingroup;        // in-group updates: 1 left-looking, 2 right-looking, 3 two-level, 0 auto (by batch)
   int64_t rl_max_tiles;   // auto: right-looking while batch x (block rows) stays below this
 };
 
