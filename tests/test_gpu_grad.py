@@ -116,3 +116,22 @@ def test_gradient_not_positive_definite_is_nan():
     m = _metric(SE, x, y)
     nl, grads, gn = m.get_metric_and_gradient(hyp_list([0.5]), torch.tensor(-1.0, dtype=torch.float64))
     assert math.isinf(float(nl)) and math.isnan(float(gn)) and math.isnan(float(grads[0]))
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_gradient_under_every_in_group_schedule(mode):
+    """The identity-augmented factorisation (K^-1 rows, structurally zero tiles skipped) under the
+    left-looking, right-looking and two-level in-group schedules, over several panel groups."""
+    old = engine.nat.tune("ingroup", mode)
+    try:
+        x, y = o.make_inputs("C1", n=1100, seed=12)
+        f = build_gp(SE, x, y).covariance_matrix.inverse_factorization(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64))
+        Kn = o.k_noised(SE, [0.1], 1e-2, x)
+        Ki = np.linalg.inv(Kn)
+        assert np.linalg.norm(f.k_inv(0).cpu().numpy() - Ki) / np.linalg.norm(Ki) < 1e-8
+        nl_ref, g_ref, gn_ref = ad.nlml_and_grad(SE, [0.1], 1e-2, x, y)
+        g = f.gradient()[0].cpu().numpy()
+        _check_grad([g[:1], g[1]], [g_ref[0], gn_ref])
+        assert abs(float(f.nlml()[0]) - nl_ref) <= 1e-9 * abs(nl_ref)
+    finally:
+        engine.nat.tune("ingroup", old)

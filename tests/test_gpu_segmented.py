@@ -367,3 +367,15 @@ def test_cp_encapsulated_kernel_matches_oracle():
     assert float(none) == 0.0
     full = cpo.get_tf_tensor([0.4, 0.2, 0.3], x, x)
     assert float(torch.max(torch.abs(full - (K0 + K1)))) <= 1e-14
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_ragged_paths_under_every_in_group_schedule(mode):
+    """Ragged batches (per-member sizes, zero-row skipping) and test rows under the left-looking,
+    right-looking and two-level in-group schedules: the same oracle bars as above."""
+    old = nat.tune("ingroup", mode)
+    try:
+        test_ragged_nlml_factor_alpha_match_oracle([(SE, [0.1]), (PER, [0.8, 0.5]), (("ADD", [SE, MAT52]), [0.2, 0.4])])
+        test_ragged_posterior_with_test_rows()
+    finally:
+        nat.tune("ingroup", old)
