@@ -60,6 +60,11 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define GPK_UPD_WN_F32 2
 #endif
 
+#ifndef GPK_ABLATE
+#define GPK_ABLATE 0  // timing-only ablations (wrong results): 1 no C read, 2 no epilogue, 3 K loop x2,
+                      // 4 operands from one L2-resident block, 5 no per-chunk barrier
+#endif
+
 constexpr int ROWB = 128;  // bytes of one row of a staged K chunk (8 pieces of 16 B)
 
 // bijective XCD-aware remap: consecutive logical tiles land on one XCD (blockIdx % 8 group)
@@ -227,7 +232,11 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
   const T* Ag = W + R * a.ld + a.j0;
   const T* Bg;
   int64_t ldb;
-  if (MODE == GEMM_UPDATE) {
+  if (GPK_ABLATE == 4 && MODE == GEMM_UPDATE) {
+    Ag = reinterpret_cast<const T*>(a.W) + a.row0 * a.ld + a.j0;  // timing-only: L2-resident operands
+    Bg = Ag + TM * a.ld;
+    ldb = a.ld;
+  } else if (MODE == GEMM_UPDATE) {
     Bg = W + (a.row0 + tj * TN) * a.ld + a.j0;
     ldb = a.ld;
   } else {
@@ -344,9 +353,6 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
   const int boff = (TM + wc * (TN / WN) + lr) * ROWB;
   const int p0 = swz(lr, q) * 16, p1 = swz(lr, q + 4) * 16;
 
-#ifndef GPK_ABLATE
-#define GPK_ABLATE 0  // timing-only ablations (wrong results): 1 no C read, 2 no epilogue, 3 K loop x2
-#endif
   const int NK0 = (MODE == GEMM_TRSM) ? NB / GBK : a.kdepth / GBK;
   const int NK = (GPK_ABLATE == 3 && MODE == GEMM_UPDATE) ? 2 * NK0 : NK0;
   GPK_GLDS(0, 0);
@@ -390,8 +396,10 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
     /* one barrier per chunk, at the top: it retires the chunk kc glds (vmcnt(0)) and frees stage       \
        st ^ 1, read during chunk kc - 1.  The vmcnt(0) is explicit: hipcc's wait insertion does not     \
        always see the LDS write of global_load_lds across the loop back edge. */                       \
-    __builtin_amdgcn_s_waitcnt(0x0F70); /* gfx9 encoding: vmcnt(0), expcnt(7), lgkmcnt(15) */          \
-    __syncthreads();                                                                                     \
+    if (GPK_ABLATE != 5) {                                                                               \
+      __builtin_amdgcn_s_waitcnt(0x0F70); /* gfx9 encoding: vmcnt(0), expcnt(7), lgkmcnt(15) */        \
+      __syncthreads();                                                                                   \
+    }                                                                                                    \
     if (!GMID && kc + 1 < NK) GPK_GLDS(st ^ 1, (kc + 1) % NK0);                                  \
     if ((MLIM) > 0) {                                                                                    \
       const char* sb = smem + st * STAGE;                                                                \
