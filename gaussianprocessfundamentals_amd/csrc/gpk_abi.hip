@@ -146,6 +146,7 @@ struct Tune {
   int64_t diag_version;   // diagonal-block kernel: 2 look-ahead schedule, 1 phase-serial
   int64_t ingroup;        // in-group updates: 1 left-looking, 2 right-looking, 3 two-level, 0 auto (by batch)
   int64_t rl_max_tiles;   // auto: right-looking while batch x (block rows) stays below this
+  int64_t band_skip;      // identity extra rows: leave the zero band's tiles out of the grid
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -160,7 +161,7 @@ Tune& tune() {
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
                          env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0),
                          env_i64("GPK_DIAG_VERSION", 2), env_i64("GPK_INGROUP", 0),
-                         env_i64("GPK_RL_MAX_TILES", 256)};
+                         env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1)};
   return t;
 }
 
@@ -419,6 +420,20 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   base.y_row = lay->y_row;
   base.p = lay->p;
   base.row_end = tn.skip_zero_rows ? lay->y_row + 1 : 0;  // rows below the y row are zero
+  // identity extra rows: the tiles wholly inside the zero band [zlo, zhi) are left out of the grid
+  // (launched and exiting at once they would also crowd the live tiles onto a few XCDs, since
+  // xcd_remap hands each XCD a contiguous run of tile ids).  c: a tile index from row0 -> its index
+  // in the compressed enumeration.
+  auto set_band = [&](GemmArgs& ga, int tile) {
+    if (!eye || !tn.band_skip) return;
+    const int64_t b0 = (ga.zlo - ga.row0) / tile, b1 = (ga.zhi - ga.row0) / tile;
+    if (b1 <= b0) return;
+    ga.bz0 = (int32_t)b0;
+    ga.bzn = (int32_t)(b1 - b0);
+  };
+  auto compress = [](const GemmArgs& ga, int64_t c) -> int64_t {
+    return ga.bzn == 0 || c < ga.bz0 ? c : (c >= (int64_t)ga.bz0 + ga.bzn ? c - ga.bzn : ga.bz0);
+  };
   // panel solve of block k: every row below the block (the y / test rows included)
   auto trsm = [&](int64_t k) -> hipError_t {
     GemmArgs ga = base;
@@ -427,13 +442,16 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
     ga.row0 = ga.j0 + NB;
     const int64_t rows = lay->p - ga.row0;
     if (rows <= 0) return hipSuccess;
-    const int tile = (rows / NB * lay->batch >= tn.trsm_t128_min) ? 128 : 64;
-    ga.nt = (int32_t)(rows / tile);
     ga.kdepth = NB;
     if (eye) {  // identity rows t >= j0 + nb are still zero in this panel
       ga.zlo = lay->n_pad + ga.j0 + NB;
       ga.zhi = lay->y_row;
     }
+    set_band(ga, 128);
+    const int tile = (compress(ga, rows / NB) * lay->batch >= tn.trsm_t128_min) ? 128 : 64;
+    ga.bz0 = ga.bzn = 0;
+    set_band(ga, tile);
+    ga.nt = (int32_t)compress(ga, rows / tile);
     // algorithmic: rows that are nonzero in the panel (K part + extra rows) x nb^2
     const double rK = (double)(lay->n_pad - ga.row0) + extra_nonzero(ga.j0 + NB);
     return timed(2, (double)lay->batch * rK * NB * NB, 0.0, sp,
@@ -466,18 +484,22 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
     const int64_t t128 = rows / NB;
     if (c_hi < 0 || c_hi > t128) c_hi = t128;
     if (c_lo >= c_hi) return hipSuccess;
-    const int64_t w128 = c_hi - c_lo;
-    const int64_t tiles128 = w128 * (w128 + 1) / 2 + (t128 - c_hi) * w128;
-    const int tile = (tiles128 * lay->batch >= tn.upd_t128_min) ? 128 : 64;
-    const int64_t scale = NB / tile;
-    ga.nt = (int32_t)(rows / tile);
-    ga.c_lo = (int32_t)(c_lo * scale);
-    ga.c_hi = (int32_t)(c_hi * scale);
-    ga.band = (int32_t)std::max<int64_t>(0, tn.upd_band);
     if (eye) {  // identity rows t >= j0 + kdepth are zero in the panel columns
       ga.zlo = lay->n_pad + j0 + kdepth;
       ga.zhi = lay->y_row;
     }
+    set_band(ga, 128);
+    const int64_t w128 = compress(ga, c_hi) - compress(ga, c_lo);
+    if (w128 <= 0) return hipSuccess;
+    const int64_t tiles128 = w128 * (w128 + 1) / 2 + (compress(ga, t128) - compress(ga, c_hi)) * w128;
+    const int tile = (tiles128 * lay->batch >= tn.upd_t128_min) ? 128 : 64;
+    const int64_t scale = NB / tile;
+    ga.bz0 = ga.bzn = 0;
+    set_band(ga, tile);
+    ga.nt = (int32_t)compress(ga, rows / tile);
+    ga.c_lo = (int32_t)compress(ga, c_lo * scale);
+    ga.c_hi = (int32_t)compress(ga, c_hi * scale);
+    ga.band = (int32_t)std::max<int64_t>(0, tn.upd_band);
     // algorithmic flops: 2 kdepth x (lower-triangle elements in the column range of the rows that
     // are nonzero in the panel: the K part, then the extra rows, which follow it contiguously)
     const double rK = (double)(lay->n_pad - ga.row0) + extra_nonzero(j0 + kdepth);
@@ -1084,6 +1106,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "diag_version")) slot = &t.diag_version;
   else if (!strcmp(key, "ingroup")) slot = &t.ingroup;
   else if (!strcmp(key, "rl_max_tiles")) slot = &t.rl_max_tiles;
+  else if (!strcmp(key, "band_skip")) slot = &t.band_skip;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -65,6 +65,9 @@ struct GemmArgs {
   // rows [zlo, zhi) are structurally zero in the panel columns [j0, j0 + kdepth) (identity extra
   // rows: row n_pad + t of E L^-T is zero left of column t); tiles inside the range are skipped
   int64_t zlo, zhi;
+  // tiles [bz0, bz0 + bzn) (launch-tile units from row0) lie inside [zlo, zhi): the grid enumerates the
+  // remaining tiles only -- tile index t >= bz0 stands for t + bzn (rows and, for the update, columns)
+  int32_t bz0, bzn;
   // ragged batches (NULL: uniform): member b's training rows nb[b] .. n_pad-1 are identity rows and
   // its test rows n_pad + mb[b] .. y_row-1 zero rows; tiles of rows that are zero in the panel are skipped
   const int64_t* nb;

@@ -224,6 +224,10 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
     ti = t;
     tj = 0;
   }
+  if (a.bzn) {  // skip the band of structurally zero tiles (the grid does not enumerate it)
+    if (ti >= a.bz0) ti += a.bzn;
+    if (MODE == GEMM_UPDATE && tj >= a.bz0) tj += a.bzn;
+  }
   T* W = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs;
   const int64_t R = a.row0 + ti * TM;
   // structurally zero operand rows: the product (and so the update / solve) of the tile is zero

@@ -325,7 +325,9 @@ int gpk_timing_reset(void);
  * the y row), "upd_t128_min", "trsm_t128_min" (128-tile thresholds), "diag_version" (2: look-ahead
  * diagonal-block kernel, 1: the phase-serial one; bitwise identical results), "ingroup" (in-group
  * updates: 0 auto, 1 left-looking, 2 right-looking, 3 two-level left-looking) with "rl_max_tiles"
- * (auto picks right-looking while batch x block rows stays below it, two-level otherwise).
+ * (auto picks right-looking while batch x block rows stays below it, two-level otherwise),
+ * "band_skip" (1: with identity extra rows, the grid leaves out the tiles of the structurally zero
+ * band instead of launching them to exit at once).
  * Stores the value and returns the previous one through *old (may be NULL); 0 or -1 (unknown
  * key).  Defaults come from the environment (GPK_LOOKAHEAD, GPK_RESERVE_CUS, ...). */
 int gpk_tune(const char* key, int64_t value, int64_t* old);

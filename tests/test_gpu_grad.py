@@ -135,3 +135,41 @@ def test_gradient_under_every_in_group_schedule(mode):
         assert abs(float(f.nlml()[0]) - nl_ref) <= 1e-9 * abs(nl_ref)
     finally:
         engine.nat.tune("ingroup", old)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [2, 3])
+def test_zero_band_skip_is_bitwise_neutral(mode):
+    """Leaving the zero band's tiles out of the grid (band_skip, the default) changes which workgroups
+    exist, not what any tile computes: K^-1, the gradient and the -LML match the full grid bit for bit,
+    for a batch (two-level in-group schedule) and a single member (right-looking)."""
+    x, y = o.make_inputs("C1", n=1300, seed=13)
+    g = build_gp(SE, x, y)
+    batch = 3 if mode == 3 else 1
+    hyp = [0.08] if batch == 1 else None
+    res = {}
+    old_mode = engine.nat.tune("ingroup", mode)
+    try:
+        for skip in (0, 1):
+            old = engine.nat.tune("band_skip", skip)
+            try:
+                if batch == 1:
+                    f = g.covariance_matrix.inverse_factorization(hyp_list(hyp), torch.tensor(1e-2, dtype=torch.float64))
+                    res[skip] = (f.k_inv(0).cpu().numpy().copy(), f.gradient().cpu().numpy().copy(),
+                                 f.nlml().cpu().numpy().copy())
+                else:
+                    kd = engine.kernel_descriptor(make_kernel(SE, 1), 1)
+                    dev = engine.device()
+                    X = torch.tensor(x, dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+                    Y = torch.tensor(y, dtype=torch.float64, device=dev).reshape(1, -1).contiguous()
+                    H = torch.tensor([[0.06], [0.1], [0.14]], dtype=torch.float64, device=dev)
+                    NZ = torch.tensor([1e-2], dtype=torch.float64, device=dev)
+                    f = engine.InverseFactorization(len(x), 1, batch).run(kd, H, 1, NZ, 0, X, 0, Y, 0)
+                    res[skip] = (f.k_inv(2).cpu().numpy().copy(), f.gradient().cpu().numpy().copy(),
+                                 f.nlml().cpu().numpy().copy())
+            finally:
+                engine.nat.tune("band_skip", old)
+    finally:
+        engine.nat.tune("ingroup", old_mode)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
