@@ -147,6 +147,7 @@ struct Tune {
   int64_t ingroup;        // in-group updates: 1 left-looking, 2 right-looking, 3 two-level, 0 auto (by batch)
   int64_t rl_max_tiles;   // auto: right-looking while batch x (block rows) stays below this
   int64_t band_skip;      // identity extra rows: leave the zero band's tiles out of the grid
+  int64_t group_eye;      // panels per trailing update of identity-augmented factorisations
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -161,7 +162,8 @@ Tune& tune() {
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
                          env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0),
                          env_i64("GPK_DIAG_VERSION", 2), env_i64("GPK_INGROUP", 0),
-                         env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1)};
+                         env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1),
+                         env_i64("GPK_GROUP_EYE", 4)};
   return t;
 }
 
@@ -523,7 +525,9 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // panel chain).  A deeper K halves the read-modify-write passes over the trailing matrix per
   // doubling of G.  The first group has G0 <= G panels: its chain is exposed (nothing to overlap
   // yet), so a short one lets the first bulk update start early.
-  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tn.group, 16));
+  // identity-augmented (gradient / inverse) factorisations: groups of group_eye panels -- their
+  // trailing matrix carries the K^-1 corner, and 4-panel groups measured faster there at every batch
+  const int64_t G = std::max<int64_t>(1, std::min<int64_t>(eye ? tn.group_eye : tn.group, 16));
   const int64_t G0 = std::max<int64_t>(1, std::min<int64_t>(tn.group_first, G));
   if (la) {
     GPK_HIP(hipEventRecord(ss->fork, s), "event");
@@ -1107,6 +1111,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "ingroup")) slot = &t.ingroup;
   else if (!strcmp(key, "rl_max_tiles")) slot = &t.rl_max_tiles;
   else if (!strcmp(key, "band_skip")) slot = &t.band_skip;
+  else if (!strcmp(key, "group_eye")) slot = &t.group_eye;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -70,11 +70,11 @@ def test_autograd_backward_uses_device_gradient():
 
 
 def test_gradient_at_multi_group_sizes_and_inverse():
-    """n spans several 4-panel groups with a ragged end (the zero-tile skipping of the identity
-    rows is exercised on every schedule variant); K^-1 and L^-1 against numpy."""
+    """n spans several panel groups (group_eye 1 / 3 / 4 / 8) with a ragged end (the zero-tile skipping of
+    the identity rows is exercised on every schedule variant); K^-1 and L^-1 against numpy."""
     x, y = o.make_inputs("C1", n=1100, seed=11)
-    for group in (1, 3, 4):
-        old = engine.nat.tune("group", group)
+    for group in (1, 3, 4, 8):
+        old = engine.nat.tune("group_eye", group)
         try:
             f = build_gp(SE, x, y).covariance_matrix.inverse_factorization(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64))
             Kn = o.k_noised(SE, [0.1], 1e-2, x)
@@ -89,7 +89,7 @@ def test_gradient_at_multi_group_sizes_and_inverse():
             g = f.gradient()[0].cpu().numpy()
             _check_grad([g[:1], g[1]], [g_ref[0], gn_ref])
         finally:
-            engine.nat.tune("group", old)
+            engine.nat.tune("group_eye", old)
 
 
 def test_batched_gradient_members_are_independent():
