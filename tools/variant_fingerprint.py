@@ -40,5 +40,6 @@ def case(n, m, batch, ingroup):
 
 
 if __name__ == "__main__":
-    for args in [(4096, 0, 8, 0), (8192, 0, 16, 3), (3000, 200, 4, 1), (2048, 0, 1, 2)]:
+    for args in [(4096, 0, 8, 0), (8192, 0, 16, 3), (3000, 200, 4, 1), (2048, 0, 1, 2), (4096, 0, 1, 0),
+                 (3000, 200, 2, 2), (1300, 0, 3, 2)]:
         print(case(*args), flush=True)
