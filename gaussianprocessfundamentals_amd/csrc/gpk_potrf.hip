@@ -14,7 +14,7 @@
 // Tiles are TM x TN (128 x 128 while the grid fills the chip, 64 x 64 on small trailing
 // matrices); a 256-thread workgroup = 2 x 2 waves, double-buffered LDS staging of 16-deep K
 // chunks through registers; block ids are remapped so that each XCD (blockIdx % 8) walks runs of
-// consecutive tiles, which share panel rows in its L2.
+// consecutive tiles, which share panel rows in its L2 (xcd_remap).
 #include <math.h>
 
 #include "gpk_internal.h"
@@ -67,20 +67,19 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int ROWB = 128;  // bytes of one row of a staged K chunk (8 pieces of 16 B)
 
-// bijective XCD-aware remap of the hardware block order (XCD = blockIdx % 8) to logical tiles
-// Runs of GPK_XCD_RUN consecutive tiles are dealt round-robin over the XCDs (0: one contiguous run per
-// XCD).  Runs of 8 keep each XCD's tiles sharing panel rows in its L2 and spread clusters of
-// structurally zero tiles (ragged members' padding) over all XCDs: ragged 1 x 8192 + 15 x 4096
-// 18.0 -> 16.2 ms, uniform batches unchanged (profiles/r02y_xcd_runs.txt).
-#ifndef GPK_XCD_RUN
-#define GPK_XCD_RUN 8
-#endif
-__device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk) {
-  if (GPK_XCD_RUN > 0) {
-    const int64_t full = nblk - nblk % (8 * GPK_XCD_RUN);
+// bijective XCD-aware remap of the hardware block order (XCD = blockIdx % 8) to logical tiles.
+// run = 0: each XCD walks one contiguous run of tile ids, which share panel rows in its L2 (uniform
+// batches: the fewest L2 misses).  run > 0: runs of that many consecutive tiles are dealt round-robin
+// over the XCDs -- ragged batches, whose members' padding makes contiguous clusters of structurally
+// zero tiles that would otherwise leave some XCDs idle: 1 x 8192 + 15 x 4096 members 18.0 -> 16.2 ms;
+// on uniform batches runs of 8 are neutral in time but raise the update's L2 misses by 7-13 %
+// (profiles/r02y_xcd_runs.txt).
+__device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nblk, int64_t run) {
+  if (run > 0) {
+    const int64_t full = nblk - nblk % (8 * run);
     if (bid >= full) return bid;
     const int64_t x = bid % 8, pos = bid / 8;
-    return ((pos / GPK_XCD_RUN) * 8 + x) * GPK_XCD_RUN + pos % GPK_XCD_RUN;
+    return ((pos / run) * 8 + x) * run + pos % run;
   }
   const int64_t q = nblk / 8, r = nblk % 8;
   const int64_t x = bid % 8, pos = bid / 8;
@@ -185,7 +184,7 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   const int b = blockIdx.y;
-  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x, a.nb != nullptr ? 8 : 0);
   int64_t ti, tj;  // tile coordinates in units of TM (rows) and TN (cols)
   // tiles in row-major lower-triangle order, or banded (a.band > 0, gpk_tune("upd_band"))
   if (MODE == GEMM_UPDATE) {
