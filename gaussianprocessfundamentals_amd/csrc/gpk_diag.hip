@@ -367,7 +367,7 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
 
   d4 xs = {0.0, 0.0, 0.0, 0.0};  // wave 0: X_{s+1} (operand layout) from QR_s, stored in P_{s+1}
 #pragma unroll 1
-  for (int s = 0; s < NTL; ++s) {
+  for (int s = 0; s < ((a.dbg & 16) ? 0 : NTL); ++s) {
     // ---------------------------------------------------------------- P_s
     if (wave == 0) {
       if (s > 0) {
@@ -436,6 +436,7 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
     __syncthreads();
   }
   // after P_7: block row 7 of L to HBM, rows 6 and 7 of L^-1
+  if (a.dbg & 32) return;  // timing ablation
   if (wave >= 1) {
     inverse_tile(A, Dinv, Ib, NTL - 1, wave - 1, lr, lk);
   } else {

@@ -101,7 +101,8 @@ struct DiagArgs {
   int64_t j0;
   int64_t kblk;
   int32_t* info;
-  int32_t dbg;  // timing-only ablations (GPK_DIAG_DEBUG): 1 no inverse, 2 no potf2, 4 no tile ops
+  int32_t dbg;  // timing-only ablations (GPK_DIAG_DEBUG): 1 no inverse, 2 no potf2, 4 no tile ops,
+                // 8 no stores, 16 no step loop, 32 no final block row (diag2)
   int32_t version;  // 2: look-ahead schedule (default), 1: the phase-serial kernel (A/B measurements)
 };
 

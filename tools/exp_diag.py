@@ -3,7 +3,7 @@
 usage: python tools/exp_diag.py [batch] [n]
 Prints the average HIP-event span of the diag / trsm / update classes for the timing-only ablations
 of gpk_tune("diag_debug", v): 0 full, 1 no inverse, 2 no potf2, 4 no tile ops, 7 nothing but the
-block load / store.
+block load / store, 15 no stores either, 23 no step loop (load + final row), 63 load only.
 """
 import sys
 
@@ -29,7 +29,7 @@ def main():
     H = torch.full((batch, 1), 0.1, dtype=torch.float64, device=dev)
     NZ = torch.tensor([1e-2], dtype=torch.float64, device=dev)
     nat.tune("lookahead", 0)
-    for dbg in (0, 1, 2, 4, 7):
+    for dbg in (0, 1, 2, 4, 7, 15, 23, 63):
         nat.tune("diag_debug", dbg)
         f.run(kd, H, 1, NZ, 0, X, 0, Y, 0)
         torch.cuda.synchronize()
