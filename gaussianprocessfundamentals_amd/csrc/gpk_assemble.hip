@@ -67,6 +67,90 @@ __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs&
   }
 }
 
+// Interior tiles -- every row and column a training point of the member, no dense / E / identity
+// rows (all but the tiles along the block edges) -- with the dimension D a compile-time constant: the
+// lane's column point (and its ARD copy) is held in registers for its 16 rows, the row point is an LDS
+// broadcast, and the D loops unroll; one loop per base-kernel op, the op test hoisted out of it.  Same
+// formulas, operation order and contraction (gpk_kernels.h) as the generic path and the fused build,
+// so every path writes the same bits.
+template <typename TOut, int D, int OP>
+__device__ __forceinline__ void interior_single(FastNode fn, const double* prow, const double* pcol, int dp, int c,
+                                                int r0, int64_t gi0, int64_t gj, double noise, TOut* W, int64_t ld) {
+  double cb[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) cb[k] = pcol[fn.off + c * dp + k];
+  fn.op = OP;
+  fn.d = D;
+  for (int rr = r0; rr < ATILE; rr += 4) {
+    const double* pa = prow + fn.off + rr * dp;
+    double v = fast_value_at(fn, [pa](int k) { return pa[k]; }, [&cb](int k) { return cb[k]; });
+    const int64_t gi = gi0 + rr;
+    if (gi == gj) v += noise;
+    W[gi * ld + gj] = (TOut)v;
+  }
+}
+
+// trees whose base nodes read the raw points or ONE ARD slot (slot offset off1)
+template <typename TOut, int D>
+__device__ __forceinline__ void interior_tree(const gpk_kdesc& kd, const FastNode* fns, const double* prow,
+                                              const double* pcol, int off1, int dp, int c, int r0, int64_t gi0,
+                                              int64_t gj, double noise, TOut* W, int64_t ld) {
+  double cb0[D], cb1[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    cb0[k] = pcol[c * dp + k];
+    cb1[k] = pcol[off1 + c * dp + k];
+  }
+  for (int rr = r0; rr < ATILE; rr += 4) {
+    Stack st;
+    st.s0 = 0.0;
+    int sp = 0;
+    for (int q = 0; q < kd.n_nodes; ++q) {
+      const int op = kd.nodes[q].op;
+      if (op == GPK_OP_ADD || op == GPK_OP_MUL) {
+        const double top = st.get(sp - 1);
+        const double below = st.get(sp - 2);
+        st.set(sp - 2, op == GPK_OP_ADD ? below + top : below * top);
+        sp -= 1;
+      } else {
+        FastNode f = fns[q];
+        f.d = D;
+        const bool s1 = f.off != 0;
+        const double* pa = prow + f.off + rr * dp;
+        st.set(sp, fast_value_at(f, [pa](int k) { return pa[k]; },
+                                 [&cb0, &cb1, s1](int k) { return s1 ? cb1[k] : cb0[k]; }));
+        sp += 1;
+      }
+    }
+    double v = st.s0;
+    const int64_t gi = gi0 + rr;
+    if (gi == gj) v += noise;
+    W[gi * ld + gj] = (TOut)v;
+  }
+}
+
+template <typename TOut, int D>
+__device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& fn, const FastNode* fns, bool fast,
+                                           const double* prow, const double* pcol, int slot_stride, int dp, int c,
+                                           int r0, int64_t gi0, int64_t gj, double noise, TOut* W, int64_t ld) {
+  if (fast) {
+    switch (fn.op) {
+      case GPK_OP_SE: interior_single<TOut, D, GPK_OP_SE>(fn, prow, pcol, dp, c, r0, gi0, gj, noise, W, ld); return true;
+      case GPK_OP_PER: interior_single<TOut, D, GPK_OP_PER>(fn, prow, pcol, dp, c, r0, gi0, gj, noise, W, ld); return true;
+      case GPK_OP_MAT32: interior_single<TOut, D, GPK_OP_MAT32>(fn, prow, pcol, dp, c, r0, gi0, gj, noise, W, ld); return true;
+      case GPK_OP_MAT52: interior_single<TOut, D, GPK_OP_MAT52>(fn, prow, pcol, dp, c, r0, gi0, gj, noise, W, ld); return true;
+      default: return false;
+    }
+  }
+  if (kd.n_ard > 1 || kd.n_nodes > 8) return false;
+  interior_tree<TOut, D>(kd, fns, prow, pcol, slot_stride, dp, c, r0, gi0, gj, noise, W, ld);
+  return true;
+}
+
+#ifndef GPK_ASM_INTERIOR
+#define GPK_ASM_INTERIOR 1
+#endif
+
 template <typename TOut>
 __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -146,6 +230,18 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   const bool fast = kd.n_nodes == 1;
   FastNode fn = make_fast_node(kd.nodes[0], hyp_s, a.d);
   fn.off = fast_off(kd, slot_stride);
+  if (GPK_ASM_INTERIOR && a.A == nullptr && gi0 + ATILE <= nm) {  // lower tiles: gj0 <= gi0
+    bool done = false;
+    switch (a.d) {
+      case 1: done = interior_d<TOut, 1>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 2: done = interior_d<TOut, 2>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 3: done = interior_d<TOut, 3>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 4: done = interior_d<TOut, 4>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 8: done = interior_d<TOut, 8>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      default: break;
+    }
+    if (done) return;
+  }
 #ifndef GPK_ASM_UNROLL
 #define GPK_ASM_UNROLL 1
 #endif

@@ -1,5 +1,8 @@
 // Device evaluation of the kernel program (shared by the K build in gpk_assemble.hip and the
 // fused first trailing update in gpk_potrf.hip).  Reference formulas: see gpk_assemble.hip.
+// Multiply-adds are contracted within a source expression only (fp contract(on)): with hipcc's
+// default (fast) the fusions across statements depend on the inlining context, so the K build's
+// interior / edge loops and the fused build would round a few elements differently.
 #pragma once
 
 #include <math.h>
@@ -18,6 +21,7 @@ constexpr double PI = 3.141592653589793;
 template <int R>
 __device__ __forceinline__ void base_values(const gpk_node& nd, const double* __restrict__ hyp,
                                             const double* const (&a)[R], const double* b, int d, double (&r)[R]) {
+#pragma clang fp contract(on)  // fuse within an expression only: every caller rounds alike
   const int fl = nd.flags;
   const bool ard = (fl & GPK_NODE_ARD) != 0;
   const double* h = hyp + nd.hyp_offset;
@@ -193,6 +197,7 @@ __device__ __forceinline__ FastNode make_fast_node(const gpk_node& nd, const dou
 // [0, pi/2] (truncation <= 2.6e-16): about a third of the library sin's work, with no quadrant
 // branches.  The phase error of t itself, |t| ulp, is the reference formula's as well.
 __device__ __forceinline__ double sin2_pi(double t) {
+#pragma clang fp contract(on)  // fuse within an expression only: every caller rounds alike
   const double f = t - floor(t);
   const double g = fmin(f, 1.0 - f);
   const double x = PI * g;
@@ -213,6 +218,7 @@ __device__ __forceinline__ double sin2_pi(double t) {
 // fast_value over coordinate accessors: a(k), b(k) return coordinate k of the two points
 template <typename PA, typename PB>
 __device__ __forceinline__ double fast_value_at(const FastNode& f, PA a, PB b) {
+#pragma clang fp contract(on)  // fuse within an expression only: every caller rounds alike
   const int d = f.d;
   double r;
   if (f.op == GPK_OP_SE) {
