@@ -25,6 +25,10 @@
 namespace gpk {
 namespace {
 
+#ifndef GPK_ASM_ABLATE
+#define GPK_ASM_ABLATE 0  // timing-only: 1 skips the kernel evaluation (wrong results)
+#endif
+
 enum { CLS_TRAIN = 0, CLS_PAD = 1, CLS_TEST = 2, CLS_Y = 3, CLS_ZERO = 4 };
 
 // row / column class of index g for a member with n training and m test points
@@ -67,6 +71,13 @@ __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs&
   }
 }
 
+#ifndef GPK_ASM_INTERIOR_TREE
+#define GPK_ASM_INTERIOR_TREE 1  // trees of base nodes on the interior path too
+#endif
+#ifndef GPK_ASM_INTERIOR
+#define GPK_ASM_INTERIOR 1  // 0: every tile through the generic loop (A/B)
+#endif
+
 // Interior tiles -- every row and column a training point of the member, no dense / E / identity
 // rows (all but the tiles along the block edges) -- with the dimension D a compile-time constant: the
 // lane's column point (and its ARD copy) is held in registers for its 16 rows, the row point is an LDS
@@ -83,7 +94,7 @@ __device__ __forceinline__ void interior_single(FastNode fn, const double* prow,
   fn.d = D;
   for (int rr = r0; rr < ATILE; rr += 4) {
     const double* pa = prow + fn.off + rr * dp;
-    double v = fast_value_at(fn, [pa](int k) { return pa[k]; }, [&cb](int k) { return cb[k]; });
+    double v = GPK_ASM_ABLATE ? 0.0 : fast_value_at(fn, [pa](int k) { return pa[k]; }, [&cb](int k) { return cb[k]; });
     const int64_t gi = gi0 + rr;
     if (gi == gj) v += noise;
     W[gi * ld + gj] = (TOut)v;
@@ -129,7 +140,7 @@ __device__ __forceinline__ void interior_tree(const gpk_kdesc& kd, const FastNod
   }
 }
 
-template <typename TOut, int D>
+template <typename TOut, int D, bool TREE>
 __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& fn, const FastNode* fns, bool fast,
                                            const double* prow, const double* pcol, int slot_stride, int dp, int c,
                                            int r0, int64_t gi0, int64_t gj, double noise, TOut* W, int64_t ld) {
@@ -142,16 +153,15 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
       default: return false;
     }
   }
-  if (kd.n_ard > 1 || kd.n_nodes > 8) return false;
+  if (!TREE || GPK_ASM_INTERIOR_TREE == 0 || kd.n_ard > 1 || kd.n_nodes > 8) return false;
   interior_tree<TOut, D>(kd, fns, prow, pcol, slot_stride, dp, c, r0, gi0, gj, noise, W, ld);
   return true;
 }
 
-#ifndef GPK_ASM_INTERIOR
-#define GPK_ASM_INTERIOR 1
-#endif
 
-template <typename TOut>
+// TREE: the instantiation for kernel trees (its interior loop holds two column points in registers;
+// single-node kernels get the lighter instantiation and keep four waves per SIMD)
+template <typename TOut, bool TREE>
 __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int slot_stride = ATILE * a.dp;
@@ -233,11 +243,11 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   if (GPK_ASM_INTERIOR && a.A == nullptr && gi0 + ATILE <= nm) {  // lower tiles: gj0 <= gi0
     bool done = false;
     switch (a.d) {
-      case 1: done = interior_d<TOut, 1>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
-      case 2: done = interior_d<TOut, 2>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
-      case 3: done = interior_d<TOut, 3>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
-      case 4: done = interior_d<TOut, 4>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
-      case 8: done = interior_d<TOut, 8>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 1: done = interior_d<TOut, 1, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 2: done = interior_d<TOut, 2, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 3: done = interior_d<TOut, 3, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 4: done = interior_d<TOut, 4, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 8: done = interior_d<TOut, 8, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
       default: break;
     }
     if (done) return;
@@ -262,9 +272,6 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
       v = (gj <= gi) ? Ab[gi * a.a_ld + gj] : Ab[gj * a.a_ld + gi];
       if (gi == gj) v += noise;
     } else if ((rcls == CLS_TRAIN || rcls == CLS_TEST) && col_kernel) {
-#ifndef GPK_ASM_ABLATE
-#define GPK_ASM_ABLATE 0  // timing-only: 1 skips the kernel evaluation (wrong results)
-#endif
       if (!GPK_ASM_ABLATE)
         v = fast ? fast_value(fn, prow + fn.off + rr * a.dp, pcol + fn.off + c * a.dp)
                  : eval_tree_fast(kd, fns, prow + rr * a.dp, pcol + c * a.dp);
@@ -600,10 +607,18 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
   } else {
     grid = dim3((unsigned)(a.ntile * (a.ntile + 1) / 2), (unsigned)batch, 1);
   }
-  if (dtype == GPK_F64)
-    hipLaunchKernelGGL(assemble_kernel<double>, grid, dim3(256), lds, s, kd, a);
-  else
-    hipLaunchKernelGGL(assemble_kernel<float>, grid, dim3(256), lds, s, kd, a);
+  const bool tree = kd.n_nodes > 1;
+  if (dtype == GPK_F64) {
+    if (tree)
+      hipLaunchKernelGGL((assemble_kernel<double, true>), grid, dim3(256), lds, s, kd, a);
+    else
+      hipLaunchKernelGGL((assemble_kernel<double, false>), grid, dim3(256), lds, s, kd, a);
+  } else {
+    if (tree)
+      hipLaunchKernelGGL((assemble_kernel<float, true>), grid, dim3(256), lds, s, kd, a);
+    else
+      hipLaunchKernelGGL((assemble_kernel<float, false>), grid, dim3(256), lds, s, kd, a);
+  }
   return hipGetLastError();
 }
 
