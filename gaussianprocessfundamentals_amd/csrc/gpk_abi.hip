@@ -148,6 +148,7 @@ struct Tune {
   int64_t rl_max_tiles;   // auto: right-looking while batch x (block rows) stays below this
   int64_t band_skip;      // identity extra rows: leave the zero band's tiles out of the grid
   int64_t group_eye;      // panels per trailing update of identity-augmented factorisations
+  int64_t asm_generic;    // K build: interior tiles through the generic loop too (A/B; bitwise equal)
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -163,7 +164,7 @@ Tune& tune() {
                          env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0),
                          env_i64("GPK_DIAG_VERSION", 2), env_i64("GPK_INGROUP", 0),
                          env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1),
-                         env_i64("GPK_GROUP_EYE", 4)};
+                         env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0)};
   return t;
 }
 
@@ -293,6 +294,7 @@ static int assemble_impl(const gpk_kdesc* kd, const gpk_layout* lay, const doubl
   if (!W) return fail_arg(15, "W");
   AsmArgs a;
   memset(&a, 0, sizeof(a));
+  a.generic = tune().asm_generic != 0 ? 1 : 0;
   a.hyp = hyp_dev;
   a.hyp_stride = hyp_stride;
   a.noise = noise_dev;
@@ -1112,6 +1114,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "rl_max_tiles")) slot = &t.rl_max_tiles;
   else if (!strcmp(key, "band_skip")) slot = &t.band_skip;
   else if (!strcmp(key, "group_eye")) slot = &t.group_eye;
+  else if (!strcmp(key, "asm_generic")) slot = &t.asm_generic;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   const bool fast = kd.n_nodes == 1;
   FastNode fn = make_fast_node(kd.nodes[0], hyp_s, a.d);
   fn.off = fast_off(kd, slot_stride);
-  if (GPK_ASM_INTERIOR && a.A == nullptr && gi0 + ATILE <= nm) {  // lower tiles: gj0 <= gi0
+  if (GPK_ASM_INTERIOR && !a.generic && a.A == nullptr && gi0 + ATILE <= nm) {  // lower tiles: gj0 <= gi0
     bool done = false;
     switch (a.d) {
       case 1: done = interior_d<TOut, 1, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;

@@ -40,6 +40,7 @@ struct AsmArgs {
   double diag_add;   // plain mode
   int32_t eye;       // augmented: the m extra rows are the identity (E = I, m == n), zero corner
   int64_t tcol_hi;   // augmented: > 0 builds only the tiles of 64-tile columns [0, tcol_hi) (all rows below)
+  int32_t generic;   // 1: interior tiles too through the generic per-element loop (bitwise A/B of the fast one)
   // ragged batches (NULL: every member uses n / m): member b uses its first nb[b] training points
   // (rows nb[b] .. n_pad-1 become identity rows) and its first mb[b] test points (zero rows after)
   const int64_t* nb;

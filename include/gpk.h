@@ -328,7 +328,9 @@ int gpk_timing_reset(void);
  * (auto picks right-looking while batch x block rows stays below it, two-level otherwise),
  * "band_skip" (1: with identity extra rows, the grid leaves out the tiles of the structurally zero
  * band instead of launching them to exit at once), "group_eye" (panels per trailing update of the
- * identity-augmented factorisations, gpk_potrf_aug_ex / gpk_nlml_grad; "group" for the others).
+ * identity-augmented factorisations, gpk_potrf_aug_ex / gpk_nlml_grad; "group" for the others),
+ * "asm_generic" (1: the K build's interior tiles through the generic per-element loop as well; the
+ * same bits, slower -- for A/B checks).
  * Stores the value and returns the previous one through *old (may be NULL); 0 or -1 (unknown
  * key).  Defaults come from the environment (GPK_LOOKAHEAD, GPK_RESERVE_CUS, ...). */
 int gpk_tune(const char* key, int64_t value, int64_t* old);
