@@ -1,4 +1,5 @@
-"""The sharded sweep under torch.distributed with the gloo backend, world size 2 (CPU).
+"""The sharded sweep under torch.distributed with the gloo backend, world sizes 1, 2, 3 and 8 (CPU; SURVEY §4
+plans 1-8): contiguous shards including uneven and empty ones.
 
 The per-rank evaluator here is the CPU oracle (test infrastructure), injected explicitly; the
 product's default evaluator is the native batched device path (tested on the GPU)."""
@@ -6,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -48,15 +50,16 @@ def _worker(rank, world, port, out_q):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_sweep_matches_serial():
-    world = 2
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_gloo_sweep_matches_serial(world):
+    from gaussianprocessfundamentals_amd.sweep import shard_range
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=180) for _ in range(world)]
+    res = [q.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -67,4 +70,5 @@ def test_gloo_world2_sweep_matches_serial():
         np.testing.assert_allclose(nlml, exp, rtol=1e-12)
         assert info == [0] * 13
         assert best == int(np.argmin(exp))
-    assert res[0][4] == [7] and res[1][4] == [6]   # contiguous shards 7 + 6
+        a, b = shard_range(13, rank, world)
+        assert calls == [b - a]   # contiguous shards: 7 + 6 at world 2, 5 + 4 + 4 at 3, 2 2 2 2 2 1 1 1 at 8
