@@ -1,5 +1,5 @@
 """The sharded sweep under torch.distributed with the gloo backend, world sizes 1, 2, 3 and 8 (CPU; SURVEY §4
-plans 1-8): contiguous shards including uneven and empty ones.
+plans 1-8): contiguous, uneven shards.
 
 The per-rank evaluator here is the CPU oracle (test infrastructure), injected explicitly; the
 product's default evaluator is the native batched device path (tested on the GPU)."""
