@@ -63,7 +63,8 @@ def parse():
                     help="factorisation buffers / streams that consecutive steps rotate over (overlap of batches); "
                          "default %d for the metric config, 3 otherwise" % DEFAULT_PIPELINE_METRIC)
     ap.add_argument("--lookahead", type=int, default=None,
-                    help="panel look-ahead on side streams (default: on, off when --pipeline > 1)")
+                    help="panel look-ahead on side streams: 1 on, 0 off, 2 auto (libgpk: off below 48 128-blocks "
+                         "of the augmented matrix); default 2, 0 when --pipeline > 1")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events")
@@ -275,7 +276,7 @@ def main():
     # trailing updates of the next (the batches are independent candidate sets of the sweep)
     P = max(1, args.pipeline if args.pipeline is not None else
             (DEFAULT_PIPELINE_METRIC if args.config == "metric" else 3))
-    la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 1)
+    la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 2)
     nat.tune("lookahead", la)
     if grad_mode:
         facts = [engine.InverseFactorization(n, d, batch, dt) for _ in range(P)]
@@ -418,7 +419,7 @@ def main():
                        "batches_in_flight": P,
                        "schedule": ("consecutive steps rotate over %d factorisation buffers on %d HIP streams (one "
                                     "batch's panel chain overlaps the next batch's trailing updates), panel "
-                                    "look-ahead %s" % (P, P, "on" if la else "off")),
+                                    "look-ahead %s" % (P, P, {0: "off", 1: "on"}.get(la, "auto"))),
                        "n": n, "d": d, "kernel": kname, "panel": int(lay.nb), "parallelism": "dp%d (independent candidates)" % world},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -135,7 +135,9 @@ struct Tune {
   int64_t upd_t128_min;   // 128 x 128 update tiles when at least this many (else 64 x 64)
   int64_t trsm_t128_min;  // 128-row panel-solve tiles when at least this many (else 64)
   int64_t diag_dbg;       // timing-only ablation flags of the diagonal kernel (never set in production)
-  int64_t lookahead;      // 1: panel chain on a high-priority side stream (default), 0: one stream
+  int64_t lookahead;      // 1: panel chain on a high-priority side stream, 0: one stream, 2: auto (default:
+                          // on for large matrices, see potrf_impl)
+  int64_t la_min_blocks;  // auto look-ahead: on from this many 128-blocks of the augmented matrix
   int64_t reserve_cus;    // CUs kept free of the bulk trailing update for the panel chain
   int64_t group;          // panels per trailing update (K = 128 group)
   int64_t group_first;    // panels of the first group (a short first chain lets the bulk start early)
@@ -149,6 +151,8 @@ struct Tune {
   int64_t band_skip;      // identity extra rows: leave the zero band's tiles out of the grid
   int64_t group_eye;      // panels per trailing update of identity-augmented factorisations
   int64_t asm_generic;    // K build: interior tiles through the generic loop too (A/B; bitwise equal)
+  int64_t panel_stream;   // look-ahead panel chain: 0 high-priority side stream, 1 caller's stream,
+                          // 2 normal-priority side stream
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -158,13 +162,14 @@ int64_t env_i64(const char* name, int64_t dflt) {
 
 Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
-                         env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 1),
+                         env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 2), env_i64("GPK_LA_MIN_BLOCKS", 48),
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
                          env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0),
                          env_i64("GPK_DIAG_VERSION", 2), env_i64("GPK_INGROUP", 0),
                          env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1),
-                         env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0)};
+                         env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0),
+                         env_i64("GPK_PANEL_STREAM", 0)};
   return t;
 }
 
@@ -173,7 +178,7 @@ Tune& tune() {
 // diagonal-block kernel -- one workgroup of 150 KB LDS per batch member -- never waits for a CU
 // to drain) and the fork / join events of gpk_potrf_aug; created on first use.
 struct SideStream {
-  hipStream_t panel_s = nullptr, bulk_s = nullptr;
+  hipStream_t panel_s = nullptr, bulk_s = nullptr, panel_np = nullptr;
   hipEvent_t fork = nullptr, panel = nullptr, bulk = nullptr, join_p = nullptr, join_b = nullptr;
 };
 
@@ -188,10 +193,12 @@ void release_side_streams() {
   for (SideStream* ss : g_side_all) {
     if (ss->panel_s) hipStreamSynchronize(ss->panel_s);
     if (ss->bulk_s) hipStreamSynchronize(ss->bulk_s);
+    if (ss->panel_np) hipStreamSynchronize(ss->panel_np);
     for (hipEvent_t e : {ss->fork, ss->panel, ss->bulk, ss->join_p, ss->join_b})
       if (e) hipEventDestroy(e);
     if (ss->panel_s) hipStreamDestroy(ss->panel_s);
     if (ss->bulk_s) hipStreamDestroy(ss->bulk_s);
+    if (ss->panel_np) hipStreamDestroy(ss->panel_np);
     *ss = SideStream();
   }
   g_side_all.clear();
@@ -218,6 +225,7 @@ SideStream* side_stream() {
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return nullptr;
     if (hipStreamCreateWithPriority(&ss.panel_s, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithFlags(&ss.panel_np, hipStreamNonBlocking) != hipSuccess) return nullptr;
     const int64_t r = std::max<int64_t>(0, std::min<int64_t>(tune().reserve_cus, ncu / 2));
     if (r > 0) {
       std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
@@ -382,13 +390,20 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // stream, the bulk of each trailing update on a CU-masked stream concurrently with the next
   // panel pair's chain; both fork from and join back into the caller's stream.
   // GPK_LOOKAHEAD=0 puts everything on the caller's stream.
-  const bool la = tn.lookahead != 0;
+  // Auto (2): on when the augmented matrix has at least la_min_blocks 128-blocks.  Below that the
+  // whole factorisation is faster on the caller's stream alone: each launch on the side streams costs
+  // ~5 us more than back to back on one queue, more than the overlap of the short trailing updates
+  // saves.  ms per call, look-ahead off / on (profiles/r02s_lookahead.txt): one member N = 1024
+  // 0.45 / 0.55, 2048 0.92 / 1.09, 4096 2.10 / 2.29, 6144 3.98 / 4.03, 8192 6.53 / 6.40, 12288
+  // 15.3 / 14.5; batches of 8 at N = 4096 5.13 / 5.26; the 128-candidate C4 sweep 52.7 / 54.2;
+  // -LML + gradient (identity rows: twice the width) N = 4096 3.44 / 3.28.
+  const bool la = tn.lookahead == 1 || (tn.lookahead == 2 && lay->p / NB >= tn.la_min_blocks);
   SideStream* ss = nullptr;
   if (la) {
     ss = side_stream();
     if (!ss) return fail_hip(hipErrorInvalidValue, "side stream");
   }
-  hipStream_t sp = la ? ss->panel_s : s;
+  hipStream_t sp = !la ? s : tn.panel_stream == 1 ? s : tn.panel_stream == 2 ? ss->panel_np : ss->panel_s;
   hipStream_t sb = la ? ss->bulk_s : s;
 
   // diagonal block k: factor + invert
@@ -1115,6 +1130,8 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "band_skip")) slot = &t.band_skip;
   else if (!strcmp(key, "group_eye")) slot = &t.group_eye;
   else if (!strcmp(key, "asm_generic")) slot = &t.asm_generic;
+  else if (!strcmp(key, "panel_stream")) slot = &t.panel_stream;
+  else if (!strcmp(key, "la_min_blocks")) slot = &t.la_min_blocks;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;
