@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <initializer_list>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -138,6 +139,9 @@ struct Tune {
   int64_t lookahead;      // 1: panel chain on a high-priority side stream, 0: one stream, 2: auto (default:
                           // on for large matrices, see potrf_impl)
   int64_t la_min_blocks;  // auto look-ahead: on from this many 128-blocks of the augmented matrix
+  int64_t fuse_trsm;      // f64: panel solve fused into the diagonal-block launch (1: look-ahead off only,
+                          // 2: always; one workgroup per
+  int64_t fuse_trsm_max;  //   64-row tile, each factoring the block) while batch x tiles <= fuse_trsm_max
   int64_t reserve_cus;    // CUs kept free of the bulk trailing update for the panel chain
   int64_t group;          // panels per trailing update (K = 128 group)
   int64_t group_first;    // panels of the first group (a short first chain lets the bulk start early)
@@ -163,6 +167,7 @@ int64_t env_i64(const char* name, int64_t dflt) {
 Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 2), env_i64("GPK_LA_MIN_BLOCKS", 48),
+                         env_i64("GPK_FUSE_TRSM", 1), env_i64("GPK_FUSE_TRSM_MAX", 256),
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
                          env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0),
@@ -239,6 +244,25 @@ SideStream* side_stream() {
       if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return nullptr;
   }
   return &ss;
+}
+
+// Ticket counters of the fused panel solve (DiagArgs::ctr), one block of kFuseCtr per (device,
+// stream): launches on one stream never overlap, and each launch's writer leaves its counters at 0.
+constexpr int kFuseCtr = 256;  // members per launch
+std::mutex g_ctr_mu;
+std::map<std::pair<int, hipStream_t>, int32_t*> g_ctr;
+
+int32_t* fuse_counters(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_ctr_mu);
+  auto it = g_ctr.find({dev, s});
+  if (it != g_ctr.end()) return it->second;
+  int32_t* p = nullptr;
+  if (hipMalloc(&p, kFuseCtr * sizeof(int32_t)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, kFuseCtr * sizeof(int32_t), s) != hipSuccess) return nullptr;
+  g_ctr[{dev, s}] = p;  // owned for the life of the process
+  return p;
 }
 
 }  // namespace
@@ -406,9 +430,27 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   hipStream_t sp = !la ? s : tn.panel_stream == 1 ? s : tn.panel_stream == 2 ? ss->panel_np : ss->panel_s;
   hipStream_t sb = la ? ss->bulk_s : s;
 
+  // extra rows that are nonzero in panel columns left of c: all test rows, or the identity rows
+  // t < c (row n_pad + t of E L^-T is zero left of column t)
+  auto extra_nonzero = [&](int64_t c) -> double {
+    return (double)(eye ? std::min<int64_t>(lay->m, c) : lay->m);
+  };
+  // Small grids (f64): the panel solve of block k runs inside the diagonal-block launch -- one
+  // workgroup per 64-row tile (plus the one that writes L and L^-1), each factoring the block
+  // redundantly (the chip is otherwise idle there) and solving its rows against L^-1 in LDS, bitwise
+  // the separate gemm<TRSM>; one launch fewer on the chain per panel.
+  auto fused_tiles = [&](int64_t k) -> int64_t {
+    const int64_t rows = lay->p - (k + 1) * NB;
+    if (dt != GPK_F64 || !tn.fuse_trsm || tn.diag_version == 1 || rows <= 0) return 0;
+    if (la && tn.fuse_trsm != 2) return 0;  // beside the look-ahead's bulk updates the extra workgroups
+                                             // cost more than the launch saves (N = 8192: 6.39 -> 6.43 ms)
+    const int64_t t64 = rows / 64;
+    return (t64 + 1) * lay->batch <= tn.fuse_trsm_max && lay->batch <= kFuseCtr ? t64 : 0;
+  };
   // diagonal block k: factor + invert
   auto diag = [&](int64_t k) -> hipError_t {
     DiagArgs da;
+    memset(&da, 0, sizeof(da));
     da.W = W;
     da.ld = lay->ld;
     da.w_bs = lay->w_batch_stride;
@@ -419,13 +461,22 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
     da.info = info_dev;
     da.dbg = (int32_t)tn.diag_dbg;
     da.version = (int32_t)tn.diag_version;
-    return timed(1, (double)lay->batch * NB * NB * NB / 3.0, 0.0, sp,
-                 [&] { return launch_diag(da, dt, lay->batch, sp); });
-  };
-  // extra rows that are nonzero in panel columns left of c: all test rows, or the identity rows
-  // t < c (row n_pad + t of E L^-T is zero left of column t)
-  auto extra_nonzero = [&](int64_t c) -> double {
-    return (double)(eye ? std::min<int64_t>(lay->m, c) : lay->m);
+    da.trsm_tiles = (int32_t)fused_tiles(k);
+    double flops = (double)lay->batch * NB * NB * NB / 3.0;
+    if (da.trsm_tiles > 0) {
+      da.row0 = (k + 1) * NB;
+      da.p = lay->p;
+      da.n_pad = lay->n_pad;
+      da.y_row = lay->y_row;
+      da.zlo = eye ? lay->n_pad + da.row0 : 0;  // identity rows t >= j0 + nb are still zero
+      da.zhi = eye ? lay->y_row : 0;
+      da.nb = n_dev;
+      da.mb = m_dev;
+      da.ctr = fuse_counters(sp);
+      if (!da.ctr) return hipErrorOutOfMemory;
+      flops += (double)lay->batch * ((double)(lay->n_pad - da.row0) + extra_nonzero(da.row0)) * NB * NB;
+    }
+    return timed(1, flops, 0.0, sp, [&] { return launch_diag(da, dt, lay->batch, sp); });
   };
   GemmArgs base;
   memset(&base, 0, sizeof(base));
@@ -455,6 +506,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   };
   // panel solve of block k: every row below the block (the y / test rows included)
   auto trsm = [&](int64_t k) -> hipError_t {
+    if (fused_tiles(k) > 0) return hipSuccess;  // solved by the diagonal-block launch
     GemmArgs ga = base;
     ga.Binv = static_cast<const char*>(Winv) + (size_t)k * NB * NB * es;
     ga.j0 = k * NB;
@@ -1132,6 +1184,8 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "asm_generic")) slot = &t.asm_generic;
   else if (!strcmp(key, "panel_stream")) slot = &t.panel_stream;
   else if (!strcmp(key, "la_min_blocks")) slot = &t.la_min_blocks;
+  else if (!strcmp(key, "fuse_trsm")) slot = &t.fuse_trsm;
+  else if (!strcmp(key, "fuse_trsm_max")) slot = &t.fuse_trsm_max;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -302,7 +302,8 @@ __device__ __forceinline__ void store_inv_diag(const double* Dinv, T* Ib, int I,
 
 // tile (I, J) of L^-1, J < I: -Dinv_I sum_{K=J}^{I-1} L_{I,K} Linv_{K,J}, stored transposed in tile (J, I)
 template <typename T>
-__device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, T* Ib, int I, int J, int lr, int lk) {
+__device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, T* Ib, int I, int J, int lr, int lk,
+                                             bool st = true) {
   d4 tacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 4; ++s)  // K = J: the diagonal tile Dinv_J
@@ -321,11 +322,28 @@ __device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, T* I
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     A[(J * DB + lr) * LDA + I * DB + lk + 4 * q] = out[q];
-    Ib[(I * DB + lk + 4 * q) * NB + J * DB + lr] = (T)out[q];
+    if (st) Ib[(I * DB + lk + 4 * q) * NB + J * DB + lr] = (T)out[q];
   }
 }
 
-template <typename T>
+// rows [r0, r1) of member b are zero in the panel columns [j0, j0 + 128) (gpk_potrf.hip's zero_rows
+// for a panel solve: identity extra rows past the panel, a ragged member's padding / unused test rows)
+__device__ __forceinline__ bool panel_zero_rows(const DiagArgs& a, int b, int64_t r0, int64_t r1) {
+  if (r0 >= a.zlo && r1 <= a.zhi) return true;
+  if (a.nb == nullptr) return false;
+  const int64_t npb = (a.nb[b] + NB - 1) / NB * NB;
+  const int64_t jend = a.j0 + NB;
+  if (a.j0 >= npb) return r0 >= jend && r1 <= a.p;
+  if (r0 >= (npb > jend ? npb : jend) && r1 <= a.n_pad) return true;
+  return a.mb != nullptr && r0 >= a.n_pad + a.mb[b] && r1 <= a.y_row;
+}
+
+// FUSE (f64): a workgroup with ticket t (DiagArgs) also solves the 64 rows R = row0 + 64 t .. +63 of the panel:
+// X = A L_kk^-T with the same MFMA k-order as gemm_kernel<TRSM> (k-step s of chunk kc takes k = 16 kc +
+// 2 q + 8 (s >> 1) + (s & 1) in lane group q; chunks kc > the column block skipped), so X is bitwise
+// the separate panel solve's.  Wave w: 16-row block w & 3, column blocks of half w >> 2 (balanced).  Its A operands (32
+// doubles per lane) are loaded during the last block row of the factorisation.
+template <typename T, bool FUSE>
 __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* A = sm;
@@ -338,9 +356,12 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15;
   const int lk = lane >> 4;
-  const int b = blockIdx.x;
+  const int b = FUSE ? blockIdx.y : blockIdx.x;
+  int* ticket = flag + 1;
   T* Wb = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs + a.j0 * a.ld + a.j0;
   T* Ib = reinterpret_cast<T*>(a.Winv) + (int64_t)b * a.inv_bs + a.kblk * NB * NB;
+  typedef double dbl2 __attribute__((ext_vector_type(2)));
+  dbl2 pa[FUSE ? NTL : 1][2];  // A operands: chunk kc, pieces lk and lk + 4 (k-steps 0, 1 and 2, 3)
   {
     // the lower 16-tiles of the block, 16 B per load, every load of a thread in flight at once
     constexpr int EPC = 16 / (int)sizeof(T);
@@ -364,6 +385,17 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   }
   if (tid == 0) *flag = 0;
   __syncthreads();
+  if (FUSE) {
+    // the whole block is in LDS (every load retired into the LDS stores above): draw the ticket
+    if (tid == 0) *ticket = atomicAdd(&a.ctr[b], 1);
+    __syncthreads();
+  }
+  // FUSE: the last workgroup to load writes (alone, so its HBM stores never sit in front of a tile's
+  // solve); the others solve tile = ticket
+  const int tk = FUSE ? *ticket : 0;
+  const bool wr = !FUSE || tk == (int)gridDim.x - 1;
+  const int64_t R = a.row0 + (int64_t)tk * 64;
+  const bool live = FUSE && !wr && !panel_zero_rows(a, b, R, R + 64);
 
   d4 xs = {0.0, 0.0, 0.0, 0.0};  // wave 0: X_{s+1} (operand layout) from QR_s, stored in P_{s+1}
 #pragma unroll 1
@@ -376,11 +408,11 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
       }
       if (!(a.dbg & 2)) potf2_tile(A, Dinv + s * DB * DB, colbuf, s, lane, flag, a.j0);  // timing ablation
     } else if (s == 0) {
-      if (!(a.dbg & 8)) store_inv_zeros(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
+      if (!(a.dbg & 8) && wr) store_inv_zeros(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
     } else {
       const int w = wave - 1;
       const int I = s - 1;
-      if (w < I && !(a.dbg & 1)) inverse_tile(A, Dinv, Ib, I, w, lr, lk);
+      if (w < I && !(a.dbg & 1)) inverse_tile(A, Dinv, Ib, I, w, lr, lk, wr);
       // trailing update of step s - 1 for tile columns j >= s + 1 (column s was done in QR_{s-1});
       // the last waves take the first tiles (waves 1..I hold an inverse tile)
       const int m = NTL - 1 - s;
@@ -400,7 +432,7 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + j * DB + lr] = acc[q];
       }
-      if (!(a.dbg & 8)) {
+      if (!(a.dbg & 8) && wr) {
         store_l_rows(A, Wb, a.ld, I, tid - 64, DT - 64);
         store_inv_diag(Dinv, Ib, I, tid - 64, DT - 64);
       }
@@ -437,35 +469,79 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   }
   // after P_7: block row 7 of L to HBM, rows 6 and 7 of L^-1
   if (a.dbg & 32) return;  // timing ablation
+  if (FUSE && live) {
+    // the panel rows' A operands, in flight during the last block row (held through the factorisation
+    // they would not fit beside its registers)
+    const double* Ar = reinterpret_cast<const double*>(a.W) + (int64_t)b * a.w_bs +
+                       (R + (wave & 3) * DB + lr) * a.ld + a.j0 + 2 * lk;
+#pragma unroll
+    for (int kc = 0; kc < NTL; ++kc) {
+      pa[kc][0] = *reinterpret_cast<const dbl2*>(Ar + kc * DB);
+      pa[kc][1] = *reinterpret_cast<const dbl2*>(Ar + kc * DB + 8);
+    }
+  }
   if (wave >= 1) {
-    inverse_tile(A, Dinv, Ib, NTL - 1, wave - 1, lr, lk);
-  } else {
+    inverse_tile(A, Dinv, Ib, NTL - 1, wave - 1, lr, lk, wr);
+  } else if (wr) {
     store_inv_diag(Dinv, Ib, NTL - 1, lane, 64);
   }
-  store_l_rows(A, Wb, a.ld, NTL - 1, tid, DT);
-  if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
+  if (wr) {
+    store_l_rows(A, Wb, a.ld, NTL - 1, tid, DT);
+    if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
+    if (FUSE && tid == 0) atomicExch(&a.ctr[b], 0);  // every other workgroup has drawn its ticket
+  }
+  if (!FUSE) return;
+  __syncthreads();  // block row 7 of L^-1 in LDS
+  if (!live) return;
+  // Linv[c][k] (c in tile I, k in tile J <= I): tile (J, I) of A transposed for J < I, Dinv_I for J = I
+  const int rb = wave & 3, ch = wave >> 2;
+  double* Xr = reinterpret_cast<double*>(a.W) + (int64_t)b * a.w_bs + (R + rb * DB + lk) * a.ld + a.j0 + lr;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    // column block = tile row I of L^-1; block cb takes cb + 1 chunks, so the halves {0, 7, 2, 5} and
+    // {1, 6, 3, 4} carry 18 chunks each (contiguous halves: 10 and 26)
+    const int cb = (n & 1) ? 7 - 2 * (n >> 1) - ch : 2 * (n >> 1) + ch;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kc = 0; kc < NTL; ++kc) {
+      if (kc > cb) break;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int x = 2 * lk + 8 * (st >> 1) + (st & 1);  // k within the chunk
+        const double bv = (kc < cb) ? A[(kc * DB + x) * LDA + cb * DB + lr] : Dinv[cb * DB * DB + lr * DB + x];
+        acc = mfma64(pa[kc][st >> 1][st & 1], bv, acc);
+      }
+    }
+    // C/D layout: col = lr, row = lk + 4 q
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Xr[(int64_t)(4 * q) * a.ld + cb * DB] = acc[q];
+  }
 }
 
 }  // namespace
 
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s) {
-  static bool attr_done[4] = {false, false, false, false};
+  static bool attr_done[5] = {false, false, false, false, false};
   const bool v2 = a.version != 1;
-  const void* fn = v2 ? (dtype == GPK_F64 ? reinterpret_cast<const void*>(diag2_kernel<double>)
-                                          : reinterpret_cast<const void*>(diag2_kernel<float>))
+  const bool fuse = v2 && dtype == GPK_F64 && a.trsm_tiles > 0;
+  const void* fn = fuse ? reinterpret_cast<const void*>(diag2_kernel<double, true>)
+                 : v2 ? (dtype == GPK_F64 ? reinterpret_cast<const void*>(diag2_kernel<double, false>)
+                                          : reinterpret_cast<const void*>(diag2_kernel<float, false>))
                       : (dtype == GPK_F64 ? reinterpret_cast<const void*>(diag_kernel<double>)
                                           : reinterpret_cast<const void*>(diag_kernel<float>));
-  bool& done = attr_done[(dtype == GPK_F64 ? 0 : 1) + (v2 ? 2 : 0)];
+  bool& done = attr_done[fuse ? 4 : (dtype == GPK_F64 ? 0 : 1) + (v2 ? 2 : 0)];
   if (!done) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DIAG_LDS_BYTES);
     if (e != hipSuccess) return e;
     done = true;
   }
-  if (v2) {
+  if (fuse) {
+    hipLaunchKernelGGL((diag2_kernel<double, true>), dim3(a.trsm_tiles + 1, batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+  } else if (v2) {
     if (dtype == GPK_F64)
-      hipLaunchKernelGGL(diag2_kernel<double>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+      hipLaunchKernelGGL((diag2_kernel<double, false>), dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
     else
-      hipLaunchKernelGGL(diag2_kernel<float>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+      hipLaunchKernelGGL((diag2_kernel<float, false>), dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
   } else if (dtype == GPK_F64) {
     hipLaunchKernelGGL(diag_kernel<double>, dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
   } else {

@@ -105,6 +105,19 @@ struct DiagArgs {
   int32_t dbg;  // timing-only ablations (GPK_DIAG_DEBUG): 1 no inverse, 2 no potf2, 4 no tile ops,
                 // 8 no stores, 16 no step loop, 32 no final block row (diag2)
   int32_t version;  // 2: look-ahead schedule (default), 1: the phase-serial kernel (A/B measurements)
+  // Fused panel solve (f64, diag2 only; 0: the diagonal block alone): trsm_tiles + 1 workgroups per
+  // member each factor the block like the plain kernel.  After loading the block every workgroup draws
+  // a ticket from ctr[b] (zero on entry): the last one to load writes L, L^-1 and info and resets the
+  // counter -- so no workgroup can still be reading the block when L overwrites it (workgroups of one
+  // launch may start far apart when other streams hold the CUs) -- and ticket t < trsm_tiles solves
+  // the 64 rows row0 + 64 t .. +63 of member b against its L^-1 in LDS; the gemm<TRSM> launch of that
+  // panel is then skipped.  Rows that are zero in the panel are skipped as in gemm<TRSM> (zlo / zhi,
+  // nb / mb).  ctr: per-stream device counters (launches on one stream never overlap).
+  int32_t trsm_tiles;
+  int64_t row0, p, n_pad, y_row, zlo, zhi;
+  const int64_t* nb;
+  const int64_t* mb;
+  int32_t* ctr;
 };
 
 struct FinArgs {
