@@ -28,10 +28,11 @@ sys.path.insert(0, HERE)
 
 PEAK = {"f64": 78.6, "f32": 157.3}   # TFLOP/s dense MFMA (AMD MI355X spec; microarch guide for f32)
 HBM_PEAK = 8000.0                      # GB/s spec
-# candidates per rank per step on the metric config, and batches in flight there: 32 x 2 (64 candidates,
-# 35 GB of augmented matrices) measured 347.9 evals/s against 337.8 for 16 x 3 (48 x 2: 350.5, 64 x 2:
-# 351.1) on one box -- larger launches of the short trailing updates at the end of the factorisation
-DEFAULT_BATCH = 32
+# candidates per rank per step on the metric config, and batches in flight there: 64 x 2 (128 candidates,
+# 71 GB of augmented matrices of the 288 GB) measured 352.3 / 351.7 evals/s against 348.4 / 349.3 for 32 x 2
+# and 350.9 / 351.4 for 48 x 2 (two alternating passes on one box, tools/batch_ab.sh); 16 x 3 337.8 --
+# larger launches of the short trailing updates at the end of each factorisation
+DEFAULT_BATCH = 64
 DEFAULT_PIPELINE_METRIC = 2
 
 CONFIGS = {

@@ -31,11 +31,14 @@ constexpr int LDS_COL = 2 * DB;  // potf2 column broadcast, double-buffered
 constexpr size_t DIAG_LDS_BYTES = sizeof(double) * (LDS_A + LDS_DINV + LDS_COL) + 16;
 
 // 1/sqrt(x) from the hardware estimate plus two Newton steps (~1 ulp); NaN for x < 0.
+#ifndef GPK_RSQ_NEWTON
+#define GPK_RSQ_NEWTON 2  // Newton steps after the hardware estimate (A/B builds only)
+#endif
 __device__ __forceinline__ double rsqrt_refined(double x) {
   double r = __builtin_amdgcn_rsq(x);
   const double h = 0.5 * x;
-  r = r * fma(-h * r, r, 1.5);
-  r = r * fma(-h * r, r, 1.5);
+#pragma unroll
+  for (int i = 0; i < GPK_RSQ_NEWTON; ++i) r = r * fma(-h * r, r, 1.5);
   return r;
 }
 

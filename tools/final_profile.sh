@@ -11,7 +11,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 gpurun_out/${tag}_tests.log
 rm -rf gpurun_out/pmc
 GPK_LOOKAHEAD=0 PMC_FILE=tools/pmc_traffic.txt bash tools/pmc_pass.sh || exit 1
-python tools/pmc_traffic.py metric_b32 gpurun_out/pmc profiles/pmc_traffic.json || exit 1
+python tools/pmc_traffic.py metric_b${BATCH:-64} gpurun_out/pmc profiles/pmc_traffic.json || exit 1
 cp profiles/pmc_traffic.json gpurun_out/${tag}_pmc_traffic.json
 mv gpurun_out/pmc gpurun_out/pmc_traffic_passes
 GPK_LOOKAHEAD=0 PMC_FILE=tools/pmc_groups.txt bash tools/pmc_pass.sh || exit 1
