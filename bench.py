@@ -33,6 +33,9 @@ HBM_PEAK = 8000.0                      # GB/s spec
 # and 350.9 / 351.4 for 48 x 2 (two alternating passes on one box, tools/batch_ab.sh); 16 x 3 337.8 --
 # larger launches of the short trailing updates at the end of each factorisation
 DEFAULT_BATCH = 64
+# --mode grad (identity-augmented, p ~ 2N: 2.2 GB per candidate at N = 8192): 16 x 2 (70 GB), 106.3 / 106.3
+# evals/s against 104.9 / 104.4 for 8 x 2 (two alternating passes on one box)
+DEFAULT_BATCH_GRAD = 16
 DEFAULT_PIPELINE_METRIC = 2
 
 CONFIGS = {
@@ -59,7 +62,8 @@ def parse():
     ap.add_argument("--n", type=int, default=None, help="override N")
     ap.add_argument("--batch", type=int, default=None,
                     help="hyperparameter candidates factorised together per rank per step "
-                         "(default: %d for the metric config, 1 otherwise)" % DEFAULT_BATCH)
+                         "(default: %d for the metric config, %d with --mode grad, 1 otherwise)"
+                         % (DEFAULT_BATCH, DEFAULT_BATCH_GRAD))
     ap.add_argument("--pipeline", type=int, default=None,
                     help="factorisation buffers / streams that consecutive steps rotate over (overlap of batches); "
                          "default %d for the metric config, 3 otherwise" % DEFAULT_PIPELINE_METRIC)
@@ -259,7 +263,8 @@ def main():
         batch = len(rows)
         chunk = -(-len(cands) // world)
     else:
-        batch = args.batch or (DEFAULT_BATCH if args.config == "metric" else 1)
+        batch = args.batch or ((DEFAULT_BATCH_GRAD if args.mode == "grad" else DEFAULT_BATCH)
+                               if args.config == "metric" else 1)
         chunk = batch
         # weak scaling: every rank evaluates its own `batch` candidates (a sweep over the first
         # hyperparameter: candidate c of rank r scales it by 1 + 0.01 (r * batch + c))
