@@ -69,3 +69,28 @@ def test_product_fails_loudly_without_gpu(lib):
         pytest.skip("GPU present")
     with pytest.raises(_native.NativeUnavailable):
         _native.lib()
+
+
+def test_tune_keys_and_scheduling_defaults(lib):
+    """Every knob include/gpk.h documents is accepted (host-only call), the defaults are the measured
+    policy (auto look-ahead from 48 blocks, fused panel solve with the look-ahead off, up to 256
+    workgroups), and an unknown key is rejected."""
+    src = re.sub(r"\s+", " ", open(HEADER).read())
+    doc = src[src.index("Scheduling knobs"):src.index("int gpk_tune(")]
+    keys = sorted(set(re.findall(r'"([a-z0-9_]+)"', doc)))
+    assert {"lookahead", "la_min_blocks", "fuse_trsm", "fuse_trsm_max", "panel_stream", "group"} <= set(keys)
+    for k in keys:
+        old = _native.tune(k, 0)
+        assert _native.tune(k, old) == 0
+    import subprocess
+    import sys
+    # defaults in a fresh process (environment overrides cleared)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("GPK_")}
+    code = ("from gaussianprocessfundamentals_amd import _native as n\n"
+            "print([n.tune(k, 0) for k in ('lookahead', 'la_min_blocks', 'fuse_trsm', 'fuse_trsm_max', "
+            "'panel_stream')])")  # returns the default each knob held
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
+                         cwd=os.path.dirname(HEADER) + "/..")
+    assert out.stdout.strip().splitlines()[-1] == "[2, 48, 1, 256, 0]"
+    with pytest.raises(Exception):
+        _native.tune("no_such_knob", 1)
