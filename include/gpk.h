@@ -322,7 +322,8 @@ int gpk_timing_reset(void);
  * matrix, the default), "panel_stream" (the look-ahead's chain: 0 high-priority side stream, 1 the
  * caller's, 2 a normal-priority side stream), "fuse_trsm" (f64 panel solve inside the diagonal-block
  * launch while batch x (64-row tiles + 1) <= "fuse_trsm_max": 1 with the look-ahead off, 2 always,
- * 0 never; bitwise identical results), "reserve_cus" (CUs masked off the bulk-update stream; read
+ * 0 never; bitwise identical results; callers that overlap factorisations on several streams set
+ * 0), "reserve_cus" (CUs masked off the bulk-update stream; read
  * when that stream is first created), "group" (panels per trailing update, K = 128 group), "group_first"
  * (panels of the first group), "fuse_kbuild" (K build inside the first trailing update),
  * "upd_band" (trailing-update tile order), "skip_zero_rows" (skip the MFMAs of the zero rows below
