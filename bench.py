@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--lookahead", type=int, default=None,
                     help="panel look-ahead on side streams: 1 on, 0 off, 2 auto (libgpk: off below 48 128-blocks "
                          "of the augmented matrix); default 2, 0 when --pipeline > 1")
+    ap.add_argument("--fuse-trsm", type=int, default=None,
+                    help="panel solve inside the diagonal-block launch (libgpk fuse_trsm); default 0 when "
+                         "--pipeline > 1, else the library default (1)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events")
@@ -286,8 +289,8 @@ def main():
     nat.tune("lookahead", la)
     # batches overlapping on P > 1 streams: the panel solve stays a separate launch (fused, its redundant
     # workgroups take CUs from the other batches' updates: C5 at 3 in flight 38.2 -> 36.4 evals/s)
-    if P > 1:
-        nat.tune("fuse_trsm", 0)
+    if args.fuse_trsm is not None or P > 1:
+        nat.tune("fuse_trsm", args.fuse_trsm if args.fuse_trsm is not None else 0)
     if grad_mode:
         facts = [engine.InverseFactorization(n, d, batch, dt) for _ in range(P)]
     else:
