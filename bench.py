@@ -37,6 +37,10 @@ DEFAULT_BATCH = 64
 # evals/s against 104.9 / 104.4 for 8 x 2 (two alternating passes on one box)
 DEFAULT_BATCH_GRAD = 16
 DEFAULT_PIPELINE_METRIC = 2
+# the other configs (one candidate per step except C4): 4 buffers / streams -- C2 1091 -> 1289, C3 403 -> 436,
+# C5 38.2 -> 38.7 evals/s against 3, C4 flat; 5, 6 and 8 measured slower than 4 on C2 (785, 924, 1135) with 4, 8
+# or 16 hardware queues alike
+DEFAULT_PIPELINE_OTHER = 4
 
 CONFIGS = {
     # name: (kernel, d, n, noise, dtype, hyp)
@@ -66,7 +70,7 @@ def parse():
                          % (DEFAULT_BATCH, DEFAULT_BATCH_GRAD))
     ap.add_argument("--pipeline", type=int, default=None,
                     help="factorisation buffers / streams that consecutive steps rotate over (overlap of batches); "
-                         "default %d for the metric config, 3 otherwise" % DEFAULT_PIPELINE_METRIC)
+                         "default %d for the metric config, %d otherwise" % (DEFAULT_PIPELINE_METRIC, DEFAULT_PIPELINE_OTHER))
     ap.add_argument("--lookahead", type=int, default=None,
                     help="panel look-ahead on side streams: 1 on, 0 off, 2 auto (libgpk: off below 48 128-blocks "
                          "of the augmented matrix); default 2, 0 when --pipeline > 1")
@@ -284,7 +288,7 @@ def main():
     # so that one batch's exposed panel chain (start and tail of the factorisation) overlaps the
     # trailing updates of the next (the batches are independent candidate sets of the sweep)
     P = max(1, args.pipeline if args.pipeline is not None else
-            (DEFAULT_PIPELINE_METRIC if args.config == "metric" else 3))
+            (DEFAULT_PIPELINE_METRIC if args.config == "metric" else DEFAULT_PIPELINE_OTHER))
     la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 2)
     nat.tune("lookahead", la)
     # batches overlapping on P > 1 streams: the panel solve stays a separate launch (fused, its redundant
