@@ -441,7 +441,8 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // the separate gemm<TRSM>; one launch fewer on the chain per panel.
   auto fused_tiles = [&](int64_t k) -> int64_t {
     const int64_t rows = lay->p - (k + 1) * NB;
-    if (dt != GPK_F64 || !tn.fuse_trsm || tn.diag_version == 1 || rows <= 0) return 0;
+    // (the timing-only ablations of the diagonal kernel skip the writer's counter reset: never fused)
+    if (dt != GPK_F64 || !tn.fuse_trsm || tn.diag_version == 1 || tn.diag_dbg != 0 || rows <= 0) return 0;
     if (la && tn.fuse_trsm != 2) return 0;  // beside the look-ahead's bulk updates the extra workgroups
                                              // cost more than the launch saves (N = 8192: 6.39 -> 6.43 ms)
     const int64_t t64 = rows / 64;
