@@ -324,32 +324,21 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
     const FastNode fn = make_fast_node(nd, hyp, a.d);
     const double* ls = (nd.flags & GPK_NODE_ARD) ? hyp + nd.hyp_offset : nullptr;
     const int64_t nn = a.n, npad = a.n_pad, yrow = a.y_row;
-    // the tile in two halves of TM / 2 rows through the (still unused) staging LDS: every thread
-    // evaluates (TM / 2) TN / (128 WN) values, then the waves of that half load their accumulators
-    double* cs = reinterpret_cast<double*>(smem);
-    constexpr int HALF = (TM / 2) * TN;
-    constexpr int NT = 128 * WN;
-    static_assert(HALF * (int)sizeof(double) <= 2 * STAGE, "half tile must fit the staging LDS");
-    const int64_t cj_tile = a.row0 + tj * TN;
+    // every lane evaluates its own accumulator entries (C/D layout: row wr (TM / WM) + 16 m + RSTEP r +
+    // row(lane, 0), column wc (TN / WN) + 16 n + col), so each wave evaluates its own eighth of the tile
+    // with no LDS round trip and no barrier; the points of a 16-row block's four rows are loaded together.
+    // (The earlier form staged two half tiles through LDS, one element per iteration of a rolled loop:
+    // ~16 us per tile, 3.3 ms of a 64 x 2 metric step.)
+    const int64_t ci = R + wr * (TM / WM) + Mfma<T>::row(lane, 0);
+    const int64_t cj = a.row0 + tj * TN + wc * (TN / WN) + col;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll 1
-      for (int e = tid; e < HALF; e += NT) {
-        const int rr = e / TN, cc = e - rr * TN;
-        cs[e] = kbuild_value<KB>(fn, ls, Xb, yb, noise, nn, npad, yrow, R + h * (TM / 2) + rr, cj_tile + cc);
-      }
-      __syncthreads();
-      if (wr == h) {
+    for (int m = 0; m < MB; ++m)
 #pragma unroll
-        for (int m = 0; m < MB; ++m)
+      for (int n = 0; n < NBK; ++n)
 #pragma unroll
-          for (int n = 0; n < NBK; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              acc[m][n][r] = (T)cs[(m * 16 + r * RSTEP + Mfma<T>::row(lane, 0)) * TN + wc * (TN / WN) + n * 16 + col];
-      }
-      __syncthreads();
-    }
+        for (int r = 0; r < 4; ++r)
+          acc[m][n][r] = (T)kbuild_value<KB>(fn, ls, Xb, yb, noise, nn, npad, yrow, ci + m * 16 + r * RSTEP,
+                                             cj + n * 16);
   } else {
 #pragma unroll
     for (int m = 0; m < MB; ++m)
