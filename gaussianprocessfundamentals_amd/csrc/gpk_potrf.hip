@@ -309,6 +309,9 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
 #define GPK_CSOFF(m, n, r) (((m) * 16 + (r) * RSTEP) * ldb_s + (n) * 16 * (int)sizeof(T))
 
   acc_t acc[MB][NBK];
+  // fused K build: the first chunk's DMA goes out before the evaluation (which no longer touches the
+  // staging LDS) and lands while the lanes evaluate their entries
+  if (KB != 0) GPK_GLDS(0, 0);
   if (KB != 0) {
     // fused K build: evaluate this tile's C instead of loading it (the values gpk_assemble would
     // have written; the tile's points are read straight from X, cached in L1 / L2)
@@ -331,14 +334,39 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
     // ~16 us per tile, 3.3 ms of a 64 x 2 metric step.)
     const int64_t ci = R + wr * (TM / WM) + Mfma<T>::row(lane, 0);
     const int64_t cj = a.row0 + tj * TN + wc * (TN / WN) + col;
+    const int64_t cj_tile = a.row0 + tj * TN;
+    if (a.d == 1 && ls == nullptr && R + TM <= nn && cj_tile + TN <= nn && R != cj_tile) {
+      // interior off-diagonal tile of a one-dimensional kernel (the metric's case): every entry is the
+      // kernel value of two training points -- no class branches; the lane's 16 row points and 2
+      // column points are loaded together up front.  The same fast_value_at as kbuild_value: same bits.
+      FastNode f = fn;
+      f.op = KB;
+      double xr[MB][4], xc[NBK];
 #pragma unroll
-    for (int m = 0; m < MB; ++m)
+      for (int m = 0; m < MB; ++m)
 #pragma unroll
-      for (int n = 0; n < NBK; ++n)
+        for (int r = 0; r < 4; ++r) xr[m][r] = Xb[ci + m * 16 + r * RSTEP];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc[m][n][r] = (T)kbuild_value<KB>(fn, ls, Xb, yb, noise, nn, npad, yrow, ci + m * 16 + r * RSTEP,
-                                             cj + n * 16);
+      for (int n = 0; n < NBK; ++n) xc[n] = Xb[cj + n * 16];
+#pragma unroll
+      for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int n = 0; n < NBK; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double u = xr[m][r], v = xc[n];
+            acc[m][n][r] = (T)fast_value_at(f, [u](int) { return u; }, [v](int) { return v; });
+          }
+    } else {
+#pragma unroll
+      for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int n = 0; n < NBK; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc[m][n][r] = (T)kbuild_value<KB>(fn, ls, Xb, yb, noise, nn, npad, yrow, ci + m * 16 + r * RSTEP,
+                                               cj + n * 16);
+    }
   } else {
 #pragma unroll
     for (int m = 0; m < MB; ++m)
@@ -360,7 +388,7 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
 
   const int NK0 = (MODE == GEMM_TRSM) ? NB / GBK : a.kdepth / GBK;
   const int NK = (GPK_ABLATE == 3 && MODE == GEMM_UPDATE) ? 2 * NK0 : NK0;
-  GPK_GLDS(0, 0);
+  if (KB == 0) GPK_GLDS(0, 0);
 #ifndef GPK_SETPRIO
 #define GPK_SETPRIO 0  // 1: static priority 1 for the second-dispatched half of the waves (MI355X guide)
 #endif
