@@ -160,3 +160,23 @@ def test_fused_panel_solve_beside_a_busy_stream():
             _assert_bitwise(quiet, res)
         torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize()
+
+
+def test_fused_panel_solve_beside_the_lookahead_bulk_stream():
+    """fuse_trsm = 2 also fuses with the panel look-ahead on: the fused launches then run beside the bulk
+    trailing updates of the CU-masked stream (late-starting workgroups, the ticket counter under real
+    concurrency) and must still give the separate launch's bits."""
+    old_la = engine.nat.tune("lookahead", 1)
+    try:
+        out = {}
+        for fuse in (0, 2):
+            old = engine.nat.tune("fuse_trsm", fuse)
+            try:
+                res = _plain(6300, 0, 1, hyps=[[0.07]], seed=9)()
+                torch.cuda.synchronize()
+                out[fuse] = [np.array(r.cpu().numpy(), copy=True) for r in res]
+            finally:
+                engine.nat.tune("fuse_trsm", old)
+        _assert_bitwise(out[0], out[2])
+    finally:
+        engine.nat.tune("lookahead", old_la)
