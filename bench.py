@@ -72,7 +72,7 @@ def parse():
                     help="factorisation buffers / streams that consecutive steps rotate over (overlap of batches); "
                          "default %d for the metric config, %d otherwise" % (DEFAULT_PIPELINE_METRIC, DEFAULT_PIPELINE_OTHER))
     ap.add_argument("--lookahead", type=int, default=None,
-                    help="panel look-ahead on side streams: 1 on, 0 off, 2 auto (libgpk: off below 48 128-blocks "
+                    help="panel look-ahead on side streams: 1 on, 0 off, 2 auto (libgpk: off below 64 128-blocks "
                          "of the augmented matrix); default 2, 0 when --pipeline > 1")
     ap.add_argument("--fuse-trsm", type=int, default=None,
                     help="panel solve inside the diagonal-block launch (libgpk fuse_trsm); default 0 when "

@@ -166,7 +166,7 @@ int64_t env_i64(const char* name, int64_t dflt) {
 
 Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
-                         env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 2), env_i64("GPK_LA_MIN_BLOCKS", 48),
+                         env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 2), env_i64("GPK_LA_MIN_BLOCKS", 64),
                          env_i64("GPK_FUSE_TRSM", 1), env_i64("GPK_FUSE_TRSM_MAX", 256),
                          env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
@@ -420,7 +420,8 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // saves.  ms per call, look-ahead off / on (profiles/r02s_lookahead.txt): one member N = 1024
   // 0.45 / 0.55, 2048 0.92 / 1.09, 4096 2.10 / 2.29, 6144 3.98 / 4.03, 8192 6.53 / 6.40, 12288
   // 15.3 / 14.5; batches of 8 at N = 4096 5.13 / 5.26; the 128-candidate C4 sweep 52.7 / 54.2;
-  // -LML + gradient (identity rows: twice the width) N = 4096 3.44 / 3.28.
+  // -LML + gradient (identity rows: twice the width) N = 4096 3.44 / 3.28.  With the panel solve fused
+  // (look-ahead off only): N = 6144 3.89 / 4.02, 7168 5.01 / 5.05, 8192 6.43 / 6.39 -> 64 blocks.
   const bool la = tn.lookahead == 1 || (tn.lookahead == 2 && lay->p / NB >= tn.la_min_blocks);
   SideStream* ss = nullptr;
   if (la) {

@@ -318,7 +318,7 @@ int gpk_timing_reset(void);
 
 /* Scheduling knobs of the factorisation (no reference counterpart: tf.linalg.cholesky exposes
  * none).  Keys: "lookahead" (1: panel chain on a high-priority stream overlapping the bulk
- * trailing update, 0: one stream, 2: auto -- on from "la_min_blocks" 128-blocks of the augmented
+ * trailing update, 0: one stream, 2: auto -- on from "la_min_blocks" (64) 128-blocks of the augmented
  * matrix, the default), "panel_stream" (the look-ahead's chain: 0 high-priority side stream, 1 the
  * caller's, 2 a normal-priority side stream), "fuse_trsm" (f64 panel solve inside the diagonal-block
  * launch while batch x (64-row tiles + 1) <= "fuse_trsm_max": 1 with the look-ahead off, 2 always,

@@ -73,7 +73,7 @@ def test_product_fails_loudly_without_gpu(lib):
 
 def test_tune_keys_and_scheduling_defaults(lib):
     """Every knob include/gpk.h documents is accepted (host-only call), the defaults are the measured
-    policy (auto look-ahead from 48 blocks, fused panel solve with the look-ahead off, up to 256
+    policy (auto look-ahead from 64 blocks, fused panel solve with the look-ahead off, up to 256
     workgroups), and an unknown key is rejected."""
     src = re.sub(r"\s+", " ", open(HEADER).read())
     doc = src[src.index("Scheduling knobs"):src.index("int gpk_tune(")]
@@ -91,6 +91,6 @@ def test_tune_keys_and_scheduling_defaults(lib):
             "'panel_stream')])")  # returns the default each knob held
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
                          cwd=os.path.dirname(HEADER) + "/..")
-    assert out.stdout.strip().splitlines()[-1] == "[2, 48, 1, 256, 0]"
+    assert out.stdout.strip().splitlines()[-1] == "[2, 64, 1, 256, 0]"
     with pytest.raises(Exception):
         _native.tune("no_such_knob", 1)
