@@ -16,6 +16,8 @@
 // Writes L_kk to W (lower triangle) and L_kk^-1 (zeros above the diagonal) to Winv; the first
 // non-positive pivot (1-based global column) goes to info[b] (LAPACK convention, as the
 // InvalidArgumentError of tf.linalg.cholesky at gpbasics/Statistics/CovarianceMatrix.py:250).
+#include <type_traits>
+
 #include "gpk_internal.h"
 
 namespace gpk {
@@ -345,7 +347,7 @@ __device__ __forceinline__ bool panel_zero_rows(const DiagArgs& a, int b, int64_
 // X = A L_kk^-T with the same MFMA k-order as gemm_kernel<TRSM> (k-step s of chunk kc takes k = 16 kc +
 // 2 q + 8 (s >> 1) + (s & 1) in lane group q; chunks kc > the column block skipped), so X is bitwise
 // the separate panel solve's.  Wave w: 16-row block w & 3, column blocks of half w >> 2 (balanced).  Its A operands (32
-// doubles per lane) are loaded during the last block row of the factorisation.
+// doubles per lane) are loaded during the last step of the factorisation.
 template <typename T, bool FUSE>
 __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -400,16 +402,32 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   const int64_t R = a.row0 + (int64_t)tk * 64;
   const bool live = FUSE && !wr && !panel_zero_rows(a, b, R, R + 64);
 
+  // FUSE: the panel rows' A operands (32 doubles per lane) are loaded in the last step -- waves 1..7 at its
+  // start, wave 0 after its potf2 -- so their latency hides under that step; the last step is peeled off
+  // the loop, so they are not live (and do not spill) through the earlier steps
+  bool fetched = false;
+  auto prefetch = [&]() {
+    if (!FUSE || !live) return;
+    const double* Ar = reinterpret_cast<const double*>(a.W) + (int64_t)b * a.w_bs +
+                       (R + (wave & 3) * DB + lr) * a.ld + a.j0 + 2 * lk;
+#pragma unroll
+    for (int kc = 0; kc < NTL; ++kc) {
+      pa[kc][0] = *reinterpret_cast<const dbl2*>(Ar + kc * DB);
+      pa[kc][1] = *reinterpret_cast<const dbl2*>(Ar + kc * DB + 8);
+    }
+    fetched = true;
+  };
   d4 xs = {0.0, 0.0, 0.0, 0.0};  // wave 0: X_{s+1} (operand layout) from QR_s, stored in P_{s+1}
-#pragma unroll 1
-  for (int s = 0; s < ((a.dbg & 16) ? 0 : NTL); ++s) {
+  auto step = [&](int s, auto last) {
     // ---------------------------------------------------------------- P_s
+    if (decltype(last)::value && wave != 0) prefetch();
     if (wave == 0) {
       if (s > 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) A[(s * DB + lr) * LDA + (s - 1) * DB + lk + 4 * q] = xs[q];
       }
       if (!(a.dbg & 2)) potf2_tile(A, Dinv + s * DB * DB, colbuf, s, lane, flag, a.j0);  // timing ablation
+      if (decltype(last)::value) prefetch();
     } else if (s == 0) {
       if (!(a.dbg & 8) && wr) store_inv_zeros(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
     } else {
@@ -469,20 +487,14 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
       }
     }
     __syncthreads();
-  }
+    };
+  const int nsteps = (a.dbg & 16) ? 0 : NTL;
+#pragma unroll 1
+  for (int s = 0; s + 1 < nsteps; ++s) step(s, std::false_type());
+  if (nsteps > 0) step(nsteps - 1, std::integral_constant<bool, FUSE>());
   // after P_7: block row 7 of L to HBM, rows 6 and 7 of L^-1
   if (a.dbg & 32) return;  // timing ablation
-  if (FUSE && live) {
-    // the panel rows' A operands, in flight during the last block row (held through the factorisation
-    // they would not fit beside its registers)
-    const double* Ar = reinterpret_cast<const double*>(a.W) + (int64_t)b * a.w_bs +
-                       (R + (wave & 3) * DB + lr) * a.ld + a.j0 + 2 * lk;
-#pragma unroll
-    for (int kc = 0; kc < NTL; ++kc) {
-      pa[kc][0] = *reinterpret_cast<const dbl2*>(Ar + kc * DB);
-      pa[kc][1] = *reinterpret_cast<const dbl2*>(Ar + kc * DB + 8);
-    }
-  }
+  if (!fetched) prefetch();  // (only when the step loop was ablated away)
   if (wave >= 1) {
     inverse_tile(A, Dinv, Ib, NTL - 1, wave - 1, lr, lk, wr);
   } else if (wr) {
