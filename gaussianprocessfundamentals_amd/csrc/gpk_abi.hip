@@ -142,7 +142,9 @@ struct Tune {
   int64_t fuse_trsm;      // f64: panel solve fused into the diagonal-block launch (1: look-ahead off only,
                           // 2: always; one workgroup per
   int64_t fuse_trsm_max;  //   64-row tile, each factoring the block) while batch x tiles <= fuse_trsm_max
-  int64_t reserve_cus;    // CUs kept free of the bulk trailing update for the panel chain
+  int64_t reserve_cus;    // CUs kept free of the bulk trailing update for the panel chain (32: single N = 8192
+                          // 6.46 -> 6.26 ms, -LML + gradient N = 4096 3.29 -> 3.04 ms, batches of 2 / 8 / 32
+                          // without pipelining +1.9 / +0.6 / +0.4 % against 8)
   int64_t group;          // panels per trailing update (K = 128 group)
   int64_t group_first;    // panels of the first group (a short first chain lets the bulk start early)
   int64_t fuse_kbuild;    // gpk_nlml: K build fused into the first trailing update (single-node kernels)
@@ -168,7 +170,7 @@ Tune& tune() {
   static Tune t = {env_i64("GPK_UPD_T128_MIN", 512), env_i64("GPK_TRSM_T128_MIN", 256),
                          env_i64("GPK_DIAG_DEBUG", 0), env_i64("GPK_LOOKAHEAD", 2), env_i64("GPK_LA_MIN_BLOCKS", 64),
                          env_i64("GPK_FUSE_TRSM", 1), env_i64("GPK_FUSE_TRSM_MAX", 256),
-                         env_i64("GPK_RESERVE_CUS", 8), env_i64("GPK_GROUP", 8),
+                         env_i64("GPK_RESERVE_CUS", 32), env_i64("GPK_GROUP", 8),
                          env_i64("GPK_GROUP_FIRST", 8), env_i64("GPK_FUSE_KBUILD", 1),
                          env_i64("GPK_UPD_BAND", 0), env_i64("GPK_SKIP_ZERO_ROWS", 1), env_i64("GPK_SYEVJ_ABS_TOL_E3", 0),
                          env_i64("GPK_DIAG_VERSION", 2), env_i64("GPK_INGROUP", 0),
