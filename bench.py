@@ -84,7 +84,62 @@ def parse():
     ap.add_argument("--dist", action="store_true",
                     help="run the multi-GPU code path (RCCL process group, per-step all-gather, barriers, MAX "
                          "over ranks) even at world size 1: the rehearsal of the N > 1 bench on a 1-GPU box")
+    ap.add_argument("--launch-dry", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo group, all-gathers its rank and "
+                         "rank 0 prints the ranks it saw (no HIP call)")
+    ap.add_argument("--slice-of", type=int, default=1, metavar="W",
+                    help="C4 only: time on this GPU the slice rank 0 evaluates when the 128-candidate sweep is "
+                         "sharded over W ranks (128 / W candidates per step) -- the per-rank work of the W-GPU run")
+    ap.add_argument("--check-candidates", default=None,
+                    help="comma-separated batch indices whose -LML is checked against the oracle after the "
+                         "timed region (default: first, middle, last)")
+    ap.add_argument("--no-check", action="store_true", help="skip the oracle check of the bench's own values")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N ranks, one process per GPU, through
+    torch.distributed.run (127.0.0.1 rendezvous) as a child process -- nothing in this process has
+    touched the GPU -- and return its exit code."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # the box supports dmabuf IPC only (RCCL)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_dry(args):
+    """Every rank: a gloo group, all-gather of (rank, local rank, pid); rank 0 prints them."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    mine = torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0")), os.getpid()], dtype=torch.int64)
+    got = [torch.zeros_like(mine) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(got, mine)
+    else:
+        got = [mine]
+    if rank == 0:
+        print(json.dumps({"launch_dry": True, "n_gpus": world, "gpus_flag": args.gpus,
+                          "ranks": [int(g[0]) for g in got], "local_ranks": [int(g[1]) for g in got],
+                          "distinct_pids": len({int(g[2]) for g in got})}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def pmc_traffic(cfg, batch):
@@ -142,7 +197,7 @@ def cpu_baseline_grad(cfg_name, n):
     import torch
     from oracle import gp_autodiff as ad
     from oracle import gp_oracle as o
-    threads = int(os.environ.get("GPK_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    threads, _ = host_threads()
     torch.set_num_threads(threads)
     kname, d, _, noise, _, hyp = CONFIGS[cfg_name]
     tree = {"SE": ("SE", {}), "SE-SCALED": ("SE", {})}.get(kname)
@@ -160,52 +215,114 @@ def cpu_baseline_grad(cfg_name, n):
                       % (cfg_name, n, threads, t1)}
 
 
-def cpu_baseline(cfg_name, n, budget_s):
-    """Time the oracle (numpy/SciPy restatement of the reference path) on this host."""
-    import numpy as np
-    from threadpoolctl import threadpool_limits
-    from oracle import gp_oracle as o
-    threads = int(os.environ.get("GPK_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    kname, d, _, noise, _, hyp = CONFIGS[cfg_name]
-    tree = {"SE": ("SE", {}), "SE-SCALED": ("SE", {}), "MAT52-ARD": ("MAT52", {"ard": True, "standard": True}),
+def host_threads():
+    """Host threads of the CPU baseline: the CPUs this process may run on (sched_getaffinity), capped
+    by the cgroup CPU quota and by OMP_NUM_THREADS when either is set (the GPU box exposes the whole
+    machine's CPUs but grants one GPU's share).  GPK_CPU_THREADS overrides.  Returns (threads, facts)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:  # cgroup v2
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = aff
+    if quota:
+        threads = min(threads, max(1, int(math.ceil(quota))))
+    if omp and omp.isdigit() and int(omp) > 0:
+        threads = min(threads, int(omp))
+    if os.environ.get("GPK_CPU_THREADS"):
+        threads = int(os.environ["GPK_CPU_THREADS"])
+    return threads, {"sched_getaffinity": aff, "cgroup_cpu_quota": quota, "omp_num_threads": omp,
+                     "os_cpu_count": os.cpu_count()}
+
+
+def oracle_tree(kname):
+    return {"SE": ("SE", {}), "SE-SCALED": ("SE", {}), "MAT52-ARD": ("MAT52", {"ard": True, "standard": True}),
             "SE-ARD+PER": ("ADD", [("SE", {"ard": True}), ("PER", {"standard": True})])}[kname]
+
+
+def oracle_hyp(row, kname, d):
+    """A flat device hyperparameter row -> the oracle's nested list (ARD length scales as one list)."""
+    if kname == "MAT52-ARD":
+        return [list(row[:d])]
+    if kname == "SE-ARD+PER":
+        return [list(row[:d])] + list(row[d:])
+    return list(row)
+
+
+def cpu_baseline(cfg_name, n, budget_s, row):
+    """Time the oracle (numpy/SciPy restatement of the reference path, oracle/gp_oracle.nlml_stages) on
+    this host for the device's candidate `row` (a flat hyperparameter row): K build on a thread pool
+    (TF's intra-op pool spreads the reference's), dpotrf / 2 x dtrtrs through MKL (torch's CPU LAPACK --
+    here faster than scipy's OpenBLAS build, so the stronger baseline), stage by stage, with all host
+    threads and with one.  Returns (record, nlml of the evaluated candidate)."""
+    from oracle import gp_oracle as o
+    threads, facts = host_threads()
+    kname, d, _, noise, _, _ = CONFIGS[cfg_name]
+    tree = oracle_tree(kname)
     scaled = kname == "SE-SCALED"
-    if scaled:
-        hyp = list(c4_candidates()[0])  # one candidate of the sweep per evaluation
-    elif hyp is None:
-        hyp = [list(np.linspace(0.4, 1.1, d)), 1.0, 0.5]
+    hyp = oracle_hyp(row, kname, d)
     x, y = o.make_inputs("metric" if cfg_name == "metric" else cfg_name, n=n)
     # SURVEY §8d: median of >= 5 warm repetitions with the host threads, plus one 1-thread figure
-    times = []
-    with threadpool_limits(limits=threads):
-        o.nlml(tree, hyp, noise, x, y, scaled=scaled)  # warm (BLAS pool, page-in)
-        t_all = time.perf_counter()
-        while len(times) < 5 or (time.perf_counter() - t_all < budget_s and len(times) < 9):
-            t0 = time.perf_counter()
-            o.nlml(tree, hyp, noise, x, y, scaled=scaled)
-            times.append(time.perf_counter() - t0)
-            if time.perf_counter() - t_all > 3 * budget_s:
-                break
-    with threadpool_limits(limits=1):
-        t0 = time.perf_counter()
-        o.nlml(tree, hyp, noise, x, y, scaled=scaled)
-        t1 = time.perf_counter() - t0
-    med = sorted(times)[len(times) // 2]
+    runs = []
+    o.nlml_stages(tree, hyp, noise, x[:1024], y[:1024], threads, scaled)  # warm (pools, page-in)
+    t_all = time.perf_counter()
+    while len(runs) < 5 or (time.perf_counter() - t_all < budget_s and len(runs) < 9):
+        runs.append(o.nlml_stages(tree, hyp, noise, x, y, threads, scaled))
+        if time.perf_counter() - t_all > 3 * budget_s:
+            break
+    runs.sort(key=lambda r: r[1]["total"])
+    nl, med = runs[len(runs) // 2]
+    one = None
+    if threads == 1:
+        one = med
+    elif med["total"] * min(threads, 16) < 2.0 * budget_s:
+        one = o.nlml_stages(tree, hyp, noise, x, y, 1, scaled)[1]
     try:
         cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:  # noqa: BLE001
         cpu_model = "unknown"
-    try:
-        from threadpoolctl import threadpool_info
-        blas = ",".join(sorted({"%s %s" % (i.get("internal_api"), i.get("version")) for i in threadpool_info()
-                                if i.get("user_api") == "blas"}))
-    except Exception:  # noqa: BLE001
-        blas = "unknown"
-    return {"value": 1.0 / med, "unit": "LML evals/s", "cores": threads, "kind": "port",
-            "value_1_thread": 1.0 / t1,
-            "sample": "median of %d warm full evaluations of the %s workload (N=%d, fp64: K build, dpotrf, "
-                      "2 x dtrtrs, read-out) by the numpy/SciPy oracle, %d threads (%s), %s; plus one "
-                      "1-thread evaluation (%.1f s)" % (len(times), cfg_name, n, threads, blas, cpu_model, t1)}
+    stages = {k: round(v, 4) for k, v in med.items()}
+    rec = {"value": 1.0 / med["total"], "unit": "LML evals/s", "cores": threads, "kind": "port",
+           "value_1_thread": (1.0 / one["total"]) if one else None,
+           "stages_s": stages,
+           "stages_s_1_thread": {k: round(v, 4) for k, v in one.items()} if one else None,
+           "host": dict(facts, cpu_model=cpu_model, lapack="MKL (torch CPU) dpotrf / dtrtrs",
+                        kbuild="numpy, row chunks of 256 on %d threads" % threads),
+           "sample": "median of %d warm full evaluations of the %s workload (N=%d, fp64: K build, dpotrf, "
+                     "2 x dtrtrs, read-out) by the oracle (oracle/gp_oracle.nlml_stages), %d threads = "
+                     "min(sched_getaffinity %d, cgroup quota %s, OMP_NUM_THREADS %s), %s; plus one 1-thread "
+                     "evaluation" % (len(runs), cfg_name, n, threads, facts["sched_getaffinity"],
+                                     facts["cgroup_cpu_quota"], facts["omp_num_threads"], cpu_model)}
+    return rec, nl
+
+
+def oracle_check(cfg_name, n, rows, idx, kname, d, noise, got, known=None):
+    """-LML of device candidates `idx` (rows of the hyperparameter batch) against the oracle on the
+    same inputs (`known`: oracle values already computed, by candidate); returns the check record
+    (bar: rel <= 1e-9, the fp64 tolerance of SURVEY §8d; fp32 C3: 1e-3)."""
+    from oracle import gp_oracle as o
+    threads, _ = host_threads()
+    x, y = o.make_inputs("metric" if cfg_name == "metric" else cfg_name, n=n)
+    tree = oracle_tree(kname)
+    out = []
+    for c in idx:
+        if known and c in known:
+            exp = known[c]
+        else:
+            exp, _ = o.nlml_stages(tree, oracle_hyp(rows[c], kname, d), noise, x, y, threads, kname == "SE-SCALED")
+        out.append({"candidate": int(c), "hyp": [round(v, 12) for v in rows[c]], "nlml": got[c], "oracle": exp,
+                    "rel": abs(got[c] - exp) / abs(exp)})
+    return {"candidates": out, "rel_vs_oracle": max(r["rel"] for r in out)}
 
 
 # Hardware queues per process: HIP multiplexes streams onto GPU_MAX_HW_QUEUES in-order hardware queues
@@ -218,6 +335,20 @@ HW_QUEUES = int(os.environ.get("GPK_BENCH_HW_QUEUES", "8"))  # 0: leave the runt
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks; refusing to report "
+                         "a %d-GPU number from a %s-rank job\n" % (args.gpus, env_world, args.gpus, env_world))
+        sys.exit(2)
+    if env_world is None and args.gpus > 1:
+        # no launcher: start the N ranks here, before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus))
+    if args.launch_dry:
+        launch_dry(args)
+        return
+    if args.slice_of != 1 and (args.config != "C4" or args.slice_of < 1 or args.gpus != 1):
+        sys.stderr.write("bench.py: --slice-of W needs --config C4 on one GPU\n")
+        sys.exit(2)
     # before the first HIP call of the process (torch initialises HIP lazily)
     if HW_QUEUES and int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES:
         os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
@@ -225,6 +356,9 @@ def main():
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if torch.cuda.device_count() < world:
+        sys.stderr.write("bench.py: %d ranks but only %d GPUs visible\n" % (world, torch.cuda.device_count()))
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -265,10 +399,12 @@ def main():
         # C4 (strong scaling): the 128 candidates are split contiguously over the ranks
         from gaussianprocessfundamentals_amd.sweep import shard_range
         cands = c4_candidates()
-        s0, s1 = shard_range(len(cands), rank, world)
+        # --slice-of W (one GPU): rank 0's slice of a W-way sharding, i.e. one rank's work in the W-GPU run
+        shards = world if args.slice_of == 1 else args.slice_of
+        s0, s1 = shard_range(len(cands), rank, shards)
         rows = cands[s0:s1]
         batch = len(rows)
-        chunk = -(-len(cands) // world)
+        chunk = -(-len(cands) // shards)
     else:
         batch = args.batch or ((DEFAULT_BATCH_GRAD if args.mode == "grad" else DEFAULT_BATCH)
                                if args.config == "metric" else 1)
@@ -366,7 +502,8 @@ def main():
         nat.timing_enable(False)
         iso = nat.timing_read()
         nat.tune("lookahead", old_la)
-    nl = float(fact.nlml()[0].item())
+    nl_all = [float(v) for v in fact.nlml().cpu().tolist()]
+    nl = nl_all[0]
     info = int(fact.info.abs().max().item())
     gathered_ok = None
     if use_dist:
@@ -379,7 +516,7 @@ def main():
         gathered_ok = bool(int(torch.isfinite(vals).sum()) == total and float(g[:, chunk:].nan_to_num(0).abs().max()) == 0.0)
 
     if rank == 0:
-        evals = args.steps * (len(c4_candidates()) if sweep else world * batch)
+        evals = args.steps * ((len(c4_candidates()) if args.slice_of == 1 else batch) if sweep else world * batch)
         value = evals / el
         ms = el / args.steps * 1000.0
         lay = fact.layout
@@ -411,8 +548,19 @@ def main():
             breakdown["note"] = ("sums of kernel spans per class over a %d-step events pass after the timed region; "
                                  "with the look-ahead the classes overlap" % args.roofline_steps)
         cpu = None
+        cpu_nl0 = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline_grad(args.config, n) if grad_mode else cpu_baseline(args.config, n, args.cpu_seconds)
+            if grad_mode:
+                cpu = cpu_baseline_grad(args.config, n)
+            else:
+                cpu, cpu_nl0 = cpu_baseline(args.config, n, args.cpu_seconds, rows[0])
+        # parity of the bench's own numbers: -LML of spread candidates against the oracle on the same inputs
+        check = {"nlml": nl, "info": info, **({"allgather_ok": gathered_ok} if use_dist else {})}
+        if not args.no_check:
+            idx = ([int(v) for v in args.check_candidates.split(",")] if args.check_candidates else
+                   sorted({0, batch // 2, batch - 1}))
+            check.update(oracle_check(args.config, n, rows, idx, kname, d, noise, nl_all,
+                                      known={0: cpu_nl0} if cpu_nl0 is not None else {}))
         line = {
             "metric": ("log-marginal-likelihood%s evals/sec at N=%d %s"
                        % (" + gradient" if grad_mode else "", n, "fp64" if dtn == "f64" else "fp32")),
@@ -426,7 +574,8 @@ def main():
             "scaling": "strong" if sweep else "weak",
             "vs_baseline": None,
             "dtype": dtn,
-            "data": "synthetic (SURVEY §8d generator, numpy default_rng seed 5), resident in HBM",
+            "data": "synthetic (SURVEY §8d generator, numpy default_rng seed %d), resident in HBM"
+                    % {"metric": 5, "C2": 1, "C3": 2, "C4": 3, "C5": 4}[args.config],
             "config": {"workload": ("%s GP -LML sweep, kernel=SE (scaled), D=%d, N=%d, noise=%g; one step = all %d "
                                     "(lengthscale, variance) candidates, %d per rank as one batched factorisation"
                                     % (args.config, d, n, noise, len(c4_candidates()), batch)) if sweep else
@@ -443,10 +592,15 @@ def main():
             "lml_tflops": round(f_lml * value / 1e12, 3),
             "lml_frac_of_peak": round(f_lml * value / 1e12 / PEAK[dtn], 4),
             "kernel_ms_per_step": breakdown,
-            "check": {"nlml": nl, "info": info, **({"allgather_ok": gathered_ok} if use_dist else {})},
+            "check": check,
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        if sweep and args.slice_of != 1:
+            line["slice"] = {"of_world": args.slice_of, "candidates": batch,
+                             "projected_sweep_evals_per_s": round(len(c4_candidates()) * args.steps / el, 3),
+                             "note": "this GPU timed rank 0's slice of a %d-way sharded C4 sweep; value = the slice's "
+                                     "candidates / s, projected = all 128 / the slice's step time" % args.slice_of}
         print(json.dumps(line), flush=True)
     if use_dist:
         dist.destroy_process_group()

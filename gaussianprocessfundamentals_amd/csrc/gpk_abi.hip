@@ -249,12 +249,19 @@ SideStream* side_stream() {
 }
 
 // Ticket counters of the fused panel solve (DiagArgs::ctr), one block of kFuseCtr per (device,
-// stream): launches on one stream never overlap, and each launch's writer leaves its counters at 0.
+// stream): launches on one stream never overlap.  Tickets are drawn with atomicInc(ctr, grid - 1), so
+// the grid's last draw wraps the counter back to 0 by itself (no reset store).  A handle that stands
+// for one stream per host thread (hipStreamPerThread) or a stream being captured does not get
+// counters: its panel solve stays a separate launch (fuse_counters returns nullptr).  The null stream
+// is one queue per device whatever thread launches on it (torch's default stream), so it keeps them.
 constexpr int kFuseCtr = 256;  // members per launch
 std::mutex g_ctr_mu;
 std::map<std::pair<int, hipStream_t>, int32_t*> g_ctr;
 
 int32_t* fuse_counters(hipStream_t s) {
+  if (s == hipStreamPerThread) return nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(g_ctr_mu);
@@ -262,7 +269,10 @@ int32_t* fuse_counters(hipStream_t s) {
   if (it != g_ctr.end()) return it->second;
   int32_t* p = nullptr;
   if (hipMalloc(&p, kFuseCtr * sizeof(int32_t)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(p, 0, kFuseCtr * sizeof(int32_t), s) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, kFuseCtr * sizeof(int32_t), s) != hipSuccess) {
+    hipFree(p);
+    return nullptr;
+  }
   g_ctr[{dev, s}] = p;  // owned for the life of the process
   return p;
 }
@@ -411,7 +421,9 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   const size_t es = elem_size(dt);
   const int64_t nblk = lay->n_pad / NB;
 
-  const Tune& tn = tune();
+  // one snapshot of the knobs per call: a gpk_tune from another thread (ctypes releases the GIL during
+  // the enqueue) must not change the fuse decision between a panel's diag(k) and trsm(k)
+  const Tune tn = tune();
   // The panel chain (diag, panel solve, thin and look-ahead updates) runs on a high-priority
   // stream, the bulk of each trailing update on a CU-masked stream concurrently with the next
   // panel pair's chain; both fork from and join back into the caller's stream.
@@ -442,8 +454,10 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // workgroup per 64-row tile (plus the one that writes L and L^-1), each factoring the block
   // redundantly (the chip is otherwise idle there) and solving its rows against L^-1 in LDS, bitwise
   // the separate gemm<TRSM>; one launch fewer on the chain per panel.
+  int32_t* const ctr = (dt == GPK_F64 && tn.fuse_trsm) ? fuse_counters(sp) : nullptr;
   auto fused_tiles = [&](int64_t k) -> int64_t {
     const int64_t rows = lay->p - (k + 1) * NB;
+    if (!ctr) return 0;  // no counters for this stream: the separate panel-solve launch
     // (the timing-only ablations of the diagonal kernel skip the writer's counter reset: never fused)
     if (dt != GPK_F64 || !tn.fuse_trsm || tn.diag_version == 1 || tn.diag_dbg != 0 || rows <= 0) return 0;
     if (la && tn.fuse_trsm != 2) return 0;  // beside the look-ahead's bulk updates the extra workgroups
@@ -476,8 +490,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
       da.zhi = eye ? lay->y_row : 0;
       da.nb = n_dev;
       da.mb = m_dev;
-      da.ctr = fuse_counters(sp);
-      if (!da.ctr) return hipErrorOutOfMemory;
+      da.ctr = ctr;
       flops += (double)lay->batch * ((double)(lay->n_pad - da.row0) + extra_nonzero(da.row0)) * NB * NB;
     }
     return timed(1, flops, 0.0, sp, [&] { return launch_diag(da, dt, lay->batch, sp); });
@@ -737,7 +750,7 @@ int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, 
   // Fused K build (single-base-node kernels): only the first panel group's block columns are
   // assembled; the first trailing update evaluates its C tiles instead of reading them, so the
   // trailing part of K is never written to HBM and read back.
-  const Tune& tn = tune();
+  const Tune tn = tune();
   const int64_t nblk = lay->n_pad / NB;
   const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tn.group, 16));
   const int64_t G0 = std::max<int64_t>(1, std::min<int64_t>(tn.group_first, G));

@@ -392,7 +392,8 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   __syncthreads();
   if (FUSE) {
     // the whole block is in LDS (every load retired into the LDS stores above): draw the ticket
-    if (tid == 0) *ticket = atomicAdd(&a.ctr[b], 1);
+    // tickets 0 .. grid - 1; the grid's last draw wraps the counter to 0 for the next launch
+    if (tid == 0) *ticket = (int)atomicInc(reinterpret_cast<unsigned*>(&a.ctr[b]), gridDim.x - 1u);
     __syncthreads();
   }
   // FUSE: the last workgroup to load writes (alone, so its HBM stores never sit in front of a tile's
@@ -503,7 +504,6 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   if (wr) {
     store_l_rows(A, Wb, a.ld, NTL - 1, tid, DT);
     if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
-    if (FUSE && tid == 0) atomicExch(&a.ctr[b], 0);  // every other workgroup has drawn its ticket
   }
   if (!FUSE) return;
   __syncthreads();  // block row 7 of L^-1 in LDS

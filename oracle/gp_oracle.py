@@ -362,6 +362,75 @@ def nlml_with_alpha(alpha, y, logdet, n) -> float:
     return -((-0.5 * fit + -0.5 * logdet) + (-0.5 * (n * LOG_2PI)))
 
 
+# ---------------------------------------------------------------- staged, threaded CPU baseline
+def kernel_matrix_threaded(tree, hyp, x, x_, threads: int = 1, scaled: bool = False,
+                           se_expanded: bool = False, row_chunk: int = 256) -> np.ndarray:
+    """kernel_matrix with its row chunks evaluated on `threads` host threads (numpy's elementwise
+    loops release the GIL), the way TF's intra-op pool (GP:38-39) spreads the reference's K build.
+    Every element is computed by the same numpy expression as kernel_matrix: identical values."""
+    if threads <= 1 or x.ndim != 2 or x.shape[0] <= row_chunk:
+        return kernel_matrix(tree, hyp, x, x_, scaled, se_expanded)
+    from concurrent.futures import ThreadPoolExecutor
+    out = np.empty((x.shape[0], x_.shape[0]), dtype=np.float64)
+
+    def part(i):
+        out[i:i + row_chunk] = _kernel_matrix(tree, hyp, x[i:i + row_chunk], x_, scaled, se_expanded)
+
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(part, range(0, x.shape[0], row_chunk)))
+    return out
+
+
+def nlml_stages(tree, hyp, noise, x, y, threads: int = 1, scaled: bool = False, lapack: str = "mkl"):
+    """One CHOLESKY_BASED -LML evaluation (M/LogLikelihood.py:30-65) timed stage by stage on
+    `threads` host threads: K build (+ noise on the diagonal, S/CovarianceMatrix.py:187-206),
+    dpotrf (:250), the two triangular solves (:256-265) and the read-out (M/Metrics.py:152-154).
+    lapack "mkl": torch's CPU LAPACK (MKL, OpenMP pool = `threads`); "openblas": scipy's.
+    The CPU baseline of bench.py (test infrastructure; never the measured GPU path)."""
+    import time
+    from threadpoolctl import threadpool_limits
+    y = np.asarray(y, dtype=np.float64).reshape(-1, 1)
+    n = x.shape[-2]
+    t = {}
+    with threadpool_limits(limits=threads):
+        t0 = time.perf_counter()
+        A = kernel_matrix_threaded(tree, hyp, x, x, threads, scaled)
+        A[np.diag_indices(n)] += noise
+        t["kbuild"] = time.perf_counter() - t0
+        if lapack == "mkl":
+            import torch
+            old = torch.get_num_threads()
+            torch.set_num_threads(threads)
+            try:
+                t0 = time.perf_counter()
+                At = torch.from_numpy(A)
+                Lt = torch.linalg.cholesky(At)
+                t["potrf"] = time.perf_counter() - t0
+                t0 = time.perf_counter()
+                yt = torch.from_numpy(y)
+                z = torch.linalg.solve_triangular(Lt, yt, upper=False)
+                alpha = torch.linalg.solve_triangular(Lt.mT, z, upper=True).numpy()
+                t["trsv"] = time.perf_counter() - t0
+                t0 = time.perf_counter()
+                logdet = float(2.0 * torch.log(torch.diagonal(Lt)).sum())
+            finally:
+                torch.set_num_threads(old)
+        else:
+            t0 = time.perf_counter()
+            L = cholesky_lower(A)
+            t["potrf"] = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            alpha = l_alpha(L, y)
+            t["trsv"] = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            logdet = float(2.0 * np.sum(np.log(np.diag(L))))
+        fit = float((y.T @ alpha)[0, 0])
+        ll = (-0.5 * fit + -0.5 * logdet) + (-0.5 * (n * LOG_2PI))
+        t["readout"] = time.perf_counter() - t0
+    t["total"] = sum(t.values())
+    return -ll, t
+
+
 # ---------------------------------------------------------------- synthetic configs (SURVEY §8d)
 def make_inputs(cfg: str, n: int = None, seed: int = None) -> Tuple[np.ndarray, np.ndarray]:
     """Synthetic data generators of SURVEY §8(d) (numpy default_rng(seed))."""

@@ -42,6 +42,7 @@ def test_bench_dist_rehearsal_metric():
     x, y = o.make_inputs("metric", n=n)
     exp = o.nlml(("SE", {}), [0.1], 1e-2, x, y)
     assert abs(d["check"]["nlml"] - exp) <= 1e-9 * abs(exp)
+    assert d["check"]["rel_vs_oracle"] <= 1e-9
 
 
 def test_bench_dist_rehearsal_sweep():
@@ -49,3 +50,28 @@ def test_bench_dist_rehearsal_sweep():
                   "--roofline-steps", "1", "--no-cpu-baseline")
     assert d["scaling"] == "strong" and d["config"]["candidates_per_rank_step"] == 128
     assert d["check"]["info"] == 0 and d["check"]["allgather_ok"] is True
+    assert d["check"]["rel_vs_oracle"] <= 1e-9
+
+
+def test_bench_headline_schedule_full_size_parity():
+    """The exact headline schedule at full size -- N = 8192, 64 candidates per batch, 2 batches in flight,
+    panel look-ahead off, panel solve unfused (bench.py defaults) -- with 4 spread candidates' -LML checked
+    against the oracle inside the bench run (rel <= 1e-9, SURVEY §8d fp64 bar; M/LogLikelihood.py:30-65)."""
+    d = run_bench("--steps", "1", "--warmup", "1", "--roofline-steps", "1", "--no-cpu-baseline",
+                  "--check-candidates", "0,21,42,63", timeout=110)
+    assert d["config"]["n"] == 8192 and d["config"]["candidates_per_rank_step"] == 64
+    assert d["config"]["batches_in_flight"] == 2 and "look-ahead off" in d["config"]["schedule"]
+    chk = d["check"]
+    assert chk["info"] == 0 and [c["candidate"] for c in chk["candidates"]] == [0, 21, 42, 63]
+    for c in chk["candidates"]:
+        assert abs(c["hyp"][0] - 0.1 * (1.0 + 0.01 * c["candidate"])) < 1e-15
+    assert chk["rel_vs_oracle"] <= 1e-9, chk
+
+
+def test_bench_c4_slice_mode():
+    """--slice-of W: rank 0's share of the W-way sharded C4 sweep on one GPU (the per-rank work of the
+    W-GPU run), values checked against the oracle."""
+    d = run_bench("--config", "C4", "--n", "1024", "--slice-of", "8", "--steps", "2", "--warmup", "1",
+                  "--roofline-steps", "1", "--no-cpu-baseline")
+    assert d["config"]["candidates_per_rank_step"] == 16 and d["slice"]["of_world"] == 8
+    assert d["check"]["info"] == 0 and d["check"]["rel_vs_oracle"] <= 1e-9
