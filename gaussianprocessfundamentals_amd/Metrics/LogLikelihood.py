@@ -45,8 +45,17 @@ class LogLikelihood(AbstractLogLikelihood):
             self.covariance_matrix.reset()
             self.last_covariance_matrix = None
         approx = self.local_approx in _MATRIX_APPROX
-        if approx and _wants_grad(hyper_parameter, noise):
-            raise NotImplementedError("gradients through the %s approximation are not provided" % self.local_approx)
+        H = mht.NumericalMatrixHandlingType
+        if approx and _wants_grad(hyper_parameter, noise, indices) and not (
+                self.local_approx is mht.MatrixApproximations.SKI and self.numerical_matrix_handling is H.CHOLESKY_BASED):
+            # what the reference's tape sees through the approximate metric (Optimizer/Fitter.py:76-87,
+            # :124-132, :155-156): hyperparameters, noise and -- Nystroem -- the inducing inputs
+            if self.numerical_matrix_handling is H.LINEAR_CONJUGATE_GRADIENT:
+                raise NotImplementedError("gradients through LINEAR_CONJUGATE_GRADIENT are not provided")
+            if self.data_input.data_x_train.dim() == 3:
+                raise NotImplementedError("approximate metrics are provided for DataInput, not BatchDataInput")
+            z = indices if isinstance(indices, torch.Tensor) else None
+            return _ApproxNegLogLikelihood.apply(self, z, _as_tensor(noise), *[_as_tensor(h) for h in hyper_parameter])
         if _wants_grad(hyper_parameter, noise):
             if self.numerical_matrix_handling is mht.NumericalMatrixHandlingType.LINEAR_CONJUGATE_GRADIENT:
                 # the reference's tape differentiates the CG iterations (tolerance 1e-2); the analytic
@@ -124,11 +133,76 @@ class LogLikelihood(AbstractLogLikelihood):
         if reset:
             self.covariance_matrix.reset()
             self.last_covariance_matrix = None
+        H = mht.NumericalMatrixHandlingType
+        if self.local_approx in _MATRIX_APPROX and not (self.local_approx is mht.MatrixApproximations.SKI and
+                                                        self.numerical_matrix_handling is H.CHOLESKY_BASED):
+            raise NotImplementedError("approximate metrics: differentiate get_metric(hyper_parameter, noise, "
+                                      "indices) with autograd (inducing-input gradients included)")
+        if self.numerical_matrix_handling is H.LINEAR_CONJUGATE_GRADIENT:
+            raise NotImplementedError("gradients through LINEAR_CONJUGATE_GRADIENT are not provided")
         if self.data_input.data_x_train.dim() == 3:
-            raise NotImplementedError("gradients of the BatchDataInput aggregate (Q7) are not provided")
+            return self._batch_metric_and_gradient(hyper_parameter, noise)
+        if self.numerical_matrix_handling in (H.STRICT_INVERSE, H.PSEUDO_INVERSE) and \
+                not self._positive_definite(hyper_parameter, noise):
+            return self._eigen_metric_and_gradient(hyper_parameter, noise)
         f = self.covariance_matrix.inverse_factorization(hyper_parameter, noise, gradient=True)
         g = f.gradient()[0].clone()
         return f.nlml().reshape(1, 1).clone(), _split_like(g[:-1], hyper_parameter), g[-1]
+
+    def _batch_metric_and_gradient(self, hyper_parameter: List, noise):
+        """BatchDataInput (quirk Q7).  CHOLESKY_BASED: -LML = -agg_b(-1/2 fit_b - 1/2 sum_b' logdet_b' - c):
+        with agg = mean, 1/2 mean fit + 1/2 sum logdet + c, whose gradient is the sum over members of the
+        per-member gradient with y scaled by 1 / sqrt(B) (alpha alpha^T weighted 1 / B); with agg = sum,
+        B times that.  STRICT / PSEUDO inverse ([B, 1, B] broadcast, Metrics/LogLikelihood.py:39-63): mean
+        fit + mean log-determinant, i.e. the mean of the per-member gradients (sum: B^2 entries, B times
+        their sum).  One batched identity-augmented factorisation + gradient pass (gpk_nlml_grad)."""
+        H = mht.NumericalMatrixHandlingType
+        agg = global_param.p_batch_metric_aggregator or torch.mean
+        if agg is not torch.mean and agg is not torch.sum:
+            raise NotImplementedError("batch gradients for p_batch_metric_aggregator in (torch.mean, torch.sum)")
+        B = int(self.data_input.data_x_train.shape[0])
+        chol = self.numerical_matrix_handling is H.CHOLESKY_BASED
+        value = self.get_metric([_as_tensor(h).detach() for h in hyper_parameter], _as_tensor(noise).detach(),
+                                reset=True)
+        f = self.covariance_matrix.inverse_factorization(hyper_parameter, noise, gradient=True,
+                                                         y_scale=(1.0 / math.sqrt(B)) if chol else 1.0)
+        g = f.gradient().sum(0)
+        if chol:
+            g = g * (float(B) if agg is torch.sum else 1.0)
+        else:
+            g = g * (float(B) if agg is torch.sum else 1.0 / B)
+        return value, _split_like(g[:-1], hyper_parameter), g[-1]
+
+    def _eigen_metric_and_gradient(self, hyper_parameter: List, noise):
+        """STRICT / PSEUDO inverse of a K + noise I that is not positive definite (eigendecomposition route of
+        Metrics.py): -LML = 1/2 y^T f(K) y + 1/2 sum_i log|lam_i| + c with f = 1/lam (STRICT: every
+        eigenvalue; PSEUDO: tf.linalg.pinv's kept ones).  Adjoint of K: 1/2 V diag(1/lam) V^T (slogdet) plus
+        pinv's reverse mode of 1/2 y y^T (gpk_pinv_backward_scale; = -1/2 alpha alpha^T without truncation);
+        then gpk_kernel_vjp for the hyperparameters and its trace for the noise."""
+        from .. import engine
+        H = mht.NumericalMatrixHandlingType
+        value = self._get_metric_by_strategy(hyper_parameter, noise).reshape(1, 1)
+        lam, V = self._eigen(hyper_parameter, noise)
+        rcond = 0.0 if self.numerical_matrix_handling is H.STRICT_INVERSE else -1.0
+        _, _, mu_all = engine.pinv_factor(lam, V, 0, rcond=0.0, return_mu=True)
+        _, _, mu = engine.pinv_factor(lam, V, 0, rcond=rcond, return_mu=True)
+        y = self._y(None)
+        vy = engine.dgemm(V, y, trans_a=True)                             # V^T y
+        T = engine.dgemm(vy, vy, trans_b=True, alpha=0.5)                 # V^T (1/2 y y^T) V
+        kbar = engine.pinv_backward(lam, V, mu, T=T)
+        kbar = kbar + 0.5 * engine.dgemm(V * mu_all[None, :], V, trans_b=True)
+        x = self.data_input.data_x_train
+        gh, _ = engine.kernel_vjp(self.covariance_matrix.kernel, hyper_parameter, x, x,
+                                  G=(kbar + kbar.T).contiguous())
+        return value, _split_like(0.5 * gh, hyper_parameter), torch.trace(kbar)
+
+    def get_gradients(self, hyper_parameter: List, noise, reset: bool = True) -> torch.Tensor:
+        """Metrics.py:31 (AbstractMetric.get_gradients; the reference's gradient_function of
+        Optimizer/ConjugateGradient.py:28-31 calls it): d(-LML)/d(hyperparameters) as one flat vector in
+        DFS order (the serialised layout of BasicGPComponent.serialize_hyper_parameter) -- the device
+        gradient of get_metric_and_gradient."""
+        _, grads, _ = self.get_metric_and_gradient(hyper_parameter, noise, reset=reset)
+        return torch.cat([g.reshape(-1) for g in grads]) if grads else torch.zeros(0, dtype=torch.float64)
 
     def get_metric_checked(self, hyper_parameter: List, noise, reset: bool = True) -> torch.Tensor:
         """get_metric that raises CholeskyError when K + noise I is not positive definite
@@ -146,10 +220,10 @@ def _as_tensor(h) -> torch.Tensor:
     return h if isinstance(h, torch.Tensor) else torch.as_tensor(h, dtype=torch.float64)
 
 
-def _wants_grad(hyper_parameter, noise) -> bool:
+def _wants_grad(hyper_parameter, noise, indices=None) -> bool:
     if not torch.is_grad_enabled():
         return False
-    return any(isinstance(h, torch.Tensor) and h.requires_grad for h in list(hyper_parameter) + [noise])
+    return any(isinstance(h, torch.Tensor) and h.requires_grad for h in list(hyper_parameter) + [noise, indices])
 
 
 def _split_like(flat: torch.Tensor, hyper_parameter) -> List[torch.Tensor]:
@@ -168,8 +242,11 @@ class _NegLogLikelihood(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, metric, noise, *hyper_parameter):
+        H = mht.NumericalMatrixHandlingType
         nl, grads, gnoise = metric.get_metric_and_gradient(list(hyper_parameter), noise, reset=False)
-        if metric.numerical_matrix_handling is not mht.NumericalMatrixHandlingType.CHOLESKY_BASED:
+        if metric.numerical_matrix_handling is not H.CHOLESKY_BASED and metric.data_input.data_x_train.dim() == 2:
+            # the value of the selected handling (STRICT / PSEUDO inverse of a positive-definite K: the
+            # gradient is the Cholesky one; otherwise both come from the eigendecomposition route)
             nl = metric._get_metric_by_strategy(list(hyper_parameter), noise).reshape(1, 1)
         ctx.save_for_backward(gnoise, *grads)
         ctx.meta = [(h.device, h.dtype) for h in (noise,) + hyper_parameter]
@@ -183,6 +260,71 @@ class _NegLogLikelihood(torch.autograd.Function):
         for g, (dev, dt) in zip(saved, ctx.meta):
             res.append((g * s).to(device=dev, dtype=dt))
         return tuple(res)
+
+
+class _ApproxNegLogLikelihood(torch.autograd.Function):
+    """-LML under BASIC_NYSTROEM / SKC_LOWER_BOUND / SKI (STRICT / PSEUDO) as an autograd node: forward is
+    the device metric, backward the device reverse mode of Metrics/_approx_grad.py (adjoints of the
+    hyperparameters, the noise and the inducing inputs).  The Nystroem log-determinant contributes only when
+    this call computes it (the reference caches it across calls, so a cached value is a constant for the
+    tape)."""
+
+    @staticmethod
+    def forward(ctx, metric, z, noise, *hyper_parameter):
+        A = mht.MatrixApproximations
+        hyp = [h.detach() for h in hyper_parameter]
+        zd = z.detach() if isinstance(z, torch.Tensor) else z
+        nys = metric.local_approx in (A.BASIC_NYSTROEM, A.SKC_LOWER_BOUND)
+        ctx.fresh_det = nys and metric.nystroem_matrix.K_approx_det is None
+        nl = metric._get_metric_by_strategy(hyp, noise.detach(), zd).reshape(1, 1)
+        ctx.metric, ctx.hyp, ctx.z, ctx.noise = metric, hyp, zd, noise.detach()
+        ctx.want_z = isinstance(z, torch.Tensor) and z.requires_grad
+        ctx.meta = [(h.device, h.dtype, h.shape) for h in (noise,) + hyper_parameter]
+        ctx.z_meta = (z.device, z.dtype, z.shape) if isinstance(z, torch.Tensor) else None
+        return nl.clone()
+
+    @staticmethod
+    def backward(ctx, gout):
+        from . import _approx_grad as ag
+        from .. import engine
+        A = mht.MatrixApproximations
+        H = mht.NumericalMatrixHandlingType
+        m, hyp, noise = ctx.metric, ctx.hyp, ctx.noise
+        nv = float(noise)
+        X = m.data_input.data_x_train
+        kernel = m.covariance_matrix.kernel
+        if m.local_approx is A.SKI:
+            alpha_hat = m.get_alpha(hyp, noise, None, ctx.z)
+            Ainv = m._approx_factorization(hyp, noise, ctx.z).k_inv(0).to(torch.float64).contiguous()
+            gh, gn = ag.ski_adjoint(m, hyp, noise, alpha_hat, Ainv)
+            gz = None
+        else:
+            Z = engine.as_device_f64(ctx.z)
+            Z = Z.reshape(-1, 1) if Z.dim() == 1 else Z
+            adj = ag.NystroemAdjoint(kernel, hyp, X, Z, nv)
+            if m.numerical_matrix_handling is H.CHOLESKY_BASED:
+                adj.exact_fit(m.covariance_matrix.get_L_alpha(hyp, noise), 0.5)
+            else:
+                adj.approx_fit(m.get_alpha(hyp, noise, None, ctx.z), 0.5)
+            if ctx.fresh_det:
+                adj.nystroem_logdet(0.5)
+            if m.local_approx is A.SKC_LOWER_BOUND:
+                adj.trace_correction(1.0 / (2.0 * float(global_param.p_cov_matrix_jitter)))
+            gh, gn, gz = adj.finish(ctx.want_z)
+        s = gout.reshape(())
+        out = [None]
+        if ctx.z_meta is None:
+            out.append(None)
+        elif gz is None or not ctx.want_z:
+            out.append(None)
+        else:
+            dev, dt, shp = ctx.z_meta
+            out.append((gz * s).reshape(shp).to(device=dev, dtype=dt))
+        dev, dt, shp = ctx.meta[0]
+        out.append((gn * s).reshape(shp).to(device=dev, dtype=dt))
+        for g, (dev, dt, shp) in zip(_split_like(gh, hyp), ctx.meta[1:]):
+            out.append((g * s).reshape(shp).to(device=dev, dtype=dt))
+        return tuple(out)
 
 
 def blockwise_hyper_parameter_offset(_gp) -> int:

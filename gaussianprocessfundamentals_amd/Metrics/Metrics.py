@@ -55,7 +55,10 @@ class AbstractMetric:
         raise NotImplementedError
 
     def get_gradients(self, hyper_parameter: List, noise, reset: bool = True) -> torch.Tensor:
-        raise NotImplementedError("LML gradients are SURVEY §8f 'next'")
+        """Metrics.py:31: an abstract stub in the reference (``pass``).  LogLikelihood overrides it with the
+        device gradient (get_metric_and_gradient); metrics without one say so."""
+        raise NotImplementedError("%s provides no gradient; LogLikelihood.get_gradients does"
+                                  % type(self).__name__)
 
 
 class Metric(AbstractMetric):

@@ -170,7 +170,7 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
             if f.batch == 1 and self.data_input.data_x_train.dim() == 2:
                 self.L_alpha = f.alpha(0).reshape(-1, 1)
             else:
-                self.L_alpha = torch.stack([f.alpha(b).reshape(-1, 1) for b in range(f.batch)])
+                self.L_alpha = f.alphas().reshape(f.batch, -1, 1)  # one batched solve for every member
         return self.L_alpha
 
     def _inverse_factorization(self, hyper_parameter, noise):
@@ -181,10 +181,11 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
             self._inv_fact.check_info()
         return self._inv_fact
 
-    def inverse_factorization(self, hyper_parameter, noise, gradient: bool = True):
+    def inverse_factorization(self, hyper_parameter, noise, gradient: bool = True, y_scale: float = 1.0):
         """One factorisation with identity extra rows (engine.InverseFactorization): -LML, K^-1,
         L^-1, alpha and (gradient=True) d(-LML)/d(hyperparameters, noise) for every member of a
-        DataInput (batch 1) or BatchDataInput (one member per batch entry).  Not memoised."""
+        DataInput (batch 1) or BatchDataInput (one member per batch entry).  y_scale multiplies the
+        targets (the batch aggregate's gradient weights the data fit by 1 / B).  Not memoised."""
         self._require_data()
         if not _is_scalar(noise):
             raise Exception("No Data Input given or Noise unspecified")
@@ -193,7 +194,8 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
         kd = engine.kernel_descriptor(self.kernel, d)
         hyp = engine.pack_hyper_parameter(hyper_parameter, kd.n_hyp)
         f = engine.InverseFactorization(n, d, batch, global_param.p_dtype)
-        yv = y.reshape(batch, n).to(torch.float64).contiguous()
+        yv = y.reshape(batch, n).to(torch.float64)
+        yv = (yv * y_scale if y_scale != 1.0 else yv).contiguous()
         f.run(kd, hyp, 0, noise_vector(noise), 0, x.contiguous(), n * d if batch > 1 else 0, yv,
               n if batch > 1 else 0, gradient=gradient)
         self.kernel._record_hyper_parameter(list(hyper_parameter))

@@ -32,6 +32,7 @@ EXPORTS = (
     "gpk_finalize_ragged", "gpk_nlml_ragged", "gpk_gemv",
     "gpk_assemble_dense", "gpk_dgemm", "gpk_syevj_workspace_bytes", "gpk_syevj", "gpk_pinv_factor",
     "gpk_ski_weights", "gpk_add_diagonal", "gpk_distance_matrix", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower",
+    "gpk_kernel_vjp_workspace_bytes", "gpk_kernel_vjp", "gpk_pinv_backward_scale",
 )
 
 
@@ -111,6 +112,10 @@ def _declare(lib):
         "gpk_nlml_batched": (c_int, [POINTER(GpkKdesc), c_int32, P, P, c_int, P, P, c_int64, c_int32, P, c_size_t,
                                      P, P, P]),
         "gpk_potrf_lower": (c_int, [c_int, P, c_int64, c_int64, P, c_size_t, P, P, P]),
+        "gpk_pinv_backward_scale": (c_int, [c_int64, c_int32, P, P, P, P]),
+        "gpk_kernel_vjp_workspace_bytes": (c_size_t, [POINTER(GpkKdesc), c_int64, c_int64, c_int32, c_int32]),
+        "gpk_kernel_vjp": (c_int, [POINTER(GpkKdesc), P, P, c_int64, P, c_int64, c_int32, P, c_int64, P, P, P, P,
+                                   P, c_size_t, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

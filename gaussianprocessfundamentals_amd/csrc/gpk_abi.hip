@@ -1130,6 +1130,17 @@ int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam
   return 0;
 }
 
+int gpk_pinv_backward_scale(int64_t m, int32_t batch, const double* lam, const double* mu, double* T, void* stream) {
+  if (m <= 0) return fail_arg(1, "m");
+  if (batch <= 0) return fail_arg(2, "batch");
+  if (!lam) return fail_arg(3, "lam");
+  if (!mu) return fail_arg(4, "mu");
+  if (!T) return fail_arg(5, "T");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(launch_pinv_bwd_scale(lam, mu, (int)m, T, batch, s), "pinv_backward_scale");
+  return 0;
+}
+
 int gpk_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int32_t d, double* Wm, double* work,
                     void* stream) {
   if (!X) return fail_arg(1, "X");
@@ -1158,6 +1169,42 @@ int gpk_distance_matrix(int mode, const double* A, int64_t n, int64_t a_bstride,
   if (ldo < m) return fail_arg(11, "ldo");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   GPK_HIP(launch_distance(mode, A, n, a_bstride, B, m, b_bstride, d, batch, out, ldo, o_bstride, s), "distance");
+  return 0;
+}
+
+size_t gpk_kernel_vjp_workspace_bytes(const gpk_kdesc* kd, int64_t n, int64_t m, int32_t d, int32_t want_z) {
+  if (!kd || n <= 0 || m <= 0 || d <= 0) return 0;
+  return vjp_workspace_elems(*kd, n, m, d, want_z != 0) * sizeof(double);
+}
+
+int gpk_kernel_vjp(const gpk_kdesc* kd, const double* hyp_dev, const double* X, int64_t n, const double* Z, int64_t m,
+                   int32_t d, const double* G, int64_t ldg, const double* gu, const double* gv, double* grad_hyp,
+                   double* grad_z, void* work, size_t work_bytes, void* stream) {
+  if (!valid_kdesc(kd, d)) return fail_arg(1, "kernel descriptor");
+  if (!hyp_dev && kd->n_hyp > 0) return fail_arg(2, "hyp_dev");
+  if (!X) return fail_arg(3, "X");
+  if (n <= 0) return fail_arg(4, "n");
+  if (!Z) return fail_arg(5, "Z");
+  if (m <= 0) return fail_arg(6, "m");
+  if (d <= 0 || d > GPK_MAX_DIM) return fail_arg(7, "d");
+  if (!G && !(gu && gv)) return fail_arg(8, "G (or the rank-1 weights gu, gv)");
+  if (G && ldg < m) return fail_arg(9, "ldg");
+  if (!grad_hyp && kd->n_hyp > 0) return fail_arg(12, "grad_hyp");
+  if (!work || work_bytes < gpk_kernel_vjp_workspace_bytes(kd, n, m, d, grad_z != nullptr ? 1 : 0))
+    return fail_arg(14, "work (see gpk_kernel_vjp_workspace_bytes)");
+  VjpArgs g;
+  memset(&g, 0, sizeof(g));
+  g.hyp = hyp_dev;
+  g.G = G;
+  g.ldg = ldg;
+  g.gu = gu;
+  g.gv = gv;
+  g.part_h = static_cast<double*>(work);
+  adjoint_masks(*kd, g.adj_mask);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(timed(6, 0.0, 8.0 * (double)n * (double)m, s,
+                [&] { return launch_vjp(*kd, g, X, n, Z, m, d, grad_hyp, grad_z, s); }),
+          "kernel_vjp");
   return 0;
 }
 

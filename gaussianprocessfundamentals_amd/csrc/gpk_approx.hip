@@ -274,6 +274,33 @@ __global__ __launch_bounds__(256) void pinv_mu_kernel(const double* lam, int m, 
   if (tid == 0) rank[b] = (cnt[0] >> 20) ? -1 : (cnt[0] & ((1 << 20) - 1));
 }
 
+// Reverse mode of tf.linalg.pinv on a symmetric matrix A = V diag(lam) V^T (Statistics/Nystroem_K.py:53,
+// the gradient TensorFlow's SVD backward gives for the kept singular values): with T = V^T Pbar V,
+// Abar = V (F o sym(T)) V^T, F_ij = (f_i - f_j) / (lam_i - lam_j), f = 1/lam on the kept values, 0 on the
+// dropped ones (mu of pinv_mu_kernel, mode 0): kept / kept -mu_i mu_j (the same quotient without its
+// cancellation), kept i / dropped j mu_i / (lam_i - lam_j), dropped / dropped 0.  In place, one thread per
+// pair i <= j.
+__global__ __launch_bounds__(256) void pinv_bwd_scale_kernel(const double* lam, const double* mu, int m, double* T) {
+  const int b = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t mm = (int64_t)m * m;
+  if (e >= mm) return;
+  const int i = (int)(e / m), j = (int)(e % m);
+  if (j < i) return;
+  const double* l = lam + (int64_t)b * m;
+  const double* u = mu + (int64_t)b * m;
+  double* Tb = T + b * mm;
+  const double t = 0.5 * (Tb[(int64_t)i * m + j] + Tb[(int64_t)j * m + i]);
+  const double ui = u[i], uj = u[j];
+  double f;
+  if (ui != 0.0 && uj != 0.0) f = -ui * uj;
+  else if (ui != 0.0) f = ui / (l[i] - l[j]);
+  else if (uj != 0.0) f = uj / (l[j] - l[i]);
+  else f = 0.0;
+  Tb[(int64_t)i * m + j] = f * t;
+  Tb[(int64_t)j * m + i] = f * t;
+}
+
 __global__ __launch_bounds__(256) void scale_cols_kernel(const double* V, const double* mu, int m, double* U) {
   const int b = blockIdx.y;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -474,6 +501,12 @@ hipError_t launch_pinv_factor(const double* V, const double* lam, int m, double 
   hipLaunchKernelGGL(pinv_mu_kernel, dim3(batch), dim3(256), 0, s, lam, m, rcond, mode, mu, rank);
   const int64_t mm = (int64_t)m * m;
   hipLaunchKernelGGL(scale_cols_kernel, dim3((unsigned)((mm + 255) / 256), batch), dim3(256), 0, s, V, mu, m, U);
+  return hipGetLastError();
+}
+
+hipError_t launch_pinv_bwd_scale(const double* lam, const double* mu, int m, double* T, int32_t batch, hipStream_t s) {
+  const int64_t mm = (int64_t)m * m;
+  hipLaunchKernelGGL(pinv_bwd_scale_kernel, dim3((unsigned)((mm + 255) / 256), batch), dim3(256), 0, s, lam, mu, m, T);
   return hipGetLastError();
 }
 

@@ -558,7 +558,240 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(GradArgs g, int64_t nt
   if (tid == 0) g.grad[(int64_t)b * np1 + p] = g.info[b] != 0 ? NAN : 0.5 * red[0];
 }
 
+// ===================================================================== kernel-matrix reverse mode
+// gpk_kernel_vjp: for a weight matrix G [n, m] (the adjoint of K(X, Z) = kernel(X, Z), as TensorFlow's
+// tape would hand it back from the ops downstream of get_tf_tensor), the hyperparameter adjoints
+// sum_ij G_ij dK_ij / d theta_p and the adjoints of the SECOND argument's points, sum_i G_ij dK_ij / d z_jk
+// (the inducing inputs of the Nystroem metrics, Optimizer/Fitter.py:76-87,128-130).  A symmetric K(Z, Z)
+// is handled by the caller with G + G^T (k(a, b) = k(b, a)).  Derivatives are the analytic ones of the
+// reference formulas; at coincident points the distance terms differentiate to 0 (tf.abs' sign(0)
+// = 0 for the L1 kernels; for SE the reference's sqrt-then-square, Auxiliary/Distances.py:5-7, would
+// give TensorFlow's 0 * inf = NaN there -- the analytic limit 0 is returned instead).
+
+// acc_z[k] += coef * d k_node(a, b) / d b_k in the node's own coordinates (ARD nodes: scaled points)
+__device__ __forceinline__ void base_input_partials(const gpk_node& nd, const double* __restrict__ hyp,
+                                                    const double* a, const double* b, int d, double coef,
+                                                    double (&acc)[GPK_MAX_DIM]) {
+  const int fl = nd.flags;
+  const bool ard = (fl & GPK_NODE_ARD) != 0;
+  const bool scaled = (fl & GPK_NODE_SCALED) != 0;
+  const double* h = hyp + nd.hyp_offset;
+  const double v = base_value(nd, hyp, a, b, d);  // includes sg
+  if (nd.op == GPK_OP_SE) {
+    const double l = ard ? 1.0 : h[0];
+    const double c = coef * v / (l * l);
+#pragma unroll
+    for (int k = 0; k < GPK_MAX_DIM; ++k)
+      if (k < d) acc[k] += c * (a[k] - b[k]);
+    return;
+  }
+  if (nd.op == GPK_OP_PER) {
+    const double l = h[0], per = h[1];
+    const double c = coef * v * (-2.0 / (l * l)) * (PI / per);  // d k / d sn * d theta / d |t|
+    if (fl & GPK_NODE_STANDARD) {
+#pragma unroll
+      for (int k = 0; k < GPK_MAX_DIM; ++k)
+        if (k < d) {
+          const double t = a[k] - b[k];
+          const double th = PI * (fabs(t) / per);
+          const double sgn = t > 0.0 ? 1.0 : (t < 0.0 ? -1.0 : 0.0);
+          acc[k] += c * sin(2.0 * th) * (-sgn);
+        }
+    } else {
+      double dist = 0.0;
+      for (int k = 0; k < d; ++k) dist += fabs(a[k] - b[k]);
+      const double s2 = sin(2.0 * PI * (dist / per));
+#pragma unroll
+      for (int k = 0; k < GPK_MAX_DIM; ++k)
+        if (k < d) {
+          const double t = a[k] - b[k];
+          const double sgn = t > 0.0 ? 1.0 : (t < 0.0 ? -1.0 : 0.0);
+          acc[k] += c * s2 * (-sgn);
+        }
+    }
+    return;
+  }
+  // MAT32 / MAT52: k = sg r(f), f = c dist / |l|
+  const bool std_form = (fl & GPK_NODE_STANDARD) != 0;
+  double dist = 0.0;
+  if (std_form) {
+    for (int k = 0; k < d; ++k) {
+      const double t = a[k] - b[k];
+      dist += t * t;
+    }
+    dist = sqrt(dist);
+  } else {
+    for (int k = 0; k < d; ++k) dist += fabs(a[k] - b[k]);
+  }
+  const double cc = (nd.op == GPK_OP_MAT52) ? SQRT5 : SQRT3;
+  const double sg = scaled ? h[ard ? d : 1] : 1.0;
+  const double l = ard ? 1.0 : fabs(h[0]);
+  const double f = (cc * dist) / l;
+  const double e = exp(-f);
+  const double drdf = (nd.op == GPK_OP_MAT52) ? -(f / 3.0) * (1.0 + f) * e : -f * e;
+  const double c = coef * sg * drdf * (cc / l);  // times d dist / d b_k
+#pragma unroll
+  for (int k = 0; k < GPK_MAX_DIM; ++k)
+    if (k < d) {
+      const double t = a[k] - b[k];
+      double dd;
+      if (std_form) dd = dist > 0.0 ? -t / dist : 0.0;
+      else dd = -(t > 0.0 ? 1.0 : (t < 0.0 ? -1.0 : 0.0));
+      acc[k] += c * dd;
+    }
+}
+
+// one 64 x 64 tile of K(X, Z) per workgroup (row tile ti = blockIdx.y, column tile tj = blockIdx.x);
+// lane = column, wave w = rows w, w + 4, ...; per-tile partial sums to the workspace, reduced in a
+// fixed order by vjp_reduce_kernel (deterministic)
+__global__ __launch_bounds__(256) void vjp_kernel(gpk_kdesc kd, AsmArgs a, VjpArgs g) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int slot_stride = ATILE * a.dp;
+  double* hyp_s = smem;                                  // GPK_MAX_HYP
+  double* red = hyp_s + GPK_MAX_HYP;                     // [4 waves][GNP]
+  double* zred = red + 4 * GNP;                          // [4 waves][64][d]
+  double* prow = zred + 4 * ATILE * a.d;
+  double* pcol = prow + (1 + kd.n_ard) * slot_stride;
+  double* vals = pcol + (1 + kd.n_ard) * slot_stride;    // [n_nodes][256] node values (MUL trees)
+
+  const int64_t ti = blockIdx.y, tj = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < kd.n_hyp; e += 256) hyp_s[e] = g.hyp[e];
+  __syncthreads();
+  const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
+  stage_points(kd, a, hyp_s, prow, gi0, 0, true, slot_stride);
+  stage_points(kd, a, hyp_s, pcol, gj0, 0, false, slot_stride);
+  __syncthreads();
+  const int c = lane;
+  const int64_t gj = gj0 + c;
+  double* part = g.part_h + (ti * (int64_t)gridDim.x + tj) * kd.n_hyp;
+  double gz[GPK_MAX_DIM];
+#pragma unroll
+  for (int k = 0; k < GPK_MAX_DIM; ++k) gz[k] = 0.0;
+  for (int qn = 0; qn < kd.n_nodes; ++qn) {
+    const gpk_node nd = kd.nodes[qn];
+    if (nd.op == GPK_OP_ADD || nd.op == GPK_OP_MUL) continue;
+    const uint32_t mask = g.adj_mask[qn];
+    const bool ard = (nd.flags & GPK_NODE_ARD) != 0;
+    const int off = ard ? (nd.ard_slot + 1) * slot_stride : 0;
+    double acc[GNP], az[GPK_MAX_DIM];
+#pragma unroll
+    for (int k = 0; k < GNP; ++k) acc[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < GPK_MAX_DIM; ++k) az[k] = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < ATILE / 4; ++k) {
+      const int rr = wave + 4 * k;
+      const int64_t gi = gi0 + rr;
+      if (gi >= a.n || gj >= a.m) continue;
+      const double qk = g.G ? g.G[gi * g.ldg + gj] : g.gu[gi] * g.gv[gj];
+      if (qk == 0.0) continue;
+      double adj = 1.0;
+      if (mask != 0u) {
+        eval_nodes(kd, hyp_s, prow + rr * a.dp, pcol + c * a.dp, slot_stride, a.d, vals + tid);
+#pragma unroll 1
+        for (int q = 0; q < kd.n_nodes; ++q)
+          if (mask & (1u << q)) adj *= vals[q * 256 + tid];
+      }
+      base_partials(nd, hyp_s, prow + off + rr * a.dp, pcol + off + c * a.dp, a.d, qk * adj, acc);
+      if (g.want_z) base_input_partials(nd, hyp_s, prow + off + rr * a.dp, pcol + off + c * a.dp, a.d, qk * adj, az);
+    }
+    // raw coordinates: an ARD node sees z_k / l_k
+#pragma unroll
+    for (int k = 0; k < GPK_MAX_DIM; ++k)
+      if (k < a.d) gz[k] += ard ? az[k] / hyp_s[nd.hyp_offset + k] : az[k];
+    const int nshape = ard ? a.d : (nd.op == GPK_OP_PER ? 2 : 1);
+    const bool scaled = (nd.flags & GPK_NODE_SCALED) != 0;
+    const bool sg_moved = ard && scaled;
+    const int np = nshape + (scaled ? 1 : 0);
+#pragma unroll
+    for (int k = 0; k < GNP; ++k) {
+      if (k < np) {
+        const double sres = wave_sum((sg_moved && k == a.d) ? acc[GPK_MAX_DIM] : acc[k]);
+        if (lane == 0) red[wave * GNP + k] = sres;
+      }
+    }
+    __syncthreads();
+    if (tid < np) part[nd.hyp_offset + tid] = red[tid] + red[GNP + tid] + red[2 * GNP + tid] + red[3 * GNP + tid];
+    __syncthreads();
+  }
+  if (!g.want_z) return;
+  for (int k = 0; k < a.d; ++k) zred[(wave * ATILE + c) * a.d + k] = gz[k];
+  __syncthreads();
+  for (int e = tid; e < ATILE * a.d; e += 256) {
+    const int cc = e / a.d, k = e - cc * a.d;
+    if (gj0 + cc < a.m)
+      g.part_z[(ti * a.m + gj0 + cc) * a.d + k] = zred[(0 * ATILE + cc) * a.d + k] + zred[(1 * ATILE + cc) * a.d + k] +
+                                                   zred[(2 * ATILE + cc) * a.d + k] + zred[(3 * ATILE + cc) * a.d + k];
+  }
+}
+
+// out[p] = scale * sum_t part[t * stride + p] over t < nt (fixed order); one workgroup per p
+__global__ __launch_bounds__(256) void vjp_reduce_kernel(const double* part, int64_t nt, int64_t stride, double scale,
+                                                         double* out) {
+  __shared__ double red[256];
+  const int64_t p = blockIdx.x;
+  const int tid = threadIdx.x;
+  double s = 0.0;
+  for (int64_t t = tid; t < nt; t += 256) s += part[t * stride + p];
+  red[tid] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) out[p] = scale * red[0];
+}
+
 }  // namespace
+
+size_t vjp_workspace_elems(const gpk_kdesc& kd, int64_t n, int64_t m, int32_t d, bool want_z) {
+  const int64_t tr = (n + ATILE - 1) / ATILE, tc = (m + ATILE - 1) / ATILE;
+  return (size_t)(tr * tc * kd.n_hyp) + (want_z ? (size_t)(tr * m * d) : 0);
+}
+
+hipError_t launch_vjp(const gpk_kdesc& kd, const VjpArgs& g0, const double* X, int64_t n, const double* Z, int64_t m,
+                      int32_t d, double* grad_hyp, double* grad_z, hipStream_t s) {
+  AsmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.hyp = g0.hyp;
+  a.X = X;
+  a.Xs = Z;
+  a.n = n;
+  a.m = m;
+  a.d = d;
+  a.dp = (d % 2 == 0) ? d + 1 : d;
+  a.plain = 1;
+  VjpArgs g = g0;
+  g.want_z = grad_z != nullptr ? 1 : 0;
+  const int64_t tr = (n + ATILE - 1) / ATILE, tc = (m + ATILE - 1) / ATILE;
+  g.part_z = g.part_h + tr * tc * kd.n_hyp;
+  bool has_mul = false;
+  for (int q = 0; q < kd.n_nodes; ++q) has_mul |= g.adj_mask[q] != 0u;
+  const size_t lds = sizeof(double) * (GPK_MAX_HYP + 4 * GNP + 4 * (size_t)ATILE * d +
+                                       2 * (size_t)(1 + kd.n_ard) * ATILE * a.dp +
+                                       (has_mul ? (size_t)kd.n_nodes * 256 : 0));
+  if (kd.n_hyp > 0) {
+    hipLaunchKernelGGL(vjp_kernel, dim3((unsigned)tc, (unsigned)tr), dim3(256), lds, s, kd, a, g);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(vjp_reduce_kernel, dim3((unsigned)kd.n_hyp), dim3(256), 0, s, g.part_h, tr * tc,
+                       (int64_t)kd.n_hyp, 1.0, grad_hyp);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  } else if (g.want_z) {
+    hipLaunchKernelGGL(vjp_kernel, dim3((unsigned)tc, (unsigned)tr), dim3(256), lds, s, kd, a, g);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (g.want_z) {
+    hipLaunchKernelGGL(vjp_reduce_kernel, dim3((unsigned)(m * d)), dim3(256), 0, s, g.part_z, tr, m * (int64_t)d, 1.0,
+                       grad_z);
+    return hipGetLastError();
+  }
+  return hipSuccess;
+}
 
 hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_t batch, hipStream_t s) {
   // the staging helpers read the points through an augmented-layout AsmArgs

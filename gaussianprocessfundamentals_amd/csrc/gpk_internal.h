@@ -150,6 +150,19 @@ struct GradArgs {
   uint32_t adj_mask[GPK_MAX_NODES];  // per node: nodes whose values multiply its adjoint
 };
 
+// gpk_kernel_vjp (gpk_assemble.hip): adjoints of K(X, Z) = kernel(X, Z) for a weight matrix G [n, ldg]
+struct VjpArgs {
+  const double* hyp;   // [n_hyp] device
+  const double* G;     // dense weights, or (G == NULL) the rank-1 weights gu[i] gv[j]
+  int64_t ldg;
+  const double* gu;
+  const double* gv;
+  double* part_h;      // [row tiles * column tiles][n_hyp] per-tile partial sums
+  double* part_z;      // [row tiles][m][d] (set by launch_vjp)
+  int32_t want_z;
+  uint32_t adj_mask[GPK_MAX_NODES];
+};
+
 struct TrsvArgs {
   const void* W;
   int64_t ld;
@@ -170,6 +183,9 @@ hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t 
 hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s);
 hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_t batch, hipStream_t s);
+size_t vjp_workspace_elems(const gpk_kdesc& kd, int64_t n, int64_t m, int32_t d, bool want_z);
+hipError_t launch_vjp(const gpk_kdesc& kd, const VjpArgs& g, const double* X, int64_t n, const double* Z, int64_t m,
+                      int32_t d, double* grad_hyp, double* grad_z, hipStream_t s);
 hipError_t launch_trsv_diag(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x, double* y,
@@ -207,6 +223,7 @@ hipError_t launch_jacobi_out(const double* Af, const double* Vf, int m, double* 
                              hipStream_t s);
 hipError_t launch_pinv_factor(const double* V, const double* lam, int m, double rcond, int mode, double* mu,
                               double* U, int32_t* rank, int32_t batch, hipStream_t s);
+hipError_t launch_pinv_bwd_scale(const double* lam, const double* mu, int m, double* T, int32_t batch, hipStream_t s);
 hipError_t launch_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int d, double* Wm,
                               double* work, hipStream_t s);
 hipError_t launch_copy_lower(const double* src, int64_t lds, double* dst, int64_t ldd, int64_t n, hipStream_t s);

@@ -180,6 +180,7 @@ class AugmentedFactorization:
             E: Optional[torch.Tensor] = None, e_bstride: int = 0):
         lay = self.layout
         B, n, m, d = self.batch, self.n, self.m, self.d
+        self._alphas = None
         # the device reads these extents blindly: check them here (an undersized operand would
         # be read out of bounds, not reported)
         _check_operand("hyper_parameter", hyp, hyp_stride, kd.n_hyp, B, self.W.device)
@@ -258,16 +259,21 @@ class AugmentedFactorization:
     def posterior_var_diag(self, b: int = 0) -> torch.Tensor:
         return self.var[b * self.m:(b + 1) * self.m]
 
+    def alphas(self) -> torch.Tensor:
+        """[batch, n]: alpha_b = L_b^-T z_b = (K_b + noise I)^-1 y_b for every member from ONE batched
+        backward solve (gpk_trsv), computed once per run and kept until the next one."""
+        if getattr(self, "_alphas", None) is None:
+            lay = self.layout
+            x = torch.zeros((self.batch, lay.n_pad), dtype=torch.float64, device=self.W.device)
+            x[:, :self.n] = self.W.view(self.batch, lay.p, lay.ld)[:, lay.y_row, :self.n]
+            nat.check(self.L.gpk_trsv(ctypes.byref(lay), 1, nat.ptr(self.W), nat.ptr(self.Winv),
+                                      nat.ptr(x), nat.stream_handle(self.W.device)), "gpk_trsv")
+            self._alphas = x[:, :self.n]
+        return self._alphas
+
     def alpha(self, b: int = 0) -> torch.Tensor:
-        """alpha = L^-T z = (K + noise I)^-1 y via gpk_trsv (backward solve)."""
-        lay = self.layout
-        x = torch.zeros(self.batch * lay.n_pad, dtype=torch.float64, device=self.W.device)
-        xv = x.view(self.batch, lay.n_pad)
-        for bb in range(self.batch):
-            xv[bb, :self.n] = self.z(bb).to(torch.float64)
-        nat.check(self.L.gpk_trsv(ctypes.byref(lay), 1, nat.ptr(self.W), nat.ptr(self.Winv),
-                                  nat.ptr(x), nat.stream_handle(self.W.device)), "gpk_trsv")
-        return xv[b, :self.n]
+        """alpha = L^-T z = (K + noise I)^-1 y of member b (see :meth:`alphas`)."""
+        return self.alphas()[b]
 
     def check_info(self):
         """Raise CholeskyError if any batch member failed (synchronises)."""
@@ -299,6 +305,7 @@ class InverseFactorization(AugmentedFactorization):
         lay = self.layout
         B, n, d = self.batch, self.n, self.d
         dev = self.W.device
+        self._alphas = None
         _check_operand("hyper_parameter", hyp, hyp_stride, kd.n_hyp, B, dev)
         _check_operand("noise", noise, noise_stride, 1, B, dev)
         _check_operand("X", X, x_bstride, n * d, B, dev)
@@ -379,6 +386,7 @@ class RaggedFactorization(AugmentedFactorization):
         """members[b] = (kdesc, hyp [n_hyp] fp64, X_b [n_b, d], y_b [n_b], Xs_b [m_b, d] or None);
         noise: rank-0 or one value per member."""
         B, n, m, d = self.batch, self.n, self.m, self.d
+        self._alphas = None
         if len(members) != B:
             raise ValueError("expected %d members, got %d" % (B, len(members)))
         dev = self.W.device
@@ -460,14 +468,16 @@ class RaggedFactorization(AugmentedFactorization):
         return self.var[b * self.m:b * self.m + self.test_sizes[b]]
 
     def alphas(self) -> List[torch.Tensor]:
-        """alpha_b = L_b^-T z_b for every member: one batched backward solve (gpk_trsv)."""
-        lay = self.layout
-        x = torch.zeros((self.batch, lay.n_pad), dtype=torch.float64, device=self.W.device)
-        for b in range(self.batch):
-            x[b, :self.sizes[b]] = self.z(b).to(torch.float64)
-        nat.check(self.L.gpk_trsv(ctypes.byref(lay), 1, nat.ptr(self.W), nat.ptr(self.Winv),
-                                  nat.ptr(x), nat.stream_handle(self.W.device)), "gpk_trsv")
-        return [x[b, :self.sizes[b]] for b in range(self.batch)]
+        """alpha_b = L_b^-T z_b for every member: one batched backward solve (gpk_trsv; a member's
+        padding rows carry z = 0), computed once per run."""
+        if getattr(self, "_alphas", None) is None:
+            lay = self.layout
+            x = torch.zeros((self.batch, lay.n_pad), dtype=torch.float64, device=self.W.device)
+            x[:, :self.n] = self.W.view(self.batch, lay.p, lay.ld)[:, lay.y_row, :self.n]
+            nat.check(self.L.gpk_trsv(ctypes.byref(lay), 1, nat.ptr(self.W), nat.ptr(self.Winv),
+                                      nat.ptr(x), nat.stream_handle(self.W.device)), "gpk_trsv")
+            self._alphas = [x[b, :self.sizes[b]] for b in range(self.batch)]
+        return self._alphas
 
     def alpha(self, b: int = 0) -> torch.Tensor:
         return self.alphas()[b]
@@ -557,9 +567,9 @@ def syevj(A: torch.Tensor, max_sweeps: int = 60):
     return lam, V, int(sweeps.value)
 
 
-def pinv_factor(lam: torch.Tensor, V: torch.Tensor, mode: int, rcond: float = -1.0):
+def pinv_factor(lam: torch.Tensor, V: torch.Tensor, mode: int, rcond: float = -1.0, return_mu: bool = False):
     """U = V diag(mu) with tf.linalg.pinv's cutoff (gpk_pinv_factor): mode 0 mu = 1/lam (pinv = U V^T),
-    mode 1 mu = lam^-1/2 (pinv = U U^T).  Returns (U, rank [B] int32 device tensor)."""
+    mode 1 mu = lam^-1/2 (pinv = U U^T).  Returns (U, rank [B] int32 device tensor) (+ mu)."""
     squeeze = V.dim() == 2
     V3 = V.unsqueeze(0) if squeeze else V
     lam2 = lam.unsqueeze(0) if lam.dim() == 1 else lam
@@ -570,6 +580,8 @@ def pinv_factor(lam: torch.Tensor, V: torch.Tensor, mode: int, rcond: float = -1
     nat.check(nat.lib().gpk_pinv_factor(m, batch, nat.ptr(V3.contiguous()), nat.ptr(lam2.contiguous()),
                                         float(rcond), int(mode), nat.ptr(mu), nat.ptr(U), nat.ptr(rank),
                                         nat.stream_handle(V.device)), "gpk_pinv_factor")
+    if return_mu:
+        return (U[0] if squeeze else U), rank, (mu[0] if squeeze else mu)
     return (U[0] if squeeze else U), rank
 
 
@@ -579,6 +591,57 @@ def pinv_sym(A: torch.Tensor, rcond: float = -1.0) -> torch.Tensor:
     lam, V, _ = syevj(A)
     U, _ = pinv_factor(lam, V, 0, rcond)
     return dgemm(U, V, trans_b=True)
+
+
+def pinv_backward(lam: torch.Tensor, V: torch.Tensor, mu: torch.Tensor, Pbar: Optional[torch.Tensor] = None,
+                  T: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Adjoint of a symmetric A from the adjoint Pbar of pinv(A) (tf.linalg.pinv's reverse mode,
+    gpbasics/Statistics/Nystroem_K.py:53): V (F o sym(V^T Pbar V)) V^T with the Daleckii-Krein quotients of
+    f = 1/lam over the kept eigenvalues (gpk_pinv_backward_scale); lam, V from :func:`syevj`, mu the mode-0
+    factors of :func:`pinv_factor`.  T: the adjoint already in the eigenbasis (V^T Pbar V) instead."""
+    m = int(V.shape[-1])
+    if T is None:
+        T = dgemm(dgemm(V, Pbar.contiguous(), trans_a=True), V)
+    T = T.contiguous().clone()
+    nat.check(nat.lib().gpk_pinv_backward_scale(m, 1, nat.ptr(lam.contiguous()), nat.ptr(mu.contiguous()),
+                                                nat.ptr(T), nat.stream_handle(V.device)), "gpk_pinv_backward_scale")
+    return dgemm(dgemm(V, T), V, trans_b=True)
+
+
+def kernel_vjp(kernel, hyper_parameter, X, Z, G: Optional[torch.Tensor] = None, gu: Optional[torch.Tensor] = None,
+               gv: Optional[torch.Tensor] = None, want_z: bool = False):
+    """Reverse mode of K = kernel(X, Z) (gpk_kernel_vjp) for the adjoint G [n, m] of K, or the rank-1
+    adjoint gu gv^T: returns (flat hyperparameter adjoint [n_hyp], adjoint of Z [m, d] or None)."""
+    L = nat.lib()
+    X = as_device_f64(X)
+    Z = as_device_f64(Z)
+    n, d = int(X.shape[0]), int(X.shape[1])
+    m = int(Z.shape[0])
+    kd = kernel_descriptor(kernel, d)
+    hyp = pack_hyper_parameter(hyper_parameter, kd.n_hyp)
+    gh = torch.zeros(max(1, kd.n_hyp), dtype=torch.float64, device=X.device)
+    gz = torch.zeros((m, d), dtype=torch.float64, device=X.device) if want_z else None
+    if n == 0 or m == 0:
+        return gh[:kd.n_hyp], gz
+    if G is not None:
+        G = G.to(dtype=torch.float64)
+        if G.dim() != 2 or tuple(G.shape) != (n, m) or G.stride(1) != 1:
+            raise ValueError("G must be a row-major [%d, %d] matrix" % (n, m))
+        ldg = int(G.stride(0))
+    else:
+        gu = gu.reshape(-1).to(dtype=torch.float64).contiguous()
+        gv = gv.reshape(-1).to(dtype=torch.float64).contiguous()
+        if gu.numel() != n or gv.numel() != m:
+            raise ValueError("rank-1 weights must hold %d and %d values" % (n, m))
+        ldg = m
+    wb = int(L.gpk_kernel_vjp_workspace_bytes(ctypes.byref(kd), n, m, d, int(want_z)))
+    work = torch.empty(max(1, (wb + 7) // 8), dtype=torch.float64, device=X.device)
+    nat.check(L.gpk_kernel_vjp(ctypes.byref(kd), nat.ptr(hyp), nat.ptr(X), n, nat.ptr(Z), m, d,
+                               nat.ptr(G) if G is not None else None, ldg,
+                               nat.ptr(gu) if G is None else None, nat.ptr(gv) if G is None else None,
+                               nat.ptr(gh), nat.ptr(gz) if want_z else None, nat.ptr(work), wb,
+                               nat.stream_handle(X.device)), "gpk_kernel_vjp")
+    return gh[:kd.n_hyp], gz
 
 
 def ski_weights(X: torch.Tensor, Z: torch.Tensor) -> torch.Tensor:
@@ -639,6 +702,7 @@ class DenseFactorization(AugmentedFactorization):
         L = self.L
         lay = self.layout
         self.info.zero_()
+        self._alphas = None
         nat.check(L.gpk_assemble_dense(ctypes.byref(lay), nat.ptr(A3), lda, abs_, nat.ptr(noise_t), ns,
                                        nat.ptr(E) if E is not None else None, ebs, int(self.inverse),
                                        nat.ptr(y), ybs, nat.ptr(self.W), s), "gpk_assemble_dense")

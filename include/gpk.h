@@ -287,6 +287,13 @@ int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
 int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam, double rcond, int32_t mode,
                     double* mu, double* U, int32_t* rank_dev, void* stream);
 
+/* Reverse mode of pinv for symmetric matrices (tf.linalg.pinv, Nystroem_K.py:53, as TensorFlow's tape
+ * differentiates it): with lam, V the eigendecomposition (gpk_syevj) and mu the mode-0 factors of
+ * gpk_pinv_factor, and T = V^T Pbar V for the adjoint Pbar of pinv(A), replaces T (in place, [batch, m, m])
+ * by F o (T + T^T)/2 with F_ij = (mu_i - mu_j) / (lam_i - lam_j) (-mu_i mu_j for two kept values, 0 for two
+ * dropped ones); the adjoint of A is then V T V^T. */
+int gpk_pinv_backward_scale(int64_t m, int32_t batch, const double* lam, const double* mu, double* T, void* stream);
+
 /* SKI interpolation weights W [n, m] (row-major) of training points X [n, d] on inducing points
  * Z [m, d]: get_weight_matrix (StructuredKernelInterpolation.py:31-49), expanded-norm euclidean
  * distances, nearest (all ties) 1 - d1 / (d1 + d2), second nearest d1 / (d1 + d2).
@@ -301,6 +308,23 @@ int gpk_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int3
 int gpk_distance_matrix(int mode, const double* A, int64_t n, int64_t a_bstride, const double* B, int64_t m,
                         int64_t b_bstride, int32_t d, int32_t batch, double* out, int64_t ldo, int64_t o_bstride,
                         void* stream);
+
+/* Reverse mode of the kernel matrix K = kernel(X, Z) (X [n, d], Z [m, d], hyp_dev [kd->n_hyp], all
+ * device fp64) for a weight matrix G [n, ldg] -- or, with G = NULL, the rank-1 weights G_ij = gu[i] gv[j]
+ * (gu [n], gv [m]) -- (the adjoint of K, e.g. what tf.GradientTape hands back
+ * to get_tf_tensor, Optimizer/Fitter.py:124-132 / :155-156, through the Nystroem metrics'
+ * K_nm and K_mm, Statistics/Nystroem_K.py:36-47):
+ *   grad_hyp[p]     = sum_ij G_ij dK_ij / d hyp_p        (device [n_hyp]; may be NULL if n_hyp == 0)
+ *   grad_z[j*d + k] = sum_i  G_ij dK_ij / d Z_jk         (device [m, d]; NULL: not computed)
+ * For a symmetric K(Z, Z) pass X = Z and G + G^T: grad_z is then the full derivative and grad_hyp
+ * twice the hyperparameter adjoint.  Derivatives of the distance terms at coincident points are 0
+ * (tf.abs' sign(0); TensorFlow would give NaN through the SE kernel's sqrt-then-square there).
+ * work: gpk_kernel_vjp_workspace_bytes(kd, n, m, d, grad_z != NULL).  Deterministic (fixed-order
+ * reductions). */
+size_t gpk_kernel_vjp_workspace_bytes(const gpk_kdesc* kd, int64_t n, int64_t m, int32_t d, int32_t want_z);
+int gpk_kernel_vjp(const gpk_kdesc* kd, const double* hyp_dev, const double* X, int64_t n, const double* Z, int64_t m,
+                   int32_t d, const double* G, int64_t ldg, const double* gu, const double* gv, double* grad_hyp,
+                   double* grad_z, void* work, size_t work_bytes, void* stream);
 
 /* A[b] += value * I (the "+ tf.eye(n) * noise" of Nystroem_K.py:68-69 and
  * StructuredKernelInterpolation.py:27). */

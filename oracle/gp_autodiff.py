@@ -143,3 +143,146 @@ def finite_difference(f, hyp: Sequence, noise: float, h: float = 1e-5):
     unpack0 = [u if np.ndim(hyp[k]) else float(u[0]) for k, u in enumerate(flat)]
     gn = (f(unpack0, noise + step) - f(unpack0, noise - step)) / (2 * step)
     return out, gn
+
+
+# ----------------------------------------------------------------------------- approximations (§8f.4)
+def tf_pinv(A: torch.Tensor) -> torch.Tensor:
+    """tf.linalg.pinv (Statistics/Nystroem_K.py:53) in torch, differentiable the way TensorFlow's is: SVD,
+    singular values s > 10 max(shape) eps max(s) inverted, the rest dropped (their reciprocal masked
+    without a NaN in the backward)."""
+    U, s, Vh = torch.linalg.svd(A, full_matrices=False)
+    rcond = 10.0 * max(A.shape) * float(np.finfo(np.float64).eps)
+    keep = s > rcond * s.max()
+    s_safe = torch.where(keep, s, torch.ones_like(s))
+    s_inv = torch.where(keep, 1.0 / s_safe, torch.zeros_like(s))
+    return (Vh.mT * s_inv) @ U.mT
+
+
+def pinv_or_inv(A: torch.Tensor) -> torch.Tensor:
+    """tf_pinv for a matrix whose singular values are all kept is inv(A); differentiate it as inv then.
+    (K_hat + noise I has n - m eigenvalues equal to the noise: an SVD-based backward divides by their zero
+    differences -- TensorFlow regularises that reciprocal -- while the derivative of the pseudo-inverse
+    itself, which is inv's there, is finite.  The device returns that analytic derivative.)"""
+    s = torch.linalg.svdvals(A.detach())
+    rcond = 10.0 * max(A.shape) * float(np.finfo(np.float64).eps)
+    if bool((s > rcond * s.max()).all()):
+        return torch.linalg.inv(A)
+    return tf_pinv(A)
+
+
+def kernel_matrix_t(tree, hyp, x, x_, scaled: bool = False) -> torch.Tensor:
+    """The kernel program in torch (differentiable in hyp and both inputs; direct squared distances for
+    SE, so coincident points differentiate to 0 rather than TensorFlow's sqrt'(0) = inf times 0)."""
+    return _kmat(tree, hyp, x, x_, scaled, False)
+
+
+def nystroem_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, z: np.ndarray,
+                           handling: str = "CHOLESKY_BASED", lower_bound: bool = False, jitter: float = 1e-8,
+                           scaled: bool = False, det_fresh: bool = True):
+    """-LML of BASIC_NYSTROEM / SKC_LOWER_BOUND (gp_oracle.nystroem_nlml, op for op) and its reverse-mode
+    gradient w.r.t. the hyperparameters, the noise and the inducing inputs z -- GradientTape through
+    Optimizer/Fitter.py:124-132.  det_fresh=False treats the Nystroem log-determinant as the constant the
+    reference's cache makes of it after an earlier call (Nystroem_K.py:92-93).
+    Returns (nlml, [d/d h], d/d noise, d/d z or None)."""
+    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
+    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
+    Z = torch.tensor(np.asarray(z, dtype=np.float64), dtype=F64, requires_grad=True)
+    X = torch.as_tensor(np.asarray(x, dtype=np.float64))
+    Y = torch.as_tensor(np.asarray(y, dtype=np.float64)).reshape(-1, 1)
+    n, m = X.shape[0], Z.shape[0]
+    knm = kernel_matrix_t(tree, params, X, Z, scaled)
+    kmm = kernel_matrix_t(tree, params, Z, Z, scaled)
+    P = tf_pinv(kmm)
+    khat = (knm @ P) @ knm.T
+    eye = torch.eye(n, dtype=F64)
+    if handling == "CHOLESKY_BASED":
+        K = kernel_matrix_t(tree, params, X, X, scaled) + nz * eye
+        L = torch.linalg.cholesky(K)
+        alpha = torch.cholesky_solve(Y, L)
+    elif handling == "PSEUDO_INVERSE":
+        alpha = pinv_or_inv(khat + nz * eye) @ Y
+    elif handling == "STRICT_INVERSE":
+        alpha = torch.linalg.inv(khat + nz * eye) @ Y
+    else:
+        raise ValueError(handling)
+    fit = (Y.T @ alpha)[0, 0]
+    to_det = torch.eye(m, dtype=F64) * nz + knm.T @ (knm @ P)
+    det = (n - m) * torch.log(nz) + torch.linalg.slogdet(to_det)[1]
+    if not det_fresh:
+        det = det.detach()
+    ll = -0.5 * fit - 0.5 * det - 0.5 * n * LOG_2PI
+    if lower_bound:
+        kxx = kernel_matrix_t(tree, params, X, X, scaled)
+        ll = ll - (1.0 / (2.0 * jitter)) * torch.trace(khat + nz * eye - kxx)
+    nl = -ll
+    grads = torch.autograd.grad(nl, params + [nz, Z], allow_unused=True)
+    gz = grads[-1]
+    return (float(nl.detach()), [g.numpy() if g is not None else np.zeros(np.shape(h)) for g, h in zip(grads[:-2], hyp)],
+            float(grads[-2]), gz.numpy() if gz is not None else None)
+
+
+def ski_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, m: int,
+                      handling: str = "STRICT_INVERSE", scaled: bool = False):
+    """-LML of SKI with STRICT / PSEUDO inverse (gp_oracle.ski_nlml) and its gradient w.r.t. the
+    hyperparameters and the noise (the inducing points x[linspace] and the weights are constants)."""
+    from . import gp_oracle as o
+    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
+    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
+    X = np.asarray(x, dtype=np.float64)
+    Y = torch.as_tensor(np.asarray(y, dtype=np.float64)).reshape(-1, 1)
+    n = X.shape[0]
+    idx = o.ski_inducing_indices(n, m)
+    Zt = torch.as_tensor(X[idx])
+    W = torch.as_tensor(o.ski_weight_matrix(X, X[idx]))
+    kmm = kernel_matrix_t(tree, params, Zt, Zt, scaled)
+    A = (W @ kmm) @ W.T + nz * torch.eye(n, dtype=F64)
+    alpha = (pinv_or_inv(A) if handling == "PSEUDO_INVERSE" else torch.linalg.inv(A)) @ Y
+    fit = (Y.T @ alpha)[0, 0]
+    logdet = torch.linalg.slogdet(A)[1]
+    nl = -(-0.5 * fit - 0.5 * logdet - 0.5 * n * LOG_2PI)
+    grads = torch.autograd.grad(nl, params + [nz])
+    return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1])
+
+
+def inverse_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, handling: str,
+                          scaled: bool = False):
+    """-LML with STRICT_INVERSE (inv(K) y) / PSEUDO_INVERSE (pinv(K) y) and slogdet (M/Metrics.py:132-136,
+    :146-147) and its reverse-mode gradient -- for any nonsingular K + noise I, positive definite or not."""
+    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
+    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
+    X = torch.as_tensor(np.asarray(x, dtype=np.float64))
+    Y = torch.as_tensor(np.asarray(y, dtype=np.float64)).reshape(-1, 1)
+    n = X.shape[0]
+    K = kernel_matrix_t(tree, params, X, X, scaled) + nz * torch.eye(n, dtype=F64)
+    alpha = (pinv_or_inv(K) if handling == "PSEUDO_INVERSE" else torch.linalg.inv(K)) @ Y
+    nl = -(-0.5 * (Y.T @ alpha)[0, 0] - 0.5 * torch.linalg.slogdet(K)[1] - 0.5 * n * LOG_2PI)
+    grads = torch.autograd.grad(nl, params + [nz])
+    return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1])
+
+
+def batch_nlml_and_grad(tree, hyp: List, noise: float, xb: np.ndarray, yb: np.ndarray,
+                        handling: str = "CHOLESKY_BASED", agg: str = "mean", scaled: bool = False):
+    """BatchDataInput -LML (quirk Q7) and its gradient: CHOLESKY_BASED -agg_b(-1/2 fit_b - 1/2 sum_b' logdet_b'
+    - c) (M/LogLikelihood.py:39-63 with M/Metrics.py:153-154's axis-free reduce_sum); STRICT / PSEUDO
+    inverse: -agg over the [B, 1, B] broadcast of fit_b and slogdet_b' (gp_oracle.batch_nlml's sibling)."""
+    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
+    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
+    B, n = xb.shape[0], xb.shape[1]
+    fits, logdets = [], []
+    for b in range(B):
+        X = torch.as_tensor(np.asarray(xb[b], dtype=np.float64))
+        Y = torch.as_tensor(np.asarray(yb[b], dtype=np.float64)).reshape(-1, 1)
+        K = kernel_matrix_t(tree, params, X, X, scaled) + nz * torch.eye(n, dtype=F64)
+        L = torch.linalg.cholesky(K)
+        fits.append((Y.T @ torch.cholesky_solve(Y, L))[0, 0])
+        logdets.append(2.0 * torch.sum(torch.log(torch.diagonal(L))))
+    fit, logdet = torch.stack(fits), torch.stack(logdets)
+    c = 0.5 * n * LOG_2PI
+    red = torch.mean if agg == "mean" else torch.sum
+    if handling == "CHOLESKY_BASED":
+        ll = -0.5 * fit - 0.5 * torch.sum(logdet) - c
+    else:
+        ll = (-0.5 * fit).reshape(B, 1, 1) + (-0.5 * logdet).reshape(1, 1, B) - c
+    nl = -red(ll)
+    grads = torch.autograd.grad(nl, params + [nz])
+    return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1])

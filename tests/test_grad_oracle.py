@@ -44,3 +44,76 @@ def test_autodiff_oracle_matches_value_and_finite_differences(case):
     for g, e in zip(grads, fd):
         np.testing.assert_allclose(g, e, rtol=1e-5, atol=1e-6)
     assert abs(gnoise - fdn) < 1e-5 * max(1.0, abs(fdn))
+
+
+# Nystroem / SKC / SKI gradient oracle (SURVEY §8f.1 x §8f.4): value == gp_oracle's, gradients == central
+# differences on well-conditioned K_mm (short length scales: FD through a near-singular pinv is noise)
+NYS_CASES = [
+    ("CHOLESKY_BASED", False, ("SE", {}), [0.03], False),
+    ("CHOLESKY_BASED", True, ("SE", {}), [0.03, 1.3], True),
+    ("STRICT_INVERSE", False, ("MAT52", {}), [0.05], False),
+    ("PSEUDO_INVERSE", True, ("ADD", [("SE", {}), ("PER", {})]), [0.03, 0.5, 1.7], False),
+]
+
+
+@pytest.mark.parametrize("case", range(len(NYS_CASES)))
+def test_nystroem_gradient_oracle_matches_finite_differences(case):
+    handling, lower, tree, hyp, scaled = NYS_CASES[case]
+    x, y = o.make_inputs("C1", n=120, seed=3)
+    z = np.sort(np.random.default_rng(case).uniform(0, 1, (12, 1)), axis=0)
+    noise, jitter = 0.05, 1e-3
+    f = lambda h, nz, zz=z: o.nystroem_nlml(tree, h, nz, x, y, zz, handling, lower, jitter, scaled)
+    nl, g, gn, gz = ad.nystroem_nlml_and_grad(tree, hyp, noise, x, y, z, handling, lower, jitter, scaled)
+    assert abs(nl - f(hyp, noise)) < 1e-9 * abs(nl)
+    fd, fdn = ad.finite_difference(f, hyp, noise, h=1e-6)
+    for a, e in zip(g, fd):
+        np.testing.assert_allclose(a, e, rtol=2e-5, atol=1e-5)
+    assert abs(gn - fdn) < 2e-5 * max(1.0, abs(fdn))
+    for j in (0, 5, 11):
+        zp, zm = z.copy(), z.copy()
+        zp[j, 0] += 1e-6
+        zm[j, 0] -= 1e-6
+        e = (f(hyp, noise, zp) - f(hyp, noise, zm)) / 2e-6
+        assert abs(gz[j, 0] - e) < 2e-4 * max(1.0, abs(e)), (j, gz[j, 0], e)
+
+
+def test_ski_gradient_oracle_matches_finite_differences():
+    x, y = o.make_inputs("C1", n=100, seed=4)
+    tree, hyp, noise = ("SE", {}), [0.08], 0.05
+    f = lambda h, nz: o.ski_nlml(tree, h, nz, x, y, 20, "STRICT_INVERSE")
+    nl, g, gn = ad.ski_nlml_and_grad(tree, hyp, noise, x, y, 20, "STRICT_INVERSE")
+    assert abs(nl - f(hyp, noise)) < 1e-9 * abs(nl)
+    fd, fdn = ad.finite_difference(f, hyp, noise, h=1e-6)
+    np.testing.assert_allclose(g[0], fd[0], rtol=2e-5)
+    assert abs(gn - fdn) < 2e-5 * max(1.0, abs(fdn))
+
+
+@pytest.mark.parametrize("handling,agg", [("CHOLESKY_BASED", "mean"), ("CHOLESKY_BASED", "sum"),
+                                          ("STRICT_INVERSE", "mean"), ("PSEUDO_INVERSE", "sum")])
+def test_batch_gradient_oracle_matches_value_and_finite_differences(handling, agg):
+    rng = np.random.default_rng(1)
+    xb = rng.uniform(0, 1, (3, 40, 1))
+    yb = np.sin(5 * xb.sum(-1)) + 0.1 * rng.standard_normal((3, 40))
+    tree, hyp = ("ADD", [("SE", {}), ("PER", {})]), [0.2, 0.8, 0.6]
+    nl, g, gn = ad.batch_nlml_and_grad(tree, hyp, 0.05, xb, yb, handling, agg)
+    if handling == "CHOLESKY_BASED" and agg == "mean":
+        assert abs(nl - o.batch_nlml(tree, hyp, 0.05, xb, yb)) < 1e-10 * abs(nl)
+    f = lambda h, nz: ad.batch_nlml_and_grad(tree, h, nz, xb, yb, handling, agg)[0]
+    fd, fdn = ad.finite_difference(f, hyp, 0.05, h=1e-6)
+    for a, e in zip(g, fd):
+        np.testing.assert_allclose(a, e, rtol=1e-5, atol=1e-5)
+    assert abs(gn - fdn) < 1e-5 * max(1.0, abs(fdn))
+
+
+@pytest.mark.parametrize("handling", ["STRICT_INVERSE", "PSEUDO_INVERSE"])
+def test_indefinite_gradient_oracle_matches_finite_differences(handling):
+    x, y = _inputs(60, 1, 5)
+    nl, g, gn = ad.inverse_nlml_and_grad(("SE", {}), [0.1], -0.3, x, y, handling)
+    K = o.k_noised(("SE", {}), [0.1], -0.3, x)
+    assert np.min(np.linalg.eigvalsh(K)) < 0
+    ref = o.nlml_with_alpha(np.linalg.inv(K) @ y, y, np.linalg.slogdet(K)[1], 60)
+    assert abs(nl - ref) < 1e-9 * abs(ref)
+    f = lambda h, nz: ad.inverse_nlml_and_grad(("SE", {}), h, nz, x, y, handling)[0]
+    fd, fdn = ad.finite_difference(f, [0.1], -0.3, h=1e-6)
+    np.testing.assert_allclose(g[0], fd[0], rtol=1e-5)
+    assert abs(gn - fdn) < 1e-5 * max(1.0, abs(fdn))
