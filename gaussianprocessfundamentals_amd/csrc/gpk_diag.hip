@@ -25,10 +25,28 @@ namespace {
 
 constexpr int DB = 16;            // tile edge
 constexpr int NTL = NB / DB;      // tiles per block edge (8)
-constexpr int LDA = NB + 2;       // LDS row stride (doubles): 16 rows of one column on distinct banks
+#ifndef GPK_DIAG_SWIZZLE
+#define GPK_DIAG_SWIZZLE 0
+#endif
+// LDS row stride (doubles).  Default: 130, so the 16 rows of one column that the MFMA operand reads take
+// (lanes along rows) sit on distinct banks; the accumulator-layout accesses (lanes along 16 columns x 2
+// consecutive rows) are then 2-way conflicted.  GPK_DIAG_SWIZZLE=1: rows of 128 with the columns XOR-swizzled
+// per row, c ^ (16 (r & 1) + 2 ((r >> 1) & 7)), conflict-free for both patterns (SQ_LDS_BANK_CONFLICT per LDS
+// instruction 2.12 -> 0.75) but slower: the fused diagonal launch at N = 4096 took 44.8 instead of 40.2 us
+// (the swizzled addresses split the block load's 16-B LDS stores and add VALU work on the potf2 path).
+constexpr int LDA = GPK_DIAG_SWIZZLE ? NB : NB + 2;
 constexpr int DT = 512;           // threads (8 waves)
 constexpr int LDS_A = NB * LDA;
-constexpr int LDS_DINV = NTL * DB * DB;
+
+__device__ __forceinline__ int aidx(int r, int c) {
+  return GPK_DIAG_SWIZZLE ? r * LDA + (c ^ (((r & 1) << 4) | (((r >> 1) & 7) << 1))) : r * LDA + c;
+}
+#ifndef GPK_DINV_LD
+#define GPK_DINV_LD 18  // row stride of the inverted pivot tiles: lane (r, k) reads of a tile row hit distinct
+#endif              // banks (stride 16: the 16 rows sat on two banks, an 8-way conflict per read)
+constexpr int DBS = GPK_DINV_LD;   // Dinv tile row stride (doubles)
+constexpr int DTS = DB * DBS;      // Dinv tile stride
+constexpr int LDS_DINV = NTL * DTS;
 constexpr int LDS_COL = 2 * DB;  // potf2 column broadcast, double-buffered
 constexpr size_t DIAG_LDS_BYTES = sizeof(double) * (LDS_A + LDS_DINV + LDS_COL) + 16;
 
@@ -67,7 +85,7 @@ __device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf
   double w[DB];
 #pragma unroll
   for (int c = 0; c < DB; c += 2) {
-    const dbl2 t = *reinterpret_cast<const dbl2*>(A + (c0 + r) * LDA + c0 + c);
+    const dbl2 t = *reinterpret_cast<const dbl2*>(A + aidx(c0 + r, c0 + c));
     w[c] = inv ? ((c == r) ? 1.0 : 0.0) : t.x;
     w[c + 1] = inv ? ((c + 1 == r) ? 1.0 : 0.0) : t.y;
   }
@@ -101,10 +119,10 @@ __device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf
   if (bad != 0 && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + bad);
   if (lane < DB) {
 #pragma unroll
-    for (int c = 0; c < DB; ++c) A[(c0 + r) * LDA + c0 + c] = (c <= r) ? w[c] : 0.0;
+    for (int c = 0; c < DB; ++c) A[aidx(c0 + r, c0 + c)] = (c <= r) ? w[c] : 0.0;
   } else if (lane < 2 * DB) {
 #pragma unroll
-    for (int rr = 0; rr < DB; ++rr) Dk[rr * DB + r] = w[rr];  // Dinv[rr][r]
+    for (int rr = 0; rr < DB; ++rr) Dk[rr * DBS + r] = w[rr];  // Dinv[rr][r]
   }
 }
 
@@ -142,7 +160,7 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
 #pragma unroll
       for (int q = 0; q < LB; ++q) {
         const int r = (tid >> 7) + (g + q) * (DT / NB);
-        A[r * LDA + c] = (c <= r) ? v[q] : 0.0;
+        A[aidx(r, c)] = (c <= r) ? v[q] : 0.0;
       }
     }
   }
@@ -151,7 +169,7 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
 
 #pragma unroll 1
   for (int kb = 0; kb < NTL; ++kb) {
-    double* Dk = Dinv + kb * DB * DB;
+    double* Dk = Dinv + kb * DTS;
     if (wave == 0 && !(a.dbg & 2)) potf2_tile(A, Dk, colbuf, kb, lane, flag, a.j0);
     if (a.dbg & 4) continue;
     __syncthreads();
@@ -163,12 +181,12 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
         d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const double av = A[(i * DB + lr) * LDA + kb * DB + 4 * s + lk];
-          const double bv = Dk[lr * DB + 4 * s + lk];
+          const double av = A[aidx(i * DB + lr, kb * DB + 4 * s + lk)];
+          const double bv = Dk[lr * DBS + 4 * s + lk];
           acc = mfma64(av, bv, acc);
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + kb * DB + lr] = acc[q];
+        for (int q = 0; q < 4; ++q) A[aidx(i * DB + lk + 4 * q, kb * DB + lr)] = acc[q];
       }
     }
     __syncthreads();
@@ -183,15 +201,15 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
         const int i = kb + 1 + ti, j = kb + 1 + tj;
         d4 acc;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = A[(i * DB + lk + 4 * q) * LDA + j * DB + lr];
+        for (int q = 0; q < 4; ++q) acc[q] = A[aidx(i * DB + lk + 4 * q, j * DB + lr)];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const double av = -A[(i * DB + lr) * LDA + kb * DB + 4 * s + lk];
-          const double bv = A[(j * DB + lr) * LDA + kb * DB + 4 * s + lk];
+          const double av = -A[aidx(i * DB + lr, kb * DB + 4 * s + lk)];
+          const double bv = A[aidx(j * DB + lr, kb * DB + 4 * s + lk)];
           acc = mfma64(av, bv, acc);
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + j * DB + lr] = acc[q];
+        for (int q = 0; q < 4; ++q) A[aidx(i * DB + lk + 4 * q, j * DB + lr)] = acc[q];
       }
     }
     __syncthreads();
@@ -200,7 +218,7 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
   // L_kk back to W (lower triangle only)
   for (int e = tid; e < NB * NB; e += DT) {
     const int r = e >> 7, c = e & (NB - 1);
-    if (c <= r) Wb[(int64_t)r * a.ld + c] = (T)A[r * LDA + c];
+    if (c <= r) Wb[(int64_t)r * a.ld + c] = (T)A[aidx(r, c)];
   }
   if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
 
@@ -214,30 +232,30 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
       for (int K = J; K < I; ++K) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const double av = A[(I * DB + lr) * LDA + K * DB + 4 * s + lk];
-          const double bv = A[(K * DB + 4 * s + lk) * LDA + J * DB + lr];
+          const double av = A[aidx(I * DB + lr, K * DB + 4 * s + lk)];
+          const double bv = A[aidx(K * DB + 4 * s + lk, J * DB + lr)];
           tacc = mfma64(av, bv, tacc);
         }
       }
-      const double* Di = Dinv + I * DB * DB;
+      const double* Di = Dinv + I * DTS;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) out = mfma64(-Di[lr * DB + 4 * s + lk], tacc[s], out);
+      for (int s = 0; s < 4; ++s) out = mfma64(-Di[lr * DBS + 4 * s + lk], tacc[s], out);
     }
     __syncthreads();
     if (active) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) A[(I * DB + lk + 4 * q) * LDA + J * DB + lr] = out[q];
+      for (int q = 0; q < 4; ++q) A[aidx(I * DB + lk + 4 * q, J * DB + lr)] = out[q];
     }
     if (wave == NTL - 1) {
-      const double* Di = Dinv + I * DB * DB;
-      for (int e = lane; e < DB * DB; e += 64) A[(I * DB + e / DB) * LDA + I * DB + e % DB] = Di[e];
+      const double* Di = Dinv + I * DTS;
+      for (int e = lane; e < DB * DB; e += 64) A[aidx(I * DB + e / DB, I * DB + e % DB)] = Di[(e / DB) * DBS + e % DB];
     }
     __syncthreads();
   }
   T* Ib = reinterpret_cast<T*>(a.Winv) + (int64_t)b * a.inv_bs + a.kblk * NB * NB;
   for (int e = tid; e < NB * NB; e += DT) {
     const int r = e >> 7, c = e & (NB - 1);
-    Ib[e] = (T)((c <= r) ? A[r * LDA + c] : 0.0);
+    Ib[e] = (T)((c <= r) ? A[aidx(r, c)] : 0.0);
   }
 }
 
@@ -271,12 +289,12 @@ __device__ __forceinline__ void store_l_rows(const double* A, T* Wb, int64_t ld,
     if (c0 + EPC - 1 <= r) {
       vT v;
 #pragma unroll
-      for (int u = 0; u < EPC; ++u) v[u] = (T)A[r * LDA + c0 + u];
+      for (int u = 0; u < EPC; ++u) v[u] = (T)A[aidx(r, c0 + u)];
       *reinterpret_cast<vT*>(Wb + (int64_t)r * ld + c0) = v;
     } else {
 #pragma unroll
       for (int u = 0; u < EPC; ++u)
-        if (c0 + u <= r) Wb[(int64_t)r * ld + c0 + u] = (T)A[r * LDA + c0 + u];
+        if (c0 + u <= r) Wb[(int64_t)r * ld + c0 + u] = (T)A[aidx(r, c0 + u)];
     }
   }
 }
@@ -302,7 +320,8 @@ __device__ __forceinline__ void store_inv_zeros(T* Ib, int t, int nt) {
 template <typename T>
 __device__ __forceinline__ void store_inv_diag(const double* Dinv, T* Ib, int I, int t, int nt) {
   // diagonal tile I of L^-1 (Dinv_I, zeros above its diagonal)
-  for (int e = t; e < DB * DB; e += nt) Ib[(I * DB + e / DB) * NB + I * DB + e % DB] = (T)Dinv[I * DB * DB + e];
+  for (int e = t; e < DB * DB; e += nt)
+    Ib[(I * DB + e / DB) * NB + I * DB + e % DB] = (T)Dinv[I * DTS + (e / DB) * DBS + e % DB];
 }
 
 // tile (I, J) of L^-1, J < I: -Dinv_I sum_{K=J}^{I-1} L_{I,K} Linv_{K,J}, stored transposed in tile (J, I)
@@ -312,21 +331,21 @@ __device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, T* I
   d4 tacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 4; ++s)  // K = J: the diagonal tile Dinv_J
-    tacc = mfma64(A[(I * DB + lr) * LDA + J * DB + 4 * s + lk], Dinv[J * DB * DB + (4 * s + lk) * DB + lr], tacc);
+    tacc = mfma64(A[aidx(I * DB + lr, J * DB + 4 * s + lk)], Dinv[J * DTS + (4 * s + lk) * DBS + lr], tacc);
   for (int K = J + 1; K < I; ++K) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
-      tacc = mfma64(A[(I * DB + lr) * LDA + K * DB + 4 * s + lk], A[(J * DB + lr) * LDA + K * DB + 4 * s + lk], tacc);
+      tacc = mfma64(A[aidx(I * DB + lr, K * DB + 4 * s + lk)], A[aidx(J * DB + lr, K * DB + 4 * s + lk)], tacc);
   }
-  const double* Di = Dinv + I * DB * DB;
+  const double* Di = Dinv + I * DTS;
   d4 out = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int s = 0; s < 4; ++s) out = mfma64(-Di[lr * DB + 4 * s + lk], tacc[s], out);
+  for (int s = 0; s < 4; ++s) out = mfma64(-Di[lr * DBS + 4 * s + lk], tacc[s], out);
   // out[q] = Linv_{I,J}[lk + 4q][lr]  ->  tile (J, I) [lr][lk + 4q] for the later rows, and straight
   // from the registers to HBM (16 lanes of a row store 128 contiguous bytes)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    A[(J * DB + lr) * LDA + I * DB + lk + 4 * q] = out[q];
+    A[aidx(J * DB + lr, I * DB + lk + 4 * q)] = out[q];
     if (st) Ib[(I * DB + lk + 4 * q) * NB + J * DB + lr] = (T)out[q];
   }
 }
@@ -384,7 +403,7 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
       const int r = r0 + q * RPP;
       if (pc * EPC <= (r | (DB - 1))) {
 #pragma unroll
-        for (int u = 0; u < EPC; ++u) A[r * LDA + pc * EPC + u] = (double)v[q][u];
+        for (int u = 0; u < EPC; ++u) A[aidx(r, pc * EPC + u)] = (double)v[q][u];
       }
     }
   }
@@ -425,9 +444,9 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
     if (wave == 0) {
       if (s > 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) A[(s * DB + lr) * LDA + (s - 1) * DB + lk + 4 * q] = xs[q];
+        for (int q = 0; q < 4; ++q) A[aidx(s * DB + lr, (s - 1) * DB + lk + 4 * q)] = xs[q];
       }
-      if (!(a.dbg & 2)) potf2_tile(A, Dinv + s * DB * DB, colbuf, s, lane, flag, a.j0);  // timing ablation
+      if (!(a.dbg & 2)) potf2_tile(A, Dinv + s * DTS, colbuf, s, lane, flag, a.j0);  // timing ablation
       if (decltype(last)::value) prefetch();
     } else if (s == 0) {
       if (!(a.dbg & 8) && wr) store_inv_zeros(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
@@ -446,13 +465,13 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
         const int i = s + 1 + ti, j = s + 1 + tj;
         d4 acc;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = A[(i * DB + lk + 4 * q) * LDA + j * DB + lr];
+        for (int q = 0; q < 4; ++q) acc[q] = A[aidx(i * DB + lk + 4 * q, j * DB + lr)];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          acc = mfma64(-A[(i * DB + lr) * LDA + (s - 1) * DB + 4 * k + lk],
-                       A[(j * DB + lr) * LDA + (s - 1) * DB + 4 * k + lk], acc);
+          acc = mfma64(-A[aidx(i * DB + lr, (s - 1) * DB + 4 * k + lk)],
+                       A[aidx(j * DB + lr, (s - 1) * DB + 4 * k + lk)], acc);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + j * DB + lr] = acc[q];
+        for (int q = 0; q < 4; ++q) A[aidx(i * DB + lk + 4 * q, j * DB + lr)] = acc[q];
       }
       if (!(a.dbg & 8) && wr) {
         store_l_rows(A, Wb, a.ld, I, tid - 64, DT - 64);
@@ -464,27 +483,27 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
     xs = d4{0.0, 0.0, 0.0, 0.0};  // (the old value is dead: nothing keeps it alive across potf2)
     if (s < NTL - 1 && wave < NTL - 1 - s && !(a.dbg & 4)) {
       const int i = s + 1 + wave;
-      const double* Dk = Dinv + s * DB * DB;
+      const double* Dk = Dinv + s * DTS;
       d4 xi = {0.0, 0.0, 0.0, 0.0}, x1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const double dv = Dk[lr * DB + 4 * k + lk];
-        xi = mfma64(dv, A[(i * DB + lr) * LDA + s * DB + 4 * k + lk], xi);
-        if (wave != 0) x1 = mfma64(dv, A[((s + 1) * DB + lr) * LDA + s * DB + 4 * k + lk], x1);
+        const double dv = Dk[lr * DBS + 4 * k + lk];
+        xi = mfma64(dv, A[aidx(i * DB + lr, s * DB + 4 * k + lk)], xi);
+        if (wave != 0) x1 = mfma64(dv, A[aidx((s + 1) * DB + lr, s * DB + 4 * k + lk)], x1);
       }
       if (wave == 0) x1 = xi;
       // xi[q] = X_i[lr][lk + 4q]: the A operand of k-step q; x1 likewise the B operand
       d4 acc;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = A[(i * DB + lk + 4 * q) * LDA + (s + 1) * DB + lr];
+      for (int q = 0; q < 4; ++q) acc[q] = A[aidx(i * DB + lk + 4 * q, (s + 1) * DB + lr)];
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc = mfma64(-xi[q], x1[q], acc);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) A[(i * DB + lk + 4 * q) * LDA + (s + 1) * DB + lr] = acc[q];
+      for (int q = 0; q < 4; ++q) A[aidx(i * DB + lk + 4 * q, (s + 1) * DB + lr)] = acc[q];
       xs = xi;  // wave 0: tile (s + 1, s) is read by every wave of this phase, stored in P_{s+1}
       if (wave != 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) A[(i * DB + lr) * LDA + s * DB + lk + 4 * q] = xi[q];
+        for (int q = 0; q < 4; ++q) A[aidx(i * DB + lr, s * DB + lk + 4 * q)] = xi[q];
       }
     }
     __syncthreads();
@@ -523,7 +542,7 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const int x = 2 * lk + 8 * (st >> 1) + (st & 1);  // k within the chunk
-        const double bv = (kc < cb) ? A[(kc * DB + x) * LDA + cb * DB + lr] : Dinv[cb * DB * DB + lr * DB + x];
+        const double bv = (kc < cb) ? A[aidx(kc * DB + x, cb * DB + lr)] : Dinv[cb * DTS + lr * DBS + x];
         acc = mfma64(pa[kc][st >> 1][st & 1], bv, acc);
       }
     }

@@ -78,7 +78,7 @@ def test_get_gradients_is_the_device_gradient():
     rng = np.random.default_rng(9)
     x = rng.uniform(0, 1, (200, 2))
     y = np.sin(4 * x.sum(1))
-    tree, hyp = ("ADD", [("SE", {}), ("MAT32", {})]), [0.3, 0.5]
+    tree, hyp = ("ADD", [("SE", {}), ("MAT32", {"standard": True})]), [0.3, 0.5]
     met = get_metric_by_type(MetricType.LL, build_gp(tree, x, y))
     g = met.get_gradients(hyp_list(hyp), torch.tensor(0.02, dtype=F64))
     _, gref, _ = ad.nlml_and_grad(tree, hyp, 0.02, x, y)

@@ -2,7 +2,7 @@
 candidate, float() of the result (a host synchronisation) after each call -- the pattern of the
 reference's fitters (gpbasics/Optimizer/Fitter.py:91-167) -- and get_metric_and_gradient likewise.
 
-usage: python tools/bench_api_latency.py [n ...]
+usage: python tools/bench_api_latency.py [--no-grad] [n ...]
 Prints one JSON line per N with the per-call milliseconds (median of 20 calls, distinct lengthscales).
 """
 import json
@@ -25,7 +25,7 @@ from gaussianprocessfundamentals_amd.Metrics.Metrics import MetricType  # noqa: 
 from gaussianprocessfundamentals_amd.Statistics.GaussianProcess import GaussianProcess  # noqa: E402
 
 
-def run(n):
+def run(n, grad=True):
     rng = np.random.default_rng(1)
     x = np.sort(rng.uniform(0.0, 1.0, n)).reshape(n, 1)
     y = np.sin(4.0 * np.pi * x[:, 0]) + 0.1 * rng.standard_normal(n)
@@ -43,7 +43,7 @@ def run(n):
         t1 = time.perf_counter()
         if i >= 3:
             times.append((t1 - t0) * 1e3)
-    for i, c in enumerate(cands):
+    for i, c in enumerate(cands if grad else []):
         t0 = time.perf_counter()
         nl, grads, gn = m.get_metric_and_gradient([torch.tensor(c, dtype=torch.float64)], noise)
         float(nl), float(grads[0]), float(gn)
@@ -51,9 +51,10 @@ def run(n):
         if i >= 3:
             gtimes.append((t1 - t0) * 1e3)
     return {"n": n, "get_metric_ms": round(statistics.median(times), 3),
-            "get_metric_and_gradient_ms": round(statistics.median(gtimes), 3), "last_nlml": v}
+            "get_metric_and_gradient_ms": round(statistics.median(gtimes), 3) if gtimes else None, "last_nlml": v}
 
 
 if __name__ == "__main__":
-    for n in [int(a) for a in sys.argv[1:]] or [4096, 8192]:
-        print(json.dumps(run(n)), flush=True)
+    grad = "--no-grad" not in sys.argv
+    for n in [int(a) for a in sys.argv[1:] if not a.startswith("--")] or [4096, 8192]:
+        print(json.dumps(run(n, grad)), flush=True)
