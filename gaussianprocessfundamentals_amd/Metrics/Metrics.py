@@ -183,7 +183,7 @@ class Metric(AbstractMetric):
 
     # largest n for the eigendecomposition fallback of a matrix that is not positive definite (the
     # Jacobi sweeps cost O(n^3) each with n - 1 launches per sweep)
-    EIGEN_FALLBACK_MAX_N = 2048
+    EIGEN_FALLBACK_MAX_N = 8192
 
     def _positive_definite(self, hyper_parameter: List, noise, indices=None) -> bool:
         f = (self._approx_factorization(hyper_parameter, noise, indices) if self._approximate()
@@ -200,7 +200,7 @@ class Metric(AbstractMetric):
             if n > self.EIGEN_FALLBACK_MAX_N:
                 raise NotImplementedError("the covariance matrix is not positive definite and n = %d exceeds the "
                                           "eigendecomposition fallback (n <= %d)" % (n, self.EIGEN_FALLBACK_MAX_N))
-            lam, V, _ = engine.syevj(K.contiguous())
+            lam, V, _ = engine.eigh(K.contiguous())
             self._eig, self._eig_src = (lam, V), K
         return self._eig
 

@@ -54,7 +54,7 @@ class NystroemAdjoint:
         if self._nys is None:
             knm = engine.kernel_matrix(self.kernel, self.hyp, self.X, self.Z)
             kmm = engine.kernel_matrix(self.kernel, self.hyp, self.Z, self.Z)
-            lam, V, _ = engine.syevj(kmm)
+            lam, V, _ = engine.eigh(kmm)
             U0, _, mu0 = engine.pinv_factor(lam, V, 0, return_mu=True)
             P = engine.dgemm(U0, V, trans_b=True)
             self._nys = (knm, lam, V, mu0, P)

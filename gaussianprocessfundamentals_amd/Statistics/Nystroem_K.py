@@ -105,7 +105,7 @@ class NystroemMatrix:
                 raise ValueError("%d inducing inputs given, n_inducting_train is %d (the reference's "
                                  "noise * eye(m) would not conform)" % (kmm.shape[0], m))
             nv = _noise_value(noise)
-            lam, V, _ = engine.syevj(kmm)
+            lam, V, _ = engine.eigh(kmm)
             U, rank = engine.pinv_factor(lam, V, 1)
             if int(rank.cpu()[0]) < 0:
                 raise NotImplementedError("K_mm has a negative eigenvalue above the pinv cutoff")

@@ -32,7 +32,8 @@ EXPORTS = (
     "gpk_finalize_ragged", "gpk_nlml_ragged", "gpk_gemv",
     "gpk_assemble_dense", "gpk_dgemm", "gpk_syevj_workspace_bytes", "gpk_syevj", "gpk_pinv_factor",
     "gpk_ski_weights", "gpk_add_diagonal", "gpk_distance_matrix", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower",
-    "gpk_kernel_vjp_workspace_bytes", "gpk_kernel_vjp", "gpk_pinv_backward_scale",
+    "gpk_kernel_vjp_workspace_bytes", "gpk_kernel_vjp", "gpk_pinv_backward_scale", "gpk_syevd_workspace_bytes",
+    "gpk_syevd",
 )
 
 
@@ -113,6 +114,8 @@ def _declare(lib):
                                      P, P, P]),
         "gpk_potrf_lower": (c_int, [c_int, P, c_int64, c_int64, P, c_size_t, P, P, P]),
         "gpk_pinv_backward_scale": (c_int, [c_int64, c_int32, P, P, P, P]),
+        "gpk_syevd_workspace_bytes": (c_size_t, [c_int64]),
+        "gpk_syevd": (c_int, [c_int64, c_int32, P, c_int64, c_int64, P, P, P, c_size_t, P]),
         "gpk_kernel_vjp_workspace_bytes": (c_size_t, [POINTER(GpkKdesc), c_int64, c_int64, c_int32, c_int32]),
         "gpk_kernel_vjp": (c_int, [POINTER(GpkKdesc), P, P, c_int64, P, c_int64, c_int32, P, c_int64, P, P, P, P,
                                    P, c_size_t, P]),

@@ -1114,6 +1114,116 @@ int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
   return 0;
 }
 
+// ------------------------------------------------------------------- tridiagonal eigensolver (gpk_eig.hip)
+namespace {
+constexpr int kEigNb = 32;  // reflectors per compact-WY block of the back-transformation
+#define GPK_SYEVD_MAX_M 4096   // dc_deflate_kernel sorts a merged block in LDS (4096 keys + indices + z)
+
+struct EigWs {  // carving of the gpk_syevd workspace
+  double *W, *Qg, *U, *d, *e, *tau, *Y, *T1, *T2, *Gs, *S;
+  DcLevel L;
+  size_t bytes;
+};
+
+EigWs eig_carve(int64_t m, void* base) {
+  EigWs ws;
+  memset(&ws, 0, sizeof(ws));
+  char* p = static_cast<char*>(base);
+  size_t off = 0;
+  auto take = [&](size_t n) -> double* {
+    double* r = reinterpret_cast<double*>(p ? p + off : nullptr);
+    off += (n * sizeof(double) + 255) & ~(size_t)255;
+    return r;
+  };
+  auto itake = [&](size_t n) -> int32_t* { return reinterpret_cast<int32_t*>(take((n + 1) / 2)); };
+  const size_t mm = (size_t)m * (size_t)m, hp = (size_t)m / 2 + 1;
+  ws.W = take(mm);
+  ws.Qg = take(mm);
+  ws.U = take(mm);
+  ws.d = take(m);
+  ws.e = take(m);
+  ws.tau = take(m);
+  ws.Y = take((size_t)m * kEigNb);
+  ws.T1 = take((size_t)m * kEigNb);
+  ws.T2 = take((size_t)m * kEigNb);
+  ws.Gs = take((size_t)kEigNb * kEigNb);
+  ws.S = take((size_t)kEigNb * kEigNb);
+  DcLevel& L = ws.L;
+  L.dK = take(m);
+  L.zK = take(m);
+  L.rc = take(m);
+  L.rs = take(m);
+  L.root_t = take(m);
+  L.zhat = take(m);
+  L.rho = take(hp);
+  L.idx = itake(m);
+  L.ord = itake(m);
+  L.rp = itake(m);
+  L.rn = itake(m);
+  L.root_o = itake(m);
+  L.kcnt = itake(hp);
+  L.rcnt = itake(hp);
+  L.flip = itake(hp);
+  ws.bytes = off;
+  return ws;
+}
+
+// C <- alpha op(A) op(B) + beta C (row-major, contiguous leading dimensions)
+hipError_t eig_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, double alpha, const double* A, int64_t lda,
+                    const double* B, int64_t ldb, double beta, double* C, int64_t ldc, hipStream_t s) {
+  DgemmArgs g{ta, tb, M, N, K, A, lda, 0, B, ldb, 0, C, ldc, 0, alpha, beta};
+  return launch_dgemm(g, 1, s);
+}
+}  // namespace
+
+size_t gpk_syevd_workspace_bytes(int64_t m) {
+  if (m <= 0) return 8;
+  return eig_carve(m, nullptr).bytes;
+}
+
+int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
+              void* work, size_t work_bytes, void* stream) {
+  if (m < 0 || m > GPK_SYEVD_MAX_M) return fail_arg(1, "m (gpk_syevd: m <= 4096)");
+  if (batch < 0) return fail_arg(2, "batch");
+  if (m == 0 || batch == 0) return 0;
+  if (!A) return fail_arg(3, "A");
+  if (lda < m) return fail_arg(4, "lda");
+  if (!V) return fail_arg(6, "V");
+  if (!lam) return fail_arg(7, "lam");
+  if (!work || work_bytes < gpk_syevd_workspace_bytes(m)) return fail_arg(8, "work (gpk_syevd_workspace_bytes)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  EigWs ws = eig_carve(m, work);
+  const int mi = (int)m;
+  const int64_t mm = m * m;
+  for (int32_t b = 0; b < batch; ++b) {
+    double* Vb = V + (int64_t)b * mm;
+    double* lb = lam + (int64_t)b * m;
+    GPK_HIP(launch_sym_copy(A + (int64_t)b * a_bstride, lda, mi, ws.W, s), "syevd copy");
+    if (m == 1) {
+      GPK_HIP(hipMemcpyAsync(lb, ws.W, sizeof(double), hipMemcpyDeviceToDevice, s), "syevd m=1");
+      GPK_HIP(launch_eig_identity(Vb, 1, s), "syevd m=1");
+      continue;
+    }
+    GPK_HIP(launch_eig_tridiag(ws.W, mi, ws.d, ws.e, ws.tau, s), "syevd tridiag");
+    // eigenvectors of T into V, eigenvalues into lam
+    DcLevel L = ws.L;
+    L.lam = lb;
+    GPK_HIP(launch_eig_dc(ws.d, ws.e, mi, L, Vb, ws.Qg, ws.U, s), "syevd divide and conquer");
+    // V <- Q V, Q = H_0 ... H_{m-2}: blocks of reflectors from the last to the first, V <- V - Y (S (Y^T V))
+    const int nref = mi - 1;
+    for (int k0 = ((nref - 1) / kEigNb) * kEigNb; k0 >= 0; k0 -= kEigNb) {
+      const int nb = std::min(kEigNb, nref - k0);
+      GPK_HIP(launch_eig_build_y(ws.W, mi, k0, nb, ws.Y, s), "syevd Y");
+      GPK_HIP(eig_gemm(1, 0, nb, nb, m, 1.0, ws.Y, nb, ws.Y, nb, 0.0, ws.Gs, nb, s), "syevd Y^T Y");
+      GPK_HIP(launch_eig_larft(ws.Gs, ws.tau, k0, nb, ws.S, s), "syevd larft");
+      GPK_HIP(eig_gemm(1, 0, nb, m, m, 1.0, ws.Y, nb, Vb, m, 0.0, ws.T1, m, s), "syevd Y^T V");
+      GPK_HIP(eig_gemm(0, 0, nb, m, nb, 1.0, ws.S, nb, ws.T1, m, 0.0, ws.T2, m, s), "syevd S (Y^T V)");
+      GPK_HIP(eig_gemm(0, 0, m, m, nb, -1.0, ws.Y, nb, ws.T2, m, 1.0, Vb, m, s), "syevd V update");
+    }
+  }
+  return 0;
+}
+
 int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam, double rcond, int32_t mode,
                     double* mu, double* U, int32_t* rank_dev, void* stream) {
   if (m <= 0) return fail_arg(1, "m");

@@ -567,6 +567,40 @@ def syevj(A: torch.Tensor, max_sweeps: int = 60):
     return lam, V, int(sweeps.value)
 
 
+def syevd(A: torch.Tensor):
+    """Eigendecomposition of a symmetric [m, m] (or [B, m, m]) device matrix by the tridiagonal route
+    (gpk_syevd: Householder tridiagonalisation, compact-WY Q, implicit QL): returns (lam, V with the
+    eigenvectors in its columns), eigenvalues in no particular order.  m > 4096 or a QL iteration that does
+    not converge go to the Jacobi solver (gpk_syevj)."""
+    A3, lda, abs_ = _mat_args(A, "A")
+    batch, m = A3.shape[0], A3.shape[1]
+    if A3.shape[2] != m:
+        raise ValueError("A must be square")
+    if m > 4096:
+        lam, V, _ = syevj(A)
+        return lam, V
+    L = nat.lib()
+    V = torch.empty((batch, m, m), dtype=torch.float64, device=A.device)
+    lam = torch.empty((batch, m), dtype=torch.float64, device=A.device)
+    wb = int(L.gpk_syevd_workspace_bytes(m))
+    work = torch.empty(max(1, (wb + 7) // 8), dtype=torch.float64, device=A.device)
+    rc = L.gpk_syevd(m, batch, nat.ptr(A3), lda, abs_, nat.ptr(V), nat.ptr(lam), nat.ptr(work), wb,
+                     nat.stream_handle(A.device))
+    if rc > 1000:
+        lam, V, _ = syevj(A)
+        return lam, V
+    nat.check(rc, "gpk_syevd")
+    if A.dim() == 2:
+        return lam[0], V[0]
+    return lam, V
+
+
+def eigh(A: torch.Tensor):
+    """The product's symmetric eigensolver: syevd (tridiagonal route); returns (lam, V, 0) like syevj."""
+    lam, V = syevd(A)
+    return lam, V, 0
+
+
 def pinv_factor(lam: torch.Tensor, V: torch.Tensor, mode: int, rcond: float = -1.0, return_mu: bool = False):
     """U = V diag(mu) with tf.linalg.pinv's cutoff (gpk_pinv_factor): mode 0 mu = 1/lam (pinv = U V^T),
     mode 1 mu = lam^-1/2 (pinv = U U^T).  Returns (U, rank [B] int32 device tensor) (+ mu)."""
@@ -588,7 +622,7 @@ def pinv_factor(lam: torch.Tensor, V: torch.Tensor, mode: int, rcond: float = -1
 def pinv_sym(A: torch.Tensor, rcond: float = -1.0) -> torch.Tensor:
     """tf.linalg.pinv of a symmetric matrix (gpbasics/Statistics/Nystroem_K.py:53): Jacobi
     eigendecomposition, the reference's cutoff 10 m eps max|lam|, then V diag(1/lam) V^T on MFMA."""
-    lam, V, _ = syevj(A)
+    lam, V, _ = eigh(A)
     U, _ = pinv_factor(lam, V, 0, rcond)
     return dgemm(U, V, trans_b=True)
 

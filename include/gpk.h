@@ -281,6 +281,16 @@ size_t gpk_syevj_workspace_bytes(int64_t m, int32_t batch);
 int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
               void* work, size_t work_bytes, int32_t max_sweeps, int32_t* sweeps_out, void* stream);
 
+/* Symmetric eigendecomposition, tridiagonal route (the default of the metrics): Householder
+ * tridiagonalisation, divide and conquer on the tridiagonal matrix (deflation, Gu-Eisenstat eigenvectors,
+ * MFMA GEMM merges), compact-WY back-transformation on the f64 MFMA GEMM.  Same outputs as gpk_syevj
+ * (V [m, m] row-major, eigenvectors in its columns; lam in no particular order); A's lower triangle is read.
+ * m <= 4096.  Asynchronous on the stream.
+ * work: gpk_syevd_workspace_bytes(m) (reused across the batch). */
+size_t gpk_syevd_workspace_bytes(int64_t m);
+int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
+              void* work, size_t work_bytes, void* stream);
+
 /* U = V diag(mu) with mu_i = 1 / lam_i (mode 0; pinv = U V^T) or 1 / sqrt(lam_i) (mode 1;
  * pinv = U U^T) for |lam_i| > rcond max|lam| and 0 otherwise -- tf.linalg.pinv's cutoff (rcond < 0:
  * its default 10 m eps).  rank_dev[b] = kept eigenvalues, -1 if mode 1 keeps a negative one. */

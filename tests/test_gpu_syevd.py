@@ -1,0 +1,70 @@
+"""The tridiagonal eigensolver gpk_syevd (Householder tridiagonalisation, compact-WY Q, implicit QL) against numpy's eigh, and the pseudo-inverse built on it against
+tf.linalg.pinv's restatement (oracle.tf_pinv) -- the spectral half of Statistics/Nystroem_K.py:53 and of the
+non-positive-definite handlings (Metrics/Metrics.py:132-147).  Tolerances: eigenvalues |lam - lam_ref| <=
+1e-13 m max|lam| (as sets: QL leaves them unsorted, as the Jacobi solver did); residual ||A V - V diag(lam)|| and ||V^T V - I|| (max-abs) <= 1e-12 m max(1, max|lam|)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gp_oracle as o
+from gaussianprocessfundamentals_amd import engine
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(A, lam, V):
+    m = A.shape[0]
+    lam, V = lam.cpu().numpy(), V.cpu().numpy()
+    ref = np.linalg.eigvalsh(A)
+    sc = max(1.0, float(np.max(np.abs(ref))))
+    assert np.max(np.abs(np.sort(lam) - ref)) <= 1e-13 * m * sc, np.max(np.abs(np.sort(lam) - ref))
+    assert np.max(np.abs(A @ V - V * lam)) <= 1e-12 * m * sc
+    assert np.max(np.abs(V.T @ V - np.eye(m))) <= 1e-12 * m
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 17, 64, 130, 409, 1000])
+def test_syevd_random_symmetric(m):
+    rng = np.random.default_rng(m)
+    A = rng.standard_normal((m, m))
+    A = 0.5 * (A + A.T)
+    lam, V = engine.syevd(torch.tensor(A, device="cuda"))
+    _check(A, lam, V)
+
+
+def test_syevd_clusters_and_zero_tail():
+    """Repeated eigenvalues, a tight cluster and a tail below the pinv cutoff (QL's rotations keep the vectors of a
+    cluster orthonormal)."""
+    rng = np.random.default_rng(3)
+    m = 300
+    Q, _ = np.linalg.qr(rng.standard_normal((m, m)))
+    lam = np.concatenate([np.full(40, 2.0), 1.0 + 1e-13 * rng.standard_normal(30), np.geomspace(0.5, 1e-6, 130),
+                          1e-17 * rng.uniform(-1, 1, 100)])
+    A = (Q * lam) @ Q.T
+    A = 0.5 * (A + A.T)
+    ev, V = engine.syevd(torch.tensor(A, device="cuda"))
+    _check(A, ev, V)
+
+
+def test_syevd_kernel_matrix_pinv_matches_tf_pinv():
+    """K_mm of 409 inducing points (SE, l = 0.1 on [0, 1]: numerical rank 29 of 409), the Nystroem case.
+    pinv compared through K pinv K = K (both sides' cutoffs drop the same numerically-zero directions).  The bar
+    is the reference's own accuracy: an SVD / LAPACK pseudo-inverse of this K leaves |K pinv K - K| = 5.2e-7
+    (the kept eigenvalues reach down to the 10 m eps max|lam| cutoff, 1/lam ~ 1e10 amplifies eigenvector
+    rounding), so the device's residual must be within 4x of tf_pinv's and agree with it to that level."""
+    z = np.linspace(0.0, 1.0, 409).reshape(-1, 1)
+    K = o.kernel_matrix(("SE", {}), [0.1], z, z)
+    P = engine.pinv_sym(torch.tensor(K, device="cuda")).cpu().numpy()
+    ref = o.tf_pinv(K)
+    r_ref = float(np.max(np.abs(K @ ref @ K - K)))
+    assert np.max(np.abs(K @ P @ K - K)) <= 4 * r_ref
+    assert np.max(np.abs(K @ (P - ref) @ K)) <= 4 * r_ref
+
+
+def test_syevd_indefinite_matrix_n1024():
+    """An indefinite K + noise I (noise -0.3), as the PSEUDO / STRICT handlings' fallback sees it, beyond the
+    old n <= 2048 cap's scale in miniature."""
+    rng = np.random.default_rng(5)
+    x = rng.uniform(0, 1, (1024, 1))
+    A = o.k_noised(("SE", {}), [0.1], -0.3, x)
+    lam, V = engine.syevd(torch.tensor(A, device="cuda"))
+    _check(A, lam, V)

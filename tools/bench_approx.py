@@ -3,7 +3,7 @@
 usage: python tools/bench_approx.py [n] [reps]
 Prints one JSON line: per-metric device ms (median of reps after one warm-up; every metric is built
 fresh per repetition so no cache carries over), the building blocks' rates (gpk_dgemm TF/s on an
-n x n x m product, gpk_syevj ms and sweeps on K_mm) and the numpy/SciPy oracle's ms for the same
+n x n x m product, gpk_syevj ms and sweeps and gpk_syevd ms on K_mm) and the numpy/SciPy oracle's ms for the same
 metric (one evaluation, 16 threads)."""
 import json
 import sys
@@ -94,6 +94,12 @@ def main():
     _, _, sweeps = engine.syevj(kmm)
     torch.cuda.synchronize()
     out["syevj_m"] = {"ms": round((time.perf_counter() - t0) * 1e3, 2), "sweeps": sweeps}
+    engine.syevd(kmm)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    engine.syevd(kmm)
+    torch.cuda.synchronize()
+    out["syevd_m"] = {"ms": round((time.perf_counter() - t0) * 1e3, 2)}
     # oracle (host)
     for name, fn in (("exact_cholesky", lambda: o.nlml(SE, [l], noise, x, y)),
                      ("nystroem_cholesky", lambda: o.nystroem_nlml(SE, [l], noise, x, y, z)),
