@@ -181,9 +181,9 @@ class Metric(AbstractMetric):
             return engine.gemv(f.k_inv(0).contiguous(), self._y(y))
         return engine.gemv(self.covariance_matrix.get_K_inv(hyper_parameter, noise).contiguous(), self._y(y))
 
-    # largest n for the eigendecomposition fallback of a matrix that is not positive definite (the
-    # Jacobi sweeps cost O(n^3) each with n - 1 launches per sweep)
-    EIGEN_FALLBACK_MAX_N = 8192
+    # largest n for the eigendecomposition fallback of a matrix that is not positive definite (gpk_syevd's
+    # cap: its divide-and-conquer merges sort a merged block in LDS)
+    EIGEN_FALLBACK_MAX_N = 4096
 
     def _positive_definite(self, hyper_parameter: List, noise, indices=None) -> bool:
         f = (self._approx_factorization(hyper_parameter, noise, indices) if self._approximate()
@@ -191,7 +191,7 @@ class Metric(AbstractMetric):
         return int(f.info.abs().max()) == 0
 
     def _eigen(self, hyper_parameter: List, noise, indices=None):
-        """Eigendecomposition (gpk_syevj) of the covariance matrix the handling works on, for the
+        """Eigendecomposition (gpk_syevd) of the covariance matrix the handling works on, for the
         handlings' non-positive-definite cases; cached with that matrix."""
         from .. import engine
         K = self.get_covariance_matrix(hyper_parameter, noise, indices)

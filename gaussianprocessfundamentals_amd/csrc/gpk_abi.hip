@@ -159,6 +159,8 @@ struct Tune {
   int64_t asm_generic;    // K build: interior tiles through the generic loop too (A/B; bitwise equal)
   int64_t panel_stream;   // look-ahead panel chain: 0 high-priority side stream, 1 caller's stream,
                           // 2 normal-priority side stream
+  int64_t trd_split_m;    // gpk_syevd: above this m the tridiagonalisation's A22 v runs over the chip (three
+                          // launches per column) instead of inside one workgroup per panel
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -176,7 +178,7 @@ Tune& tune() {
                          env_i64("GPK_DIAG_VERSION", 2), env_i64("GPK_INGROUP", 0),
                          env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1),
                          env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0),
-                         env_i64("GPK_PANEL_STREAM", 0)};
+                         env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024)};
   return t;
 }
 
@@ -1120,7 +1122,7 @@ constexpr int kEigNb = 32;  // reflectors per compact-WY block of the back-trans
 #define GPK_SYEVD_MAX_M 4096   // dc_deflate_kernel sorts a merged block in LDS (4096 keys + indices + z)
 
 struct EigWs {  // carving of the gpk_syevd workspace
-  double *W, *Qg, *U, *d, *e, *tau, *Y, *T1, *T2, *Gs, *S;
+  double *W, *Qg, *U, *d, *e, *tau, *Y, *T1, *T2, *Gs, *S, *PV, *vg, *yg, *Sall;
   DcLevel L;
   size_t bytes;
 };
@@ -1148,6 +1150,10 @@ EigWs eig_carve(int64_t m, void* base) {
   ws.T2 = take((size_t)m * kEigNb);
   ws.Gs = take((size_t)kEigNb * kEigNb);
   ws.S = take((size_t)kEigNb * kEigNb);
+  ws.PV = take((size_t)3 * m * kEigNb);
+  ws.Sall = take((size_t)(m / kEigNb + 1) * kEigNb * kEigNb);
+  ws.vg = take(m);
+  ws.yg = take(m);
   DcLevel& L = ws.L;
   L.dK = take(m);
   L.zK = take(m);
@@ -1193,6 +1199,7 @@ int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
   if (!work || work_bytes < gpk_syevd_workspace_bytes(m)) return fail_arg(8, "work (gpk_syevd_workspace_bytes)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   EigWs ws = eig_carve(m, work);
+  const Tune tn = tune();
   const int mi = (int)m;
   const int64_t mm = m * m;
   for (int32_t b = 0; b < batch; ++b) {
@@ -1204,12 +1211,17 @@ int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
       GPK_HIP(launch_eig_identity(Vb, 1, s), "syevd m=1");
       continue;
     }
-    GPK_HIP(launch_eig_tridiag(ws.W, mi, ws.d, ws.e, ws.tau, s), "syevd tridiag");
+    GPK_HIP(launch_eig_tridiag(ws.W, mi, ws.d, ws.e, ws.tau, ws.PV, ws.vg, ws.yg, (int)tn.trd_split_m, s),
+            "syevd tridiag");
     // eigenvectors of T into V, eigenvalues into lam
     DcLevel L = ws.L;
     L.lam = lb;
     GPK_HIP(launch_eig_dc(ws.d, ws.e, mi, L, Vb, ws.Qg, ws.U, s), "syevd divide and conquer");
     // V <- Q V, Q = H_0 ... H_{m-2}: blocks of reflectors from the last to the first, V <- V - Y (S (Y^T V))
+    if (eig_bt_fused(mi)) {
+      GPK_HIP(launch_eig_backtransform(ws.W, ws.tau, mi, ws.Sall, Vb, s), "syevd back-transformation");
+      continue;
+    }
     const int nref = mi - 1;
     for (int k0 = ((nref - 1) / kEigNb) * kEigNb; k0 >= 0; k0 -= kEigNb) {
       const int nb = std::min(kEigNb, nref - k0);
@@ -1360,6 +1372,7 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "la_min_blocks")) slot = &t.la_min_blocks;
   else if (!strcmp(key, "fuse_trsm")) slot = &t.fuse_trsm;
   else if (!strcmp(key, "fuse_trsm_max")) slot = &t.fuse_trsm_max;
+  else if (!strcmp(key, "trd_split_m")) slot = &t.trd_split_m;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

@@ -2,9 +2,8 @@
 // paths of the metrics (tf.linalg.pinv of K_mm, gpbasics/Statistics/Nystroem_K.py:53; tf.linalg.slogdet / inv /
 // pinv of an indefinite K, gpbasics/Metrics/Metrics.py:132-147), tridiagonal route (gpk_syevd):
 //
-//   1. Householder tridiagonalisation A = Q T Q^T (tridiag_kernel, one 1024-thread workgroup: the trailing
-//      matrix is L2-resident for the Nystroem sizes; LAPACK dsytd2's reflectors, v_k stored below the
-//      subdiagonal of column k, tau_k apart)
+//   1. blocked Householder tridiagonalisation A = Q T Q^T (below; LAPACK dsytrd's reflectors, v_k stored below
+//      the subdiagonal of column k, tau_k apart), the rank-2nb trailing updates on the f64 MFMA GEMM
 //   2. back-transformation: the reflectors in blocks of 32, compact WY form I - Y S Y^T, applied to T's
 //      eigenvectors on the f64 MFMA GEMM (build_y_kernel, larft_kernel, launch_dgemm)
 //   3. divide and conquer on T (below): log2 m levels of rank-one merges whose eigenvector updates are MFMA
@@ -14,14 +13,15 @@
 // The two-sided Jacobi of gpk_approx.hip (gpk_syevj) stays available; this route replaces its O(m^3)-per-
 // sweep rounds (30 sweeps of m - 1 launches at m = 409) with O(m^3) work overall.
 #include <float.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include <math.h>
 
 #include "gpk_internal.h"
 
 namespace gpk {
 namespace {
-
-constexpr int TT = 1024;  // tridiag_kernel threads
 
 __device__ __forceinline__ double block_sum(double v, double* red) {
 #pragma unroll
@@ -36,69 +36,279 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return s;
 }
 
-// W [m, m] row-major, full symmetric on entry (working copy).  On exit d[0..m-1], e[0..m-2] hold T, tau[k]
-// the reflector scalars and W[(k + 1 + i) * m + k] (i >= 1) the reflector vectors v_k (v_k[0] = 1 implicit):
-// H_k = I - tau_k v_k v_k^T acts on rows / columns k + 1 .. m - 1, and Q = H_0 H_1 ... H_{m-2}.
-__global__ __launch_bounds__(TT) void tridiag_kernel(double* W, int m, double* d, double* e, double* tau) {
-  extern __shared__ __attribute__((aligned(16))) double sh[];
-  double* v = sh;
-  double* p = sh + m;
-  double* red = p + m;
-  const int tid = threadIdx.x;
-  for (int k = 0; k < m - 1; ++k) {
-    const int n1 = m - k - 1;
-    const int64_t base = (int64_t)(k + 1) * m + (k + 1);  // A22 = W[k + 1 .., k + 1 ..]
-    double s = 0.0;
-    for (int i = 1 + tid; i < n1; i += TT) {
-      const double t = W[(int64_t)(k + 1 + i) * m + k];
-      s += t * t;
-    }
-    s = block_sum(s, red);
-    const double alpha = W[(int64_t)(k + 1) * m + k];
-    double beta = alpha, tk = 0.0, scale = 0.0;
-    if (s > 0.0) {
-      beta = -copysign(sqrt(alpha * alpha + s), alpha);
-      tk = (beta - alpha) / beta;
-      scale = 1.0 / (alpha - beta);
-    }
-    for (int i = tid; i < n1; i += TT) v[i] = (i == 0) ? 1.0 : W[(int64_t)(k + 1 + i) * m + k] * scale;
-    if (tid == 0) {
-      d[k] = W[(int64_t)k * m + k];
-      e[k] = beta;
-      tau[k] = tk;
-    }
-    __syncthreads();
-    for (int i = 1 + tid; i < n1; i += TT) W[(int64_t)(k + 1 + i) * m + k] = v[i];
-    if (tk == 0.0) continue;  // H_k = I (wave-uniform)
-    // p = tau A22 v (A22 symmetric: column i read as row i, coalesced across threads)
-    for (int i = tid; i < n1; i += TT) {
-      double acc0 = 0.0, acc1 = 0.0;
-      int j = 0;
-      for (; j + 1 < n1; j += 2) {
-        acc0 = fma(W[base + (int64_t)j * m + i], v[j], acc0);
-        acc1 = fma(W[base + (int64_t)(j + 1) * m + i], v[j + 1], acc1);
-      }
-      if (j < n1) acc0 = fma(W[base + (int64_t)j * m + i], v[j], acc0);
-      p[i] = tk * (acc0 + acc1);
-    }
-    __syncthreads();
-    double pv = 0.0;
-    for (int i = tid; i < n1; i += TT) pv += p[i] * v[i];
-    pv = block_sum(pv, red);
-    const double a2 = -0.5 * tk * pv;
-    for (int i = tid; i < n1; i += TT) p[i] = fma(a2, v[i], p[i]);  // w
-    __syncthreads();
-    // A22 -= v w^T + w v^T
-    for (int i = tid; i < n1; i += TT) {
-      const double vi = v[i], wi = p[i];
-      for (int j = 0; j < n1; ++j) {
-        const int64_t o = base + (int64_t)j * m + i;
-        W[o] = W[o] - (v[j] * wi + p[j] * vi);
-      }
-    }
-    __syncthreads();
+__device__ __forceinline__ double block_max(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  const int nw = (blockDim.x + 63) >> 6;
+  for (int i = 0; i < nw; ++i) s = fmax(s, red[i]);
+  return s;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+  // butterfly: every lane ends with the same bits (each stage adds the same two values in either order)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Blocked Householder tridiagonalisation (LAPACK dsytrd / dlatrd, lower): panels of TRD_NB columns; inside a
+// panel each column is brought up to date with the panel's earlier reflectors (V, Wp), its reflector built and
+// y = A22 v formed against the trailing matrix as of the panel's start, corrected by V (Wp^T v) + Wp (V^T v);
+// after the panel one rank-2nb update A22 -= V Wp^T + Wp V^T on the f64 MFMA GEMM.  W [m, m] row-major, full
+// symmetric on entry; on exit d[0..m-1], e[0..m-2] hold T, tau[k] the reflector scalars and W[(k + 1 + i) m + k]
+// (i >= 1) the reflector vectors v_k (v_k[0] = 1 implicit): H_k = I - tau_k v_k v_k^T acts on rows / columns
+// k + 1 .. m - 1, and Q = H_0 H_1 ... H_{m-2}.  Vp / Wp: [m, TRD_NB] row-major panels (zero above row j + 1 in
+// column j).  Small m: one workgroup per panel (trd_panel_kernel); large m: three launches per column with the
+// product y = A22 v spread over the chip (trd_prep_kernel, trd_matvec_kernel, trd_finish_kernel).
+constexpr int TRD_NB = 32;
+
+struct TrdArgs {
+  double* W;
+  double* PV;  // [3 NB, m] row-major: rows t = V's column t, NB + t = Wp's column t, 2 NB + t = V's column t again
+               // (so that [V Wp] and [Wp V] are both contiguous row ranges: one K = 2 NB GEMM for the update)
+  double *d, *e, *tau;
+  double *vg, *yg;  // v / y in HBM for the split path
+  int m;
+  unsigned long long* prof;  // timing-only: per-phase cycle sums of trd_panel_kernel (nullptr normally)
+};
+
+// update column j (rows >= j) with the panel's q earlier reflectors, build its reflector: v (v[0] = 1, length
+// n1 = m - j - 1) into vs, PV's V rows q and 2 NB + q and W's column j; d[j], e[j], tau[j].  Returns tau_j.
+__device__ double trd_prep(const TrdArgs& A, int j, int q, double* vs, double* rowj, double* red) {
+  const int tid = threadIdx.x, T = blockDim.x, m = A.m, n1 = m - j - 1;
+  const double* V = A.PV;
+  const double* Wp = A.PV + (int64_t)TRD_NB * m;
+  for (int t = tid; t < q; t += T) {
+    rowj[t] = V[(int64_t)t * m + j];
+    rowj[TRD_NB + t] = Wp[(int64_t)t * m + j];
   }
-  if (tid == 0) d[m - 1] = W[(int64_t)(m - 1) * m + (m - 1)];
+  __syncthreads();
+  for (int r = j + tid; r < m; r += T) {
+    // q <= 31 dependent-free products: unrolled so that the loads of 8 columns are in flight together
+    double acc = A.W[(int64_t)r * m + j], a1 = 0.0;
+#pragma unroll 8
+    for (int t = 0; t < q; ++t) {
+      acc = fma(-V[(int64_t)t * m + r], rowj[TRD_NB + t], acc);
+      a1 = fma(-Wp[(int64_t)t * m + r], rowj[t], a1);
+    }
+    acc += a1;
+    if (r == j) A.d[j] = acc;
+    else vs[r - j - 1] = acc;
+  }
+  __syncthreads();
+  const double alpha = vs[0];
+  double ss = 0.0;
+  for (int i = 1 + tid; i < n1; i += T) ss += vs[i] * vs[i];
+  ss = block_sum(ss, red);
+  double beta = alpha, tk = 0.0, scale = 0.0;
+  if (ss > 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + ss), alpha);
+    tk = (beta - alpha) / beta;
+    scale = 1.0 / (alpha - beta);
+  }
+  for (int i = tid; i < n1; i += T) vs[i] = (i == 0) ? 1.0 : vs[i] * scale;
+  if (tid == 0) {
+    A.e[j] = beta;
+    A.tau[j] = tk;
+  }
+  __syncthreads();
+  double* Vq = A.PV + (int64_t)q * m;
+  double* V2q = A.PV + (int64_t)(2 * TRD_NB + q) * m;
+  for (int r = tid; r < m; r += T) {
+    const double v = r <= j ? 0.0 : vs[r - j - 1];
+    Vq[r] = v;
+    V2q[r] = v;
+    if (r >= j + 2) A.W[(int64_t)r * m + j] = v;
+  }
+  return tk;
+}
+
+// y[i] = sum_l W[j + 1 + i][j + 1 + l] v[l] for rows i in [i0, i1), one wave per row (two rows per pass)
+__device__ void trd_matvec(const TrdArgs& A, int j, const double* vs, double* ys, int i0, int i1, int wave, int nw) {
+  const int lane = threadIdx.x & 63, m = A.m, n1 = m - j - 1;
+  const double* base = A.W + (int64_t)(j + 1) * m + (j + 1);
+  int i = i0 + 2 * wave;
+  for (; i + 1 < i1; i += 2 * nw) {
+    const double* r0 = base + (int64_t)i * m;
+    const double* r1 = r0 + m;
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll 4
+    for (int l = lane; l < n1; l += 64) {
+      const double v = vs[l];
+      a0 = fma(r0[l], v, a0);
+      a1 = fma(r1[l], v, a1);
+    }
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    if (lane == 0) {
+      ys[i] = a0;
+      ys[i + 1] = a1;
+    }
+  }
+  if (i < i1) {
+    const double* r0 = base + (int64_t)i * m;
+    double a0 = 0.0;
+    for (int l = lane; l < n1; l += 64) a0 = fma(r0[l], vs[l], a0);
+    a0 = wave_sum(a0);
+    if (lane == 0) ys[i] = a0;
+  }
+}
+
+// In-workgroup form of the product (trd_panel_kernel, m <= 1024): A22 symmetric, so y_i = sum_l A22[l][i] v_l:
+// lanes over the outputs i (coalesced row reads, no cross-lane reduction), wave w over rows l = w, w + nw, ...,
+// R rows per pass so that R rows' loads are in flight together; per-wave partial sums in LDS, added in wave
+// order (deterministic).  C = 64-lane column groups held in registers (n1 <= 64 C).
+template <int C, int R>
+__device__ void trd_matvec_cols(const TrdArgs& A, int j, const double* vs, double* ys, double* part) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6, T = blockDim.x;
+  const int m = A.m, n1 = m - j - 1;
+  const double* base = A.W + (int64_t)(j + 1) * m + (j + 1);
+  double acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 0.0;
+  int l = wave;
+  for (; l + (R - 1) * nw < n1; l += R * nw) {
+    double x[R][C];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const double* row = base + (int64_t)(l + u * nw) * m;
+#pragma unroll
+      for (int c = 0; c < C; ++c) x[u][c] = (lane + 64 * c < n1) ? row[lane + 64 * c] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const double vl = vs[l + u * nw];
+#pragma unroll
+      for (int c = 0; c < C; ++c) acc[c] = fma(x[u][c], vl, acc[c]);
+    }
+  }
+  for (; l < n1; l += nw) {
+    const double* row = base + (int64_t)l * m;
+    const double vl = vs[l];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (lane + 64 * c < n1) acc[c] = fma(row[lane + 64 * c], vl, acc[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+    if (lane + 64 * c < n1) part[wave * m + lane + 64 * c] = acc[c];
+  __syncthreads();
+  for (int i = tid; i < n1; i += T) {
+    double sum = 0.0;
+    for (int w = 0; w < nw; ++w) sum += part[w * m + i];
+    ys[i] = sum;
+  }
+}
+
+// y -= V (Wp^T v) + Wp (V^T v); w = tau y - tau / 2 (tau y^T v) v into PV's Wp row q
+__device__ void trd_finish(const TrdArgs& A, int j, int q, double tk, const double* vs, double* ys, double* dots,
+                           double* red) {
+  const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
+  const int m = A.m, n1 = m - j - 1;
+  const double* V = A.PV + (j + 1);
+  const double* Wp = A.PV + (int64_t)TRD_NB * m + (j + 1);
+  for (int t2 = wave; t2 < 2 * q; t2 += nw) {
+    const double* P = t2 < q ? Wp + (int64_t)t2 * m : V + (int64_t)(t2 - q) * m;
+    double acc = 0.0, acc1 = 0.0;
+    int i = lane;
+#pragma unroll 4
+    for (; i + 64 < n1; i += 128) {
+      acc = fma(P[i], vs[i], acc);
+      acc1 = fma(P[i + 64], vs[i + 64], acc1);
+    }
+    if (i < n1) acc = fma(P[i], vs[i], acc);
+    acc = wave_sum(acc + acc1);
+    if (lane == 0) dots[t2] = acc;
+  }
+  __syncthreads();
+  double wv = 0.0;
+  for (int i = tid; i < n1; i += T) {
+    double y = ys[i], y1 = 0.0;
+#pragma unroll 8
+    for (int t = 0; t < q; ++t) {
+      y = fma(-V[(int64_t)t * m + i], dots[t], y);
+      y1 = fma(-Wp[(int64_t)t * m + i], dots[q + t], y1);
+    }
+    y = (y + y1) * tk;
+    ys[i] = y;
+    wv = fma(y, vs[i], wv);
+  }
+  wv = block_sum(wv, red);
+  const double a2 = -0.5 * tk * wv;
+  double* Wq = A.PV + (int64_t)(TRD_NB + q) * m;
+  for (int r = tid; r < m; r += T) Wq[r] = r <= j ? 0.0 : fma(a2, vs[r - j - 1], ys[r - j - 1]);
+  __syncthreads();
+}
+
+// one panel (columns k0 .. k0 + nq - 1) in one workgroup (m <= TRD_PANEL_MAX_M);
+// LDS: v, y [m], rowj [2 NB], dots [2 NB], red [32], per-wave partial products [16 m]
+constexpr int TRD_PANEL_MAX_M = 1024;
+__global__ __launch_bounds__(1024) void trd_panel_kernel(TrdArgs A, int k0, int nq) {
+  extern __shared__ __attribute__((aligned(16))) double sh[];
+  double* vs = sh;
+  double* ys = vs + A.m;
+  double* rowj = ys + A.m;
+  double* dots = rowj + 2 * TRD_NB;
+  double* red = dots + 2 * TRD_NB;
+  double* part = red + 32;
+  unsigned long long t0 = A.prof ? clock64() : 0, c_prep = 0, c_mv = 0, c_fin = 0;
+  for (int q = 0; q < nq; ++q) {
+    const int j = k0 + q, n1 = A.m - j - 1;
+    const double tk = trd_prep(A, j, q, vs, rowj, red);
+    __syncthreads();
+    if (A.prof) {
+      const unsigned long long t = clock64();
+      c_prep += t - t0;
+      t0 = t;
+    }
+    if (n1 <= 256) trd_matvec_cols<4, 4>(A, j, vs, ys, part);
+    else if (n1 <= 512) trd_matvec_cols<8, 2>(A, j, vs, ys, part);
+    else trd_matvec_cols<16, 1>(A, j, vs, ys, part);
+    __syncthreads();
+    if (A.prof) {
+      const unsigned long long t = clock64();
+      c_mv += t - t0;
+      t0 = t;
+    }
+    trd_finish(A, j, q, tk, vs, ys, dots, red);
+    if (A.prof) {
+      const unsigned long long t = clock64();
+      c_fin += t - t0;
+      t0 = t;
+    }
+  }
+  if (A.prof && threadIdx.x == 0) {
+    A.prof[0] += c_prep;
+    A.prof[1] += c_mv;
+    A.prof[2] += c_fin;
+  }
+}
+
+__global__ __launch_bounds__(1024) void trd_prep_kernel(TrdArgs A, int j, int q) {
+  __shared__ double rowj[2 * TRD_NB];
+  __shared__ double red[32];
+  trd_prep(A, j, q, A.vg, rowj, red);
+}
+
+__global__ __launch_bounds__(256) void trd_matvec_kernel(TrdArgs A, int j) {
+  const int n1 = A.m - j - 1;
+  const int i0 = blockIdx.x * 8, i1 = min(i0 + 8, n1);  // 8 rows per workgroup of 4 waves
+  trd_matvec(A, j, A.vg, A.yg, i0, i1, threadIdx.x >> 6, 4);
+}
+
+__global__ __launch_bounds__(1024) void trd_finish_kernel(TrdArgs A, int j, int q) {
+  __shared__ double dots[2 * TRD_NB];
+  __shared__ double red[32];
+  trd_finish(A, j, q, A.tau[j], A.vg, A.yg, dots, red);
+}
+
+__global__ void trd_last_kernel(const double* W, int m, double* d) {
+  if (threadIdx.x == 0) d[m - 1] = W[(int64_t)(m - 1) * m + (m - 1)];
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -121,26 +331,6 @@ __global__ __launch_bounds__(256) void dc_init_kernel(const double* d, const dou
     lam[i] = d[i] - (i > 0 ? e[i - 1] : 0.0) - (i < m - 1 ? e[i] : 0.0);
   }
   if (t < (int64_t)m * m) Q[t] = (t / m == t % m) ? 1.0 : 0.0;
-}
-
-__device__ __forceinline__ double block_max(double v, double* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  double s = 0.0;
-  const int nw = (blockDim.x + 63) >> 6;
-  for (int i = 0; i < nw; ++i) s = fmax(s, red[i]);
-  return s;
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-  // butterfly: every lane ends with the same bits (each stage adds the same two values in either order)
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
 }
 
 // One workgroup per pair.  LDS: D[P2] z[k] idx[P2] kept[k] defl[k] red[32]
@@ -437,6 +627,118 @@ __global__ __launch_bounds__(64) void larft_kernel(const double* G, const double
     if (r < nb) S[r * nb + i] = Sl[r * 65 + i];
 }
 
+// Back-transformation for m <= BT_MAX_M in two launches (in place of build_y + 4 GEMMs + larft per block):
+// bt_larft_kernel computes every block's S (one workgroup per block of BT_NB reflectors: G = Y^T Y from W's
+// reflector columns staged through LDS, then dlarft's recurrence), bt_apply_kernel applies all blocks, last to
+// first, V <- V - Y (S (Y^T V)), to a slab of BT_CW columns of V held in LDS (one workgroup per slab).
+constexpr int BT_NB = 32, BT_CW = 8, BT_RC = 128, BT_MAX_M = 1024;
+
+// Y chunk: rows [i0, i0 + BT_RC) of the block's reflector columns k0 .. k0 + nb - 1 into Yc[BT_RC][BT_NB + 1]
+__device__ __forceinline__ void bt_stage_y(const double* W, int m, int k0, int nb, int i0, double* Yc) {
+  for (int e = threadIdx.x; e < BT_RC * BT_NB; e += blockDim.x) {
+    const int r = e / BT_NB, c = e % BT_NB, i = i0 + r, k = k0 + c;
+    double v = 0.0;
+    if (c < nb && i < m) v = (i == k + 1) ? 1.0 : (i > k + 1 ? W[(int64_t)i * m + k] : 0.0);
+    Yc[r * (BT_NB + 1) + c] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void bt_larft_kernel(const double* W, const double* tau, int m, double* Sall) {
+  __shared__ double Yc[BT_RC * (BT_NB + 1)];
+  __shared__ double G[BT_NB * (BT_NB + 1)];
+  __shared__ double Sl[BT_NB * (BT_NB + 1)];
+  const int kb = blockIdx.x, k0 = kb * BT_NB, nref = m - 1, nb = min(BT_NB, nref - k0), tid = threadIdx.x;
+  const int gr = tid / BT_NB, gc = tid % BT_NB;  // 8 x 32 threads: G rows gr, gr + 8, gr + 16, gr + 24
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i0 = k0 + 1; i0 < m; i0 += BT_RC) {
+    __syncthreads();
+    bt_stage_y(W, m, k0, nb, i0, Yc);
+    __syncthreads();
+    const int rows = min(BT_RC, m - i0);
+    for (int r = 0; r < rows; ++r) {
+      const double yc = Yc[r * (BT_NB + 1) + gc];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = fma(Yc[r * (BT_NB + 1) + gr + 8 * u], yc, acc[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) G[(gr + 8 * u) * (BT_NB + 1) + gc] = acc[u];
+  __syncthreads();
+  if (tid < BT_NB) {  // S_ii = tau_i, S[0:i, i] = -tau_i S[0:i, 0:i] G[0:i, i]: lane r reads only its own row
+    const int r = tid;
+    for (int i = 0; i < nb; ++i) {
+      const double ti = tau[k0 + i];
+      if (r < i) {
+        double s = 0.0;
+        for (int c = r; c < i; ++c) s += Sl[r * (BT_NB + 1) + c] * G[c * (BT_NB + 1) + i];
+        Sl[r * (BT_NB + 1) + i] = -ti * s;
+      } else {
+        Sl[r * (BT_NB + 1) + i] = (r == i) ? ti : 0.0;
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < BT_NB * BT_NB; e += 256) {
+    const int r = e / BT_NB, c = e % BT_NB;
+    Sall[(int64_t)kb * BT_NB * BT_NB + e] = (r < nb && c < nb) ? Sl[r * (BT_NB + 1) + c] : 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void bt_apply_kernel(const double* W, int m, const double* Sall, double* V) {
+  extern __shared__ __attribute__((aligned(16))) double sh[];
+  double* Vs = sh;                           // [m][BT_CW]
+  double* Yc = Vs + (size_t)m * BT_CW;       // [BT_RC][BT_NB + 1]
+  double* T1 = Yc + BT_RC * (BT_NB + 1);     // [BT_NB][BT_CW]
+  double* T2 = T1 + BT_NB * BT_CW;           // [BT_NB][BT_CW]
+  double* S = T2 + BT_NB * BT_CW;            // [BT_NB][BT_NB]
+  const int tid = threadIdx.x, c0 = blockIdx.x * BT_CW, ncol = min(BT_CW, m - c0);
+  for (int e = tid; e < m * BT_CW; e += 256) {
+    const int i = e / BT_CW, c = e % BT_CW;
+    Vs[e] = c < ncol ? V[(int64_t)i * m + c0 + c] : 0.0;
+  }
+  const int nref = m - 1, nblk = (nref + BT_NB - 1) / BT_NB;
+  const int tc = tid / BT_CW, tcol = tid % BT_CW;  // 32 x 8 threads: T entry (tc, tcol)
+  for (int kb = nblk - 1; kb >= 0; --kb) {
+    const int k0 = kb * BT_NB, nb = min(BT_NB, nref - k0);
+    __syncthreads();
+    for (int e = tid; e < BT_NB * BT_NB; e += 256) S[e] = Sall[(int64_t)kb * BT_NB * BT_NB + e];
+    // T1 = Y^T Vs
+    double acc = 0.0;
+    for (int i0 = k0 + 1; i0 < m; i0 += BT_RC) {
+      __syncthreads();
+      bt_stage_y(W, m, k0, nb, i0, Yc);
+      __syncthreads();
+      const int rows = min(BT_RC, m - i0);
+      for (int r = 0; r < rows; ++r) acc = fma(Yc[r * (BT_NB + 1) + tc], Vs[(i0 + r) * BT_CW + tcol], acc);
+    }
+    T1[tc * BT_CW + tcol] = acc;
+    __syncthreads();
+    // T2 = S T1
+    double t2 = 0.0;
+    for (int c = 0; c < BT_NB; ++c) t2 = fma(S[tc * BT_NB + c], T1[c * BT_CW + tcol], t2);
+    T2[tc * BT_CW + tcol] = t2;
+    // Vs -= Y T2 (rows > k0)
+    for (int i0 = k0 + 1; i0 < m; i0 += BT_RC) {
+      __syncthreads();
+      bt_stage_y(W, m, k0, nb, i0, Yc);
+      __syncthreads();
+      const int rows = min(BT_RC, m - i0);
+      for (int e = tid; e < rows * BT_CW; e += 256) {
+        const int r = e / BT_CW, col = e % BT_CW;
+        double u = 0.0;
+#pragma unroll 8
+        for (int c = 0; c < BT_NB; ++c) u = fma(Yc[r * (BT_NB + 1) + c], T2[c * BT_CW + col], u);
+        Vs[(i0 + r) * BT_CW + col] -= u;
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < m * BT_CW; e += 256) {
+    const int i = e / BT_CW, c = e % BT_CW;
+    if (c < ncol) V[(int64_t)i * m + c0 + c] = Vs[e];
+  }
+}
+
 __global__ __launch_bounds__(256) void sym_copy_kernel(const double* A, int64_t lda, int m, double* W) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)m * m) return;
@@ -447,18 +749,58 @@ __global__ __launch_bounds__(256) void sym_copy_kernel(const double* A, int64_t 
 
 }  // namespace
 
-size_t eig_tridiag_lds(int m) { return sizeof(double) * (2 * (size_t)m + 32); }
+static size_t trd_panel_lds(int m) { return sizeof(double) * (18 * (size_t)m + 4 * TRD_NB + 32); }
 
-hipError_t launch_eig_tridiag(double* W, int m, double* d, double* e, double* tau, hipStream_t s) {
-  const size_t lds = eig_tridiag_lds(m);
+hipError_t launch_eig_tridiag(double* W, int m, double* d, double* e, double* tau, double* PV, double* vg,
+                              double* yg, int split_m, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(tridiag_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(trd_panel_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)trd_panel_lds(TRD_PANEL_MAX_M));
     if (err != hipSuccess) return err;
     attr = true;
   }
-  hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(TT), lds, s, W, m, d, e, tau);
+  static unsigned long long* prof = nullptr;
+  if (getenv("GPK_TRD_PROF") && !prof) {
+    hipError_t err = hipMallocManaged(&prof, 4 * sizeof(unsigned long long));
+    if (err != hipSuccess) return err;
+    memset(prof, 0, 4 * sizeof(unsigned long long));
+    atexit([] {
+      hipDeviceSynchronize();
+      fprintf(stderr, "trd_panel cycles: prep %llu matvec %llu finish %llu\n", prof[0], prof[1], prof[2]);
+    });
+  }
+  TrdArgs A{W, PV, d, e, tau, vg, yg, m, prof};
+  const bool split = m > std::min(split_m, TRD_PANEL_MAX_M);
+  for (int k0 = 0; k0 < m - 1; k0 += TRD_NB) {
+    const int nq = std::min(TRD_NB, m - 1 - k0);
+    if (nq < TRD_NB) {  // a short last panel: the rows it does not write must not carry the previous panel's
+      hipError_t err = hipMemsetAsync(PV, 0, sizeof(double) * 3 * TRD_NB * (size_t)m, s);
+      if (err != hipSuccess) return err;
+    }
+    if (!split) {
+      hipLaunchKernelGGL(trd_panel_kernel, dim3(1), dim3(1024), trd_panel_lds(m), s, A, k0, nq);
+    } else {
+      for (int q = 0; q < nq; ++q) {
+        const int j = k0 + q, n1 = m - j - 1;
+        hipLaunchKernelGGL(trd_prep_kernel, dim3(1), dim3(1024), 0, s, A, j, q);
+        hipLaunchKernelGGL(trd_matvec_kernel, dim3((unsigned)((n1 + 7) / 8)), dim3(256), 0, s, A, j);
+        hipLaunchKernelGGL(trd_finish_kernel, dim3(1), dim3(1024), 0, s, A, j, q);
+      }
+    }
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    const int p0 = k0 + nq;
+    if (p0 < m) {  // A22 -= [V Wp] [Wp V]^T over the trailing square (both triangles kept), one K = 2 NB GEMM
+      const int64_t n2 = m - p0;
+      DgemmArgs g{1, 0, n2, n2, 2 * TRD_NB, PV + p0, m, 0, PV + (int64_t)TRD_NB * m + p0, m, 0,
+                  W + (int64_t)p0 * m + p0, m, 0, -1.0, 1.0};
+      err = launch_dgemm(g, 1, s);
+      if (err != hipSuccess) return err;
+    }
+  }
+  hipLaunchKernelGGL(trd_last_kernel, dim3(1), dim3(64), 0, s, W, m, d);
   return hipGetLastError();
 }
 
@@ -533,6 +875,27 @@ hipError_t launch_eig_build_y(const double* W, int m, int k0, int nb, double* Y,
 
 hipError_t launch_eig_larft(const double* G, const double* tau, int k0, int nb, double* S, hipStream_t s) {
   hipLaunchKernelGGL(larft_kernel, dim3(1), dim3(64), 0, s, G, tau, k0, nb, S);
+  return hipGetLastError();
+}
+
+bool eig_bt_fused(int m) { return m <= BT_MAX_M; }
+
+hipError_t launch_eig_backtransform(const double* W, const double* tau, int m, double* Sall, double* V,
+                                    hipStream_t s) {
+  static bool attr = false;
+  const size_t lds = sizeof(double) * ((size_t)BT_MAX_M * BT_CW + BT_RC * (BT_NB + 1) + 2 * BT_NB * BT_CW +
+                                       BT_NB * BT_NB);
+  if (!attr) {
+    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(bt_apply_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (err != hipSuccess) return err;
+    attr = true;
+  }
+  const int nblk = (m - 1 + BT_NB - 1) / BT_NB;
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(bt_larft_kernel, dim3(nblk), dim3(256), 0, s, W, tau, m, Sall);
+  const size_t need = sizeof(double) * ((size_t)m * BT_CW + BT_RC * (BT_NB + 1) + 2 * BT_NB * BT_CW + BT_NB * BT_NB);
+  hipLaunchKernelGGL(bt_apply_kernel, dim3((unsigned)((m + BT_CW - 1) / BT_CW)), dim3(256), need, s, W, m, Sall, V);
   return hipGetLastError();
 }
 

@@ -224,7 +224,8 @@ hipError_t launch_jacobi_out(const double* Af, const double* Vf, int m, double* 
 hipError_t launch_pinv_factor(const double* V, const double* lam, int m, double rcond, int mode, double* mu,
                               double* U, int32_t* rank, int32_t batch, hipStream_t s);
 // tridiagonal eigensolver (gpk_eig.hip)
-hipError_t launch_eig_tridiag(double* W, int m, double* d, double* e, double* tau, hipStream_t s);
+hipError_t launch_eig_tridiag(double* W, int m, double* d, double* e, double* tau, double* PV, double* vg,
+                              double* yg, int split_m, hipStream_t s);
 struct DcLevel {  // divide-and-conquer scratch, every array [m] (pair arrays [m / 2 + 1])
   double *lam, *dK, *zK, *rc, *rs, *root_t, *zhat, *rho;
   int32_t *idx, *ord, *rp, *rn, *root_o, *kcnt, *rcnt, *flip;
@@ -235,6 +236,9 @@ hipError_t launch_eig_transpose(const double* A, int m, double* B, hipStream_t s
 hipError_t launch_eig_identity(double* Z, int m, hipStream_t s);
 hipError_t launch_eig_build_y(const double* W, int m, int k0, int nb, double* Y, hipStream_t s);
 hipError_t launch_eig_larft(const double* G, const double* tau, int k0, int nb, double* S, hipStream_t s);
+bool eig_bt_fused(int m);
+hipError_t launch_eig_backtransform(const double* W, const double* tau, int m, double* Sall, double* V,
+                                    hipStream_t s);
 hipError_t launch_sym_copy(const double* A, int64_t lda, int m, double* W, hipStream_t s);
 hipError_t launch_pinv_bwd_scale(const double* lam, const double* mu, int m, double* T, int32_t batch, hipStream_t s);
 hipError_t launch_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int d, double* Wm,

@@ -102,7 +102,7 @@ def test_subset_of_data_grid_is_exact_on_the_grid_subset():
 @pytest.mark.parametrize("handling", [H.STRICT_INVERSE, H.PSEUDO_INVERSE])
 def test_handlings_of_an_indefinite_covariance(handling):
     """K + noise I with a negative noise is indefinite: the Cholesky reports it, and STRICT_INVERSE /
-    PSEUDO_INVERSE + slogdet fall back to the Jacobi eigendecomposition, as the reference's LU-based
+    PSEUDO_INVERSE + slogdet fall back to the eigendecomposition (gpk_syevd), as the reference's LU-based
     tf.linalg.inv / SVD-based pinv / slogdet handle it.  NLL rel <= 1e-8 (cond(K) ~ 1e3 here)."""
     g, x, y, _, _ = setup(n=300)
     noise = -0.3
@@ -112,6 +112,23 @@ def test_handlings_of_an_indefinite_covariance(handling):
     got = float(met.get_metric(hyp_list([0.1]), T(noise)).reshape(-1)[0])
     alpha = (np.linalg.inv(K) if handling is H.STRICT_INVERSE else o.tf_pinv(K)) @ y
     ref = o.nlml_with_alpha(alpha, y, np.linalg.slogdet(K)[1], 300)
+    assert rel(got, ref) <= 1e-8, (got, ref)
+
+
+@pytest.mark.parametrize("handling", [H.STRICT_INVERSE, H.PSEUDO_INVERSE])
+def test_handlings_of_an_indefinite_covariance_n4096(handling):
+    """The same at n = 4096 (the eigendecomposition fallback's cap, gpk_syevd): K - 0.3 I of 4096 SE inputs.
+    Reference alpha / log|det| from numpy's eigh (no eigenvalue near tf.linalg.pinv's cutoff here, so pinv =
+    inv); NLL rel <= 1e-8."""
+    g, x, y, _, _ = setup(n=4096)
+    noise = -0.3
+    K = o.k_noised(SE, [0.1], noise, x)
+    lam, V = np.linalg.eigh(K)
+    assert lam[0] < 0 and np.min(np.abs(lam)) > 1e-3
+    met = get_metric_by_type(MetricType.LL, g, numerical_matrix_handling=handling)
+    got = float(met.get_metric(hyp_list([0.1]), T(noise)).reshape(-1)[0])
+    alpha = V @ ((V.T @ y) / lam)
+    ref = o.nlml_with_alpha(alpha, y, float(np.sum(np.log(np.abs(lam)))), 4096)
     assert rel(got, ref) <= 1e-8, (got, ref)
 
 

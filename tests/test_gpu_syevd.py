@@ -68,3 +68,34 @@ def test_syevd_indefinite_matrix_n1024():
     A = o.k_noised(("SE", {}), [0.1], -0.3, x)
     lam, V = engine.syevd(torch.tensor(A, device="cuda"))
     _check(A, lam, V)
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_syevd_tridiagonalisation_paths_agree(split):
+    """The blocked tridiagonalisation in one workgroup per panel (m <= trd_split_m) and with A22 v spread over the
+    chip (three launches per column, the large-m path) -- both against numpy at m = 300 (10 panels, a short last
+    one)."""
+    import gaussianprocessfundamentals_amd._native as nat
+    rng = np.random.default_rng(11)
+    A = rng.standard_normal((300, 300))
+    A = 0.5 * (A + A.T)
+    old = nat.tune("trd_split_m", 64 if split else 1024)
+    try:
+        lam, V = engine.syevd(torch.tensor(A, device="cuda"))
+    finally:
+        nat.tune("trd_split_m", old)
+    _check(A, lam, V)
+
+
+def test_syevd_m4096_indefinite():
+    """n = 4096 (the syevd cap), the PSEUDO / STRICT fallback's size in VERDICT's terms: K - 0.3 I."""
+    rng = np.random.default_rng(6)
+    x = rng.uniform(0, 1, (4096, 1))
+    A = o.k_noised(("SE", {}), [0.1], -0.3, x)
+    lam, V = engine.syevd(torch.tensor(A, device="cuda"))
+    lam, V = lam.cpu().numpy(), V.cpu().numpy()
+    ref = np.linalg.eigvalsh(A)
+    sc = float(np.max(np.abs(ref)))
+    assert np.max(np.abs(np.sort(lam) - ref)) <= 1e-12 * sc
+    assert np.max(np.abs(A @ V - V * lam)) <= 1e-11 * sc
+    assert np.max(np.abs(V.T @ V - np.eye(4096))) <= 1e-11
