@@ -154,8 +154,11 @@ struct Stack {
 
 // Single-base-node trees (the common case, e.g. every SURVEY config but C5): the node's constants
 // are computed once per thread into registers and every division by a hyperparameter becomes a
-// multiplication by its reciprocal (|error| <= ~1e-14 relative in K; the generic postfix path keeps
-// the reference's literal operation order).
+// multiplication by its reciprocal (|error| <= ~1e-14 relative in K).  Multi-node trees go through
+// eval_tree_fast with the same reciprocals and periodic nodes through sin2_pi, so the K build no
+// longer keeps the reference's literal operation order anywhere.  The gradient kernel re-evaluates K
+// with base_values (divisions, library sin): for trees its K differs from the factorised one by
+// ~1e-14 relative, far inside the gradient tests' tolerances.
 struct FastNode {
   int op, flags, d, off;
   double il, il2, i3l2, iper, sg;

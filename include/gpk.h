@@ -369,7 +369,9 @@ int gpk_timing_reset(void);
  * band instead of launching them to exit at once), "group_eye" (panels per trailing update of the
  * identity-augmented factorisations, gpk_potrf_aug_ex / gpk_nlml_grad; "group" for the others),
  * "asm_generic" (1: the K build's interior tiles through the generic per-element loop as well; the
- * same bits, slower -- for A/B checks).
+ * same bits, slower -- for A/B checks), "trd_split_m" (gpk_syevd: above this m, at most 1024, the
+ * tridiagonalisation's A22 v runs over the chip, three launches per column, instead of one workgroup per
+ * panel; default 1024).
  * Stores the value and returns the previous one through *old (may be NULL); 0 or -1 (unknown
  * key).  Defaults come from the environment (GPK_LOOKAHEAD, GPK_RESERVE_CUS, ...). */
 int gpk_tune(const char* key, int64_t value, int64_t* old);
