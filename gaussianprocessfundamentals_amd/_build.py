@@ -15,7 +15,8 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB_NAME = "libgpk.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-SOURCES = ("gpk_assemble.hip", "gpk_diag.hip", "gpk_potrf.hip", "gpk_approx.hip", "gpk_eig.hip", "gpk_abi.hip")
+SOURCES = ("gpk_assemble.hip", "gpk_diag.hip", "gpk_potrf.hip", "gpk_approx.hip", "gpk_eig.hip", "gpk_flat.hip",
+           "gpk_abi.hip")
 ARCH = "gfx950"
 
 

@@ -31,7 +31,7 @@ EXPORTS = (
     "gpk_grad_workspace_bytes", "gpk_nlml_grad", "gpk_assemble_ragged", "gpk_potrf_aug_ragged",
     "gpk_finalize_ragged", "gpk_nlml_ragged", "gpk_gemv",
     "gpk_assemble_dense", "gpk_dgemm", "gpk_syevj_workspace_bytes", "gpk_syevj", "gpk_pinv_factor",
-    "gpk_ski_weights", "gpk_add_diagonal", "gpk_distance_matrix", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower",
+    "gpk_ski_weights", "gpk_add_diagonal", "gpk_distance_matrix", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower", "gpk_trsv_lower", "gpk_posterior",
     "gpk_kernel_vjp_workspace_bytes", "gpk_kernel_vjp", "gpk_pinv_backward_scale", "gpk_syevd_workspace_bytes",
     "gpk_syevd",
 )
@@ -113,6 +113,9 @@ def _declare(lib):
         "gpk_nlml_batched": (c_int, [POINTER(GpkKdesc), c_int32, P, P, c_int, P, P, c_int64, c_int32, P, c_size_t,
                                      P, P, P]),
         "gpk_potrf_lower": (c_int, [c_int, P, c_int64, c_int64, P, c_size_t, P, P, P]),
+        "gpk_trsv_lower": (c_int, [c_int, c_int, P, c_int64, c_int64, P, P, c_size_t, P]),
+        "gpk_posterior": (c_int, [P, P, c_int, P, c_int64, P, P, c_int64, P, c_int64, c_int32, c_int32, P, P,
+                                  c_int64, P, c_size_t, P]),
         "gpk_pinv_backward_scale": (c_int, [c_int64, c_int32, P, P, P, P]),
         "gpk_syevd_workspace_bytes": (c_size_t, [c_int64]),
         "gpk_syevd": (c_int, [c_int64, c_int32, P, c_int64, c_int64, P, P, P, c_size_t, P]),

@@ -801,9 +801,19 @@ size_t gpk_workspace_bytes(int op, int dtype, int64_t n, int64_t m, int32_t batc
     return align256(lay.w_bytes) + align256(lay.inv_bytes) + align256((size_t)batch * 4 * sizeof(double));
   }
   if (op == GPK_WS_POTRF) {
-    if (dtype != GPK_F64 || gpk_plan(GPK_F64, 1, n, 0, 1, &lay)) return 0;
+    if ((dtype != GPK_F64 && dtype != GPK_F32) || gpk_plan(dtype, 1, n, 0, 1, &lay)) return 0;
     return align256(lay.w_bytes) + align256(lay.inv_bytes) + align256(8 * sizeof(double)) +
            align256((size_t)n * sizeof(double));
+  }
+  const int64_t n_pad = (n + NB - 1) / NB * NB;
+  const size_t winv = align256((size_t)n_pad * NB * sizeof(double));
+  if (op == GPK_WS_TRSV) {
+    if (dtype != GPK_F64) return 0;
+    return winv + align256((size_t)n_pad * sizeof(double));
+  }
+  if (op == GPK_WS_POSTERIOR) {
+    if (dtype != GPK_F64 || m <= 0) return 0;
+    return winv + 2 * align256((size_t)n_pad * (size_t)m * sizeof(double)) + align256(8 * sizeof(double));
   }
   return 0;
 }
@@ -830,13 +840,34 @@ int gpk_nlml_batched(const gpk_kdesc* kd, int32_t batch, const double* hyp_dev, 
   return 0;
 }
 
+static int potrf_lower_f32(float* A, int64_t n, int64_t lda, void* work, size_t work_bytes, int32_t* info_dev,
+                           double* logdet_dev, void* stream) {
+  gpk_layout lay;
+  if (int e = gpk_plan(GPK_F32, 1, n, 0, 1, &lay)) return e;
+  if (!work || work_bytes < gpk_workspace_bytes(GPK_WS_POTRF, GPK_F32, n, 0, 1)) return fail_arg(6, "work_bytes");
+  char* w = reinterpret_cast<char*>(work);
+  void* W = w;
+  void* Winv = w + align256(lay.w_bytes);
+  double* out = reinterpret_cast<double*>(w + align256(lay.w_bytes) + align256(lay.inv_bytes));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(hipMemsetAsync(info_dev, 0, sizeof(int32_t), s), "memset info");
+  GPK_HIP(launch_pack_lower(GPK_F32, A, lda, n, lay.n_pad, lay.p, W, s), "potrf_lower pack");
+  if (int e = gpk_potrf_aug(&lay, W, Winv, info_dev, stream)) return e;
+  if (int e = gpk_finalize(&lay, W, info_dev, out, nullptr, nullptr, stream)) return e;
+  GPK_HIP(launch_unpack_lower(GPK_F32, W, lay.ld, n, A, lda, s), "potrf_lower unpack");
+  if (logdet_dev) GPK_HIP(hipMemcpyAsync(logdet_dev, out + 2, sizeof(double), hipMemcpyDeviceToDevice, s), "logdet");
+  return 0;
+}
+
 int gpk_potrf_lower(int dtype, void* A, int64_t n, int64_t lda, void* work, size_t work_bytes, int32_t* info_dev,
                     double* logdet_dev, void* stream) {
-  if (dtype != GPK_F64) return fail_arg(1, "dtype (gpk_potrf_lower factors fp64)");
+  if (dtype != GPK_F64 && dtype != GPK_F32) return fail_arg(1, "dtype");
   if (!A) return fail_arg(2, "A");
   if (n <= 0) return fail_arg(3, "n");
   if (lda < n) return fail_arg(4, "lda");
   if (!info_dev) return fail_arg(7, "info_dev");
+  if (dtype == GPK_F32)
+    return potrf_lower_f32(static_cast<float*>(A), n, lda, work, work_bytes, info_dev, logdet_dev, stream);
   gpk_layout lay;
   if (int e = gpk_plan(GPK_F64, 1, n, 0, 1, &lay)) return e;
   if (!work || work_bytes < gpk_workspace_bytes(GPK_WS_POTRF, GPK_F64, n, 0, 1)) return fail_arg(6, "work_bytes");
@@ -966,12 +997,110 @@ int gpk_trsv(const gpk_layout* lay, int trans, const void* W, const void* Winv, 
   t.x_bs = lay->n_pad;
   t.n_pad = lay->n_pad;
   t.trans = trans;
+  t.n_valid = lay->n_pad;
   for (int64_t i = 0; i < nblk; ++i) {
     t.kblk = (trans == 0) ? i : nblk - 1 - i;
     GPK_HIP(timed(5, 0.0, 0.0, s, [&] { return launch_trsv_diag(t, lay->dtype, lay->batch, s); }),
             "trsv_diag");
     GPK_HIP(timed(5, 0.0, 0.0, s, [&] { return launch_trsv_update(t, lay->dtype, lay->batch, s); }),
             "trsv_update");
+  }
+  return 0;
+}
+
+int gpk_trsv_lower(int dtype, int trans, const double* L, int64_t n, int64_t ldl, double* x, void* work,
+                   size_t work_bytes, void* stream) {
+  if (dtype != GPK_F64) return fail_arg(1, "dtype (gpk_trsv_lower solves fp64)");
+  if (trans != 0 && trans != 1) return fail_arg(2, "trans");
+  if (!L) return fail_arg(3, "L");
+  if (n <= 0) return fail_arg(4, "n");
+  if (ldl < n) return fail_arg(5, "ldl");
+  if (!x) return fail_arg(6, "x");
+  if (!work || work_bytes < gpk_workspace_bytes(GPK_WS_TRSV, GPK_F64, n, 0, 1))
+    return fail_arg(8, "work (gpk_workspace_bytes(GPK_WS_TRSV))");
+  const int64_t n_pad = (n + NB - 1) / NB * NB, nblk = n_pad / NB;
+  char* w = static_cast<char*>(work);
+  double* Winv = reinterpret_cast<double*>(w);
+  double* xp = reinterpret_cast<double*>(w + align256((size_t)n_pad * NB * sizeof(double)));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  GPK_HIP(launch_trtri_blocks(L, ldl, n, Winv, s), "trsv_lower diagonal blocks");
+  GPK_HIP(hipMemsetAsync(xp, 0, (size_t)n_pad * sizeof(double), s), "trsv_lower x");
+  GPK_HIP(hipMemcpyAsync(xp, x, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s), "trsv_lower x");
+  TrsvArgs t;
+  t.W = L;
+  t.ld = ldl;
+  t.w_bs = 0;
+  t.Winv = Winv;
+  t.inv_bs = 0;
+  t.x = xp;
+  t.x_bs = n_pad;
+  t.n_pad = n_pad;
+  t.trans = trans;
+  t.n_valid = n;
+  for (int64_t i = 0; i < nblk; ++i) {
+    t.kblk = (trans == 0) ? i : nblk - 1 - i;
+    GPK_HIP(timed(5, 0.0, 0.0, s, [&] { return launch_trsv_diag(t, GPK_F64, 1, s); }), "trsv_lower diag");
+    GPK_HIP(timed(5, 0.0, 0.0, s, [&] { return launch_trsv_update(t, GPK_F64, 1, s); }), "trsv_lower update");
+  }
+  GPK_HIP(hipMemcpyAsync(x, xp, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s), "trsv_lower x");
+  return 0;
+}
+
+int gpk_posterior(const gpk_kdesc* kd, const double* hyp_dev, int dtype, const double* L, int64_t ldl,
+                  const double* alpha, const double* X, int64_t n, const double* Xs, int64_t m, int32_t d,
+                  int32_t var_mode, double* mu, double* var, int64_t ldv, void* work, size_t work_bytes,
+                  void* stream) {
+  if (!valid_kdesc(kd, d)) return fail_arg(1, "kernel descriptor");
+  if (dtype != GPK_F64) return fail_arg(3, "dtype (gpk_posterior is fp64)");
+  if (!L) return fail_arg(4, "L");
+  if (ldl < n) return fail_arg(5, "ldl");
+  if (!alpha && mu) return fail_arg(6, "alpha");
+  if (!X) return fail_arg(7, "X");
+  if (n <= 0) return fail_arg(8, "n");
+  if (!Xs) return fail_arg(9, "Xs");
+  if (m <= 0) return fail_arg(10, "m");
+  if (var_mode != 0 && var_mode != 1) return fail_arg(12, "var_mode");
+  if (var && var_mode == 1 && ldv < m) return fail_arg(15, "ldv");
+  if (!work || work_bytes < gpk_workspace_bytes(GPK_WS_POSTERIOR, GPK_F64, n, m, 1))
+    return fail_arg(16, "work (gpk_workspace_bytes(GPK_WS_POSTERIOR))");
+  const int64_t n_pad = (n + NB - 1) / NB * NB, nblk = n_pad / NB;
+  char* w = static_cast<char*>(work);
+  double* Winv = reinterpret_cast<double*>(w);
+  w += align256((size_t)n_pad * NB * sizeof(double));
+  double* Ks = reinterpret_cast<double*>(w);
+  w += align256((size_t)n_pad * (size_t)m * sizeof(double));
+  double* V = reinterpret_cast<double*>(w);
+  w += align256((size_t)n_pad * (size_t)m * sizeof(double));
+  double* kdiag = reinterpret_cast<double*>(w);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // K_s = k(X, Xs) [n, m], zero padding rows
+  if (n_pad > n)
+    GPK_HIP(hipMemsetAsync(Ks + n * m, 0, (size_t)(n_pad - n) * (size_t)m * sizeof(double), s), "posterior pad");
+  if (int e = gpk_kernel_matrix(kd, hyp_dev, GPK_F64, 0, X, n, Xs, m, d, 0.0, Ks, m, stream)) return e;
+  if (mu) {  // mu = K_s^T alpha (S/Auxiliary.py:57-66)
+    DgemmArgs g{1, 0, m, 1, n, Ks, m, 0, alpha, 1, 0, mu, 1, 0, 1.0, 0.0};
+    GPK_HIP(launch_dgemm(g, 1, s), "posterior mu");
+  }
+  if (!var) return 0;
+  // V = L^-1 K_s, blocked: V_k = L_kk^-1 K_s,k; K_s,below -= L_below,k V_k
+  GPK_HIP(launch_trtri_blocks(L, ldl, n, Winv, s), "posterior diagonal blocks");
+  for (int64_t kb = 0; kb < nblk; ++kb) {
+    const int64_t j0 = kb * NB, nv = std::min<int64_t>(NB, n - j0);
+    DgemmArgs g1{0, 0, NB, m, NB, Winv + kb * NB * NB, NB, 0, Ks + j0 * m, m, 0, V + j0 * m, m, 0, 1.0, 0.0};
+    GPK_HIP(launch_dgemm(g1, 1, s), "posterior solve");
+    if (j0 + NB < n) {
+      DgemmArgs g2{0, 0, n - j0 - NB, m, nv, L + (j0 + NB) * ldl + j0, ldl, 0, V + j0 * m, m, 0,
+                   Ks + (j0 + NB) * m, m, 0, -1.0, 1.0};
+      GPK_HIP(launch_dgemm(g2, 1, s), "posterior update");
+    }
+  }
+  if (var_mode == 1) {  // Sigma = K_ss - V^T V (S/Auxiliary.py:68-93)
+    if (int e = gpk_kernel_matrix(kd, hyp_dev, GPK_F64, 0, Xs, m, Xs, m, d, 0.0, var, ldv, stream)) return e;
+    DgemmArgs g{1, 0, m, m, n, V, m, 0, V, m, 0, var, ldv, 0, -1.0, 1.0};
+    GPK_HIP(launch_dgemm(g, 1, s), "posterior covariance");
+  } else {  // diag: k(x*, x*) is the same for every x* (every kernel of the descriptor is stationary)
+    if (int e = gpk_kernel_matrix(kd, hyp_dev, GPK_F64, 0, Xs, 1, Xs, 1, d, 0.0, kdiag, 1, stream)) return e;
+    GPK_HIP(launch_posterior_var(V, n, m, kdiag, var, s), "posterior variance");
   }
   return 0;
 }

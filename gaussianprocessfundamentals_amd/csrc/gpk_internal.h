@@ -174,6 +174,7 @@ struct TrsvArgs {
   int64_t kblk;
   int64_t n_pad;
   int32_t trans;
+  int64_t n_valid;  // rows / columns of W that exist (n_pad for an augmented matrix; n for a caller's L)
 };
 
 // ----------------------------------------------------------------------------------- launchers
@@ -244,6 +245,13 @@ hipError_t launch_pinv_bwd_scale(const double* lam, const double* mu, int m, dou
 hipError_t launch_ski_weights(const double* X, int64_t n, const double* Z, int64_t m, int d, double* Wm,
                               double* work, hipStream_t s);
 hipError_t launch_copy_lower(const double* src, int64_t lds, double* dst, int64_t ldd, int64_t n, hipStream_t s);
+// caller-matrix entries of the §8(b) sketch (gpk_flat.hip)
+hipError_t launch_pack_lower(int dtype, const void* A, int64_t lda, int64_t n, int64_t n_pad, int64_t p, void* W,
+                             hipStream_t s);
+hipError_t launch_unpack_lower(int dtype, const void* W, int64_t ld, int64_t n, void* A, int64_t lda, hipStream_t s);
+hipError_t launch_trtri_blocks(const double* L, int64_t ldl, int64_t n, double* Winv, hipStream_t s);
+hipError_t launch_posterior_var(const double* V, int64_t n, int64_t m, const double* kdiag, double* var,
+                                hipStream_t s);
 hipError_t launch_distance(int mode, const double* A, int64_t n, int64_t a_bs, const double* B, int64_t m,
                            int64_t b_bs, int d, int32_t batch, double* out, int64_t ldo, int64_t o_bs, hipStream_t s);
 hipError_t launch_add_diag(double* A, int64_t n, int64_t lda, int64_t a_bs, double value, int32_t batch,

@@ -555,16 +555,18 @@ __global__ __launch_bounds__(256) void trsv_update_kernel(TrsvArgs a) {
   __syncthreads();
   if (a.trans == 0) {
     const int64_t i = j0 + NB + (int64_t)blockIdx.x * 256 + tid;
-    if (i >= a.n_pad) return;
+    if (i >= a.n_valid) return;  // rows past a caller L's n: padding, x stays 0 there
     const T* row = W + i * a.ld + j0;
+    const int kn = (int)((a.n_valid - j0) < NB ? (a.n_valid - j0) : NB);
     double s = 0.0;
-    for (int k = 0; k < NB; ++k) s = fma((double)row[k], xk[k], s);
+    for (int k = 0; k < kn; ++k) s = fma((double)row[k], xk[k], s);
     x[i] -= s;
   } else {
     const int64_t j = (int64_t)blockIdx.x * 256 + tid;
     if (j >= j0) return;
+    const int kn = (int)((a.n_valid - j0) < NB ? (a.n_valid - j0) : NB);
     double s = 0.0;
-    for (int k = 0; k < NB; ++k) s = fma((double)W[(j0 + k) * a.ld + j], xk[k], s);
+    for (int k = 0; k < kn; ++k) s = fma((double)W[(j0 + k) * a.ld + j], xk[k], s);
     x[j] -= s;
   }
 }

@@ -231,12 +231,30 @@ int gpk_gemv(const double* A, int64_t n, int64_t m, int64_t lda, const double* x
 
 /* ------------------------------------------------------ workspace-style entries
  * The flat signatures of the survey's boundary sketch: one caller scratch buffer of
- * gpk_workspace_bytes(op, ...) bytes replaces the layout and W / Winv.  (The single-problem
- * gpk_nlml of that sketch is gpk_nlml_batched with batch = 1; the sketch's gpk_trsv_lower and
- * gpk_posterior are served by gpk_trsv and by the test rows of the augmented factorisation --
- * gpk_assemble with Xs + gpk_potrf_aug + gpk_finalize(mu, var) -- see INTEGRATION.md.) */
-enum { GPK_WS_NLML = 0, GPK_WS_POTRF = 1 };
+ * gpk_workspace_bytes(op, dtype, n, m, batch) bytes replaces the layout and W / Winv (the sketch's
+ * gpk_trsv_lower / gpk_posterior take that buffer as two extra arguments).  The single-problem gpk_nlml of
+ * the sketch is gpk_nlml_batched with batch = 1.  GPK_WS_POTRF: fp64 or fp32; GPK_WS_TRSV, GPK_WS_POSTERIOR
+ * (m = test points): fp64.  0 for an unsupported combination. */
+enum { GPK_WS_NLML = 0, GPK_WS_POTRF = 1, GPK_WS_TRSV = 2, GPK_WS_POSTERIOR = 3 };
 size_t gpk_workspace_bytes(int op, int dtype, int64_t n, int64_t m, int32_t batch);
+
+/* x <- L^-1 x (trans 0) or L^-T x (trans 1) for a caller's lower-triangular fp64 L [n, ldl] (row-major, the
+ * upper triangle not read) and a device vector x [n]: the triangular_solve of get_L_alpha
+ * (Statistics/CovarianceMatrix.py:256-265) on an arbitrary factor.  The 128 x 128 diagonal blocks of L are
+ * inverted once into the workspace (forward substitution), then the blocked solve of gpk_trsv runs on L itself. */
+int gpk_trsv_lower(int dtype, int trans, const double* L, int64_t n, int64_t ldl, double* x, void* work,
+                   size_t work_bytes, void* stream);
+
+/* Posterior of a GP from a caller's factor L [n, ldl] of K + noise I and alpha = (K + noise I)^-1 y
+ * (Statistics/Auxiliary.py:57-103, GaussianProcess.predict): mu [m] = K_s^T alpha (may be NULL) and, if var is not
+ * NULL, var_mode 0: var [m] = diag(K_ss - V^T V), var_mode 1: var [m, ldv] = K_ss - V^T V, with K_s = k(X, Xs),
+ * V = L^-1 K_s (blocked, MFMA GEMMs against the inverted diagonal blocks).  var_mode 0 takes k(x*, x*) from the
+ * first test point (every kernel of a descriptor is stationary).  fp64.  (The augmented factorisation's test rows
+ * -- gpk_assemble with Xs + gpk_potrf_aug + gpk_finalize -- give the same without a separate pass over L.) */
+int gpk_posterior(const gpk_kdesc* kd, const double* hyp_dev, int dtype, const double* L, int64_t ldl,
+                  const double* alpha, const double* X, int64_t n, const double* Xs, int64_t m, int32_t d,
+                  int32_t var_mode, double* mu, double* var, int64_t ldv, void* work, size_t work_bytes,
+                  void* stream);
 
 /* -LML of `batch` hyperparameter / noise candidates on shared X [n, d], y [n] (device):
  * hyp_dev [batch][kd->n_hyp], noise_dev [batch], nlml_dev [batch] (+inf where info_dev[b] != 0).
@@ -245,8 +263,9 @@ int gpk_nlml_batched(const gpk_kdesc* kd, int32_t batch, const double* hyp_dev, 
                      const double* X, const double* y, int64_t n, int32_t d, void* work, size_t work_bytes,
                      double* nlml_dev, int32_t* info_dev, void* stream);
 
-/* In-place lower Cholesky of a row-major fp64 A [n, lda] (upper triangle untouched, LAPACK
- * dpotrf semantics) through the blocked MFMA factorisation: tf.linalg.cholesky of get_L_K
+/* In-place lower Cholesky of a row-major fp64 (double*) or fp32 (float*, dtype GPK_F32: factored on the f32
+ * MFMA path) A [n, lda] (upper triangle untouched, LAPACK potrf semantics) through the blocked MFMA
+ * factorisation: tf.linalg.cholesky of get_L_K
  * (Statistics/CovarianceMatrix.py:247-254).  *info_dev: 0 or the first non-positive pivot
  * (1-based); *logdet_dev (may be NULL) = 2 sum log diag L (Metrics/Metrics.py:152-154). */
 int gpk_potrf_lower(int dtype, void* A, int64_t n, int64_t lda, void* work, size_t work_bytes, int32_t* info_dev,
