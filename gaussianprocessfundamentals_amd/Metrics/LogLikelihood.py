@@ -57,10 +57,6 @@ class LogLikelihood(AbstractLogLikelihood):
             z = indices if isinstance(indices, torch.Tensor) else None
             return _ApproxNegLogLikelihood.apply(self, z, _as_tensor(noise), *[_as_tensor(h) for h in hyper_parameter])
         if _wants_grad(hyper_parameter, noise):
-            if self.numerical_matrix_handling is mht.NumericalMatrixHandlingType.LINEAR_CONJUGATE_GRADIENT:
-                # the reference's tape differentiates the CG iterations (tolerance 1e-2); the analytic
-                # gradient is the exact one, which would not belong to the CG value
-                raise NotImplementedError("gradients through LINEAR_CONJUGATE_GRADIENT are not provided")
             # differentiable form: what the reference's tf.GradientTape sees through get_metric
             # (Optimizer/Fitter.py:104-158); backward() uses the analytic device gradient.  The value
             # comes from the selected handling (STRICT / PSEUDO inverse: the exact gradient is theirs)
@@ -139,7 +135,9 @@ class LogLikelihood(AbstractLogLikelihood):
             raise NotImplementedError("approximate metrics: differentiate get_metric(hyper_parameter, noise, "
                                       "indices) with autograd (inducing-input gradients included)")
         if self.numerical_matrix_handling is H.LINEAR_CONJUGATE_GRADIENT:
-            raise NotImplementedError("gradients through LINEAR_CONJUGATE_GRADIENT are not provided")
+            if self.data_input.data_x_train.dim() == 3:
+                raise NotImplementedError("LINEAR_CONJUGATE_GRADIENT gradients are provided for DataInput")
+            return self._lcg_metric_and_gradient(hyper_parameter, noise)
         if self.data_input.data_x_train.dim() == 3:
             return self._batch_metric_and_gradient(hyper_parameter, noise)
         if self.numerical_matrix_handling in (H.STRICT_INVERSE, H.PSEUDO_INVERSE) and \
@@ -195,6 +193,36 @@ class LogLikelihood(AbstractLogLikelihood):
         gh, _ = engine.kernel_vjp(self.covariance_matrix.kernel, hyper_parameter, x, x,
                                   G=(kbar + kbar.T).contiguous())
         return value, _split_like(0.5 * gh, hyper_parameter), torch.trace(kbar)
+
+    def _lcg_metric_and_gradient(self, hyper_parameter: List, noise):
+        """LINEAR_CONJUGATE_GRADIENT (Metrics.py:141-147): -LML = 1/2 y^T x_cg + 1/2 slogdet(K) + c with x_cg the
+        reference's CG iterate (tolerance 1e-2), differentiated as tf.GradientTape does -- through the executed
+        iterations (Auxiliary.LinearConjugateGradients.linear_cg_backward: one GEMV per iteration in reverse),
+        not as the exact solve.  Adjoint of K: Q P^T from the loop (seeded with 1/2 y) plus 1/2 K^-1 from the
+        log-determinant (identity-augmented factorisation; the eigendecomposition when K is not positive
+        definite); then gpk_kernel_vjp for the hyperparameters and its trace for the noise."""
+        from .. import engine
+        from ..Auxiliary.LinearConjugateGradients import linear_cg, linear_cg_backward
+        K = self.get_covariance_matrix(hyper_parameter, noise, None).contiguous()
+        y = self._y(None)
+        tape = []
+        x = linear_cg(K, y, torch.zeros_like(y), tape=tape)
+        n = float(self.data_input.n_train)
+        logdet = self.get_log_determinant(hyper_parameter, noise, None)
+        value = (-((-0.5 * torch.sum(y * x) + -0.5 * logdet) + (-0.5 * (n * LOG_2PI)))).reshape(1, 1)
+        P, Q = linear_cg_backward(K, tape, 0.5 * y)
+        if self._positive_definite(hyper_parameter, noise):
+            f = self.covariance_matrix.inverse_factorization(hyper_parameter, noise, gradient=False)
+            G = (0.5 * f.k_inv(0).to(torch.float64)).contiguous()
+        else:
+            lam, V = self._eigen(hyper_parameter, noise)
+            _, _, mu_all = engine.pinv_factor(lam, V, 0, rcond=0.0, return_mu=True)
+            G = 0.5 * engine.dgemm(V * mu_all[None, :], V, trans_b=True)
+        if P.shape[1] > 0:
+            G = engine.dgemm(Q, P, trans_b=True, beta=1.0, C=G)
+        xin = self.data_input.data_x_train
+        gh, _ = engine.kernel_vjp(self.covariance_matrix.kernel, hyper_parameter, xin, xin, G=G)
+        return value, _split_like(gh, hyper_parameter), torch.trace(G)
 
     def get_gradients(self, hyper_parameter: List, noise, reset: bool = True) -> torch.Tensor:
         """Metrics.py:31 (AbstractMetric.get_gradients; the reference's gradient_function of

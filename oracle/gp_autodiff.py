@@ -260,6 +260,42 @@ def inverse_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.nd
     return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1])
 
 
+def lcg_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, scaled: bool = False):
+    """-LML with LINEAR_CONJUGATE_GRADIENT (alpha = linear_cg(K, y, 0), M/Metrics.py:141-144, the loop of
+    Auxiliary/LinearConjugateGradients.py:9-41 restated op for op -- |max r| > 1e-2 stopping rule, NaN early
+    return, the n-iteration guard) and slogdet (:146-147), with its reverse-mode gradient through the executed
+    iterations, as tf.GradientTape records them.  Returns (nlml, [grad per hyperparameter], grad noise,
+    iterations)."""
+    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
+    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
+    X = torch.as_tensor(np.asarray(x, dtype=np.float64))
+    Y = torch.as_tensor(np.asarray(y, dtype=np.float64)).reshape(-1, 1)
+    n = X.shape[0]
+    K = kernel_matrix_t(tree, params, X, X, scaled) + nz * torch.eye(n, dtype=F64)
+    xk = torch.zeros((n, 1), dtype=F64)
+    r = K @ xk - Y
+    p = -r
+    k, first = 0, True
+    while first or float(torch.abs(torch.max(r))) > 1e-2:
+        Ap = K @ p
+        a = (r.T @ r) / (p.T @ Ap)
+        nxt = xk + a * p
+        if bool(torch.any(torch.isnan(nxt))):
+            break
+        xk = nxt
+        r1 = r + a * Ap
+        beta = (r1.T @ r1) / (r.T @ r)
+        p = -r1 + beta * p
+        r = r1
+        k += 1
+        first = False
+        if k % (n / 4) == 0 and k > n:
+            break
+    nl = -(-0.5 * (Y.T @ xk)[0, 0] - 0.5 * torch.linalg.slogdet(K)[1] - 0.5 * n * LOG_2PI)
+    grads = torch.autograd.grad(nl, params + [nz])
+    return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1]), k
+
+
 def batch_nlml_and_grad(tree, hyp: List, noise: float, xb: np.ndarray, yb: np.ndarray,
                         handling: str = "CHOLESKY_BASED", agg: str = "mean", scaled: bool = False):
     """BatchDataInput -LML (quirk Q7) and its gradient: CHOLESKY_BASED -agg_b(-1/2 fit_b - 1/2 sum_b' logdet_b'

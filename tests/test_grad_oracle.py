@@ -117,3 +117,23 @@ def test_indefinite_gradient_oracle_matches_finite_differences(handling):
     fd, fdn = ad.finite_difference(f, [0.1], -0.3, h=1e-6)
     np.testing.assert_allclose(g[0], fd[0], rtol=1e-5)
     assert abs(gn - fdn) < 1e-5 * max(1.0, abs(fdn))
+
+
+@pytest.mark.parametrize("n,ls,noise", [(40, 0.1, 0.3), (40, 0.05, 0.5), (60, 0.1, 1.0)])
+def test_lcg_gradient_oracle_matches_finite_differences(n, ls, noise):
+    """LINEAR_CONJUGATE_GRADIENT: the restated CG loop's value and its tape gradient.  The iterate depends
+    smoothly on the hyperparameters while the number of executed iterations stays fixed, so the
+    finite-difference steps are checked to run the same iteration count.  (With small noise the CG iterate
+    is so sensitive to rounding that central differences of it are noise below h ~ 1e-4 -- the tape's
+    gradient is still exact for the executed operations -- so the checks use noise >= 0.3.)"""
+    x, y = _inputs(n, 1, 8)
+    nl, g, gn, its = ad.lcg_nlml_and_grad(("SE", {}), [ls], noise, x, y)
+    assert its >= 3
+    h = 1e-6
+    for dh in (h, -h):
+        assert ad.lcg_nlml_and_grad(("SE", {}), [ls + dh], noise, x, y)[3] == its
+        assert ad.lcg_nlml_and_grad(("SE", {}), [ls], noise + dh, x, y)[3] == its
+    f = lambda hh, nz: ad.lcg_nlml_and_grad(("SE", {}), hh, nz, x, y)[0]
+    fd, fdn = ad.finite_difference(f, [ls], noise, h=h)
+    np.testing.assert_allclose(g[0], fd[0], rtol=1e-6)
+    assert abs(gn - fdn) < 1e-6 * max(1.0, abs(fdn))
