@@ -33,7 +33,7 @@ EXPORTS = (
     "gpk_assemble_dense", "gpk_dgemm", "gpk_syevj_workspace_bytes", "gpk_syevj", "gpk_pinv_factor",
     "gpk_ski_weights", "gpk_add_diagonal", "gpk_distance_matrix", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower", "gpk_trsv_lower", "gpk_posterior",
     "gpk_kernel_vjp_workspace_bytes", "gpk_kernel_vjp", "gpk_pinv_backward_scale", "gpk_syevd_workspace_bytes",
-    "gpk_syevd",
+    "gpk_syevd", "gpk_chain_plan",
 )
 
 
@@ -119,6 +119,8 @@ def _declare(lib):
         "gpk_pinv_backward_scale": (c_int, [c_int64, c_int32, P, P, P, P]),
         "gpk_syevd_workspace_bytes": (c_size_t, [c_int64]),
         "gpk_syevd": (c_int, [c_int64, c_int32, P, c_int64, c_int64, P, P, P, c_size_t, P]),
+        "gpk_chain_plan": (c_int, [c_int64, c_int64, c_int32, P, c_int64, POINTER(c_int64)]),
+        "gpk_chain_trace": (c_int, [P, c_int64]),
         "gpk_kernel_vjp_workspace_bytes": (c_size_t, [POINTER(GpkKdesc), c_int64, c_int64, c_int32, c_int32]),
         "gpk_kernel_vjp": (c_int, [POINTER(GpkKdesc), P, P, c_int64, P, c_int64, c_int32, P, c_int64, P, P, P, P,
                                    P, c_size_t, P]),
@@ -200,6 +202,19 @@ def tune(key: str, value: int) -> int:
     old = c_int64(0)
     check(load_library().gpk_tune(key.encode(), int(value), ctypes.byref(old)), "gpk_tune")
     return int(old.value)
+
+
+def chain_plan(n_pad: int, y_row: int, grid: int):
+    """Task list of the persistent single-member factorisation (gpk_chain_plan; host only): an
+    [ntasks, 4] int32 array of (type, k, r, j) in claim order."""
+    import numpy as np
+    L = load_library()
+    nt = c_int64(0)
+    check(L.gpk_chain_plan(int(n_pad), int(y_row), int(grid), None, 0, ctypes.byref(nt)), "gpk_chain_plan")
+    out = np.zeros((int(nt.value), 4), dtype=np.int32)
+    check(L.gpk_chain_plan(int(n_pad), int(y_row), int(grid), c_void_p(out.ctypes.data), int(nt.value),
+                           ctypes.byref(nt)), "gpk_chain_plan")
+    return out
 
 
 def timing_reset():

@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <initializer_list>
 #include <map>
+#include <queue>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -161,6 +163,10 @@ struct Tune {
                           // 2 normal-priority side stream
   int64_t trd_split_m;    // gpk_syevd: above this m the tridiagonalisation's A22 v runs over the chip (three
                           // launches per column) instead of inside one workgroup per panel
+  int64_t chain;          // single f64 factorisations as ONE persistent launch (chain_kernel): 1 on, 0 off
+  int64_t chain_max_p;    //   ... while the augmented matrix has at most this many rows
+  int64_t chain_grid;     //   workgroups of that launch (0: one per CU)
+  int64_t chain_timeout_ms;  // bound of every wait inside it (then info = -1)
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -178,7 +184,9 @@ Tune& tune() {
                          env_i64("GPK_DIAG_VERSION", 2), env_i64("GPK_INGROUP", 0),
                          env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1),
                          env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0),
-                         env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024)};
+                         env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024),
+                         env_i64("GPK_CHAIN", 0), env_i64("GPK_CHAIN_MAX_P", 4480), env_i64("GPK_CHAIN_GRID", 0),
+                         env_i64("GPK_CHAIN_TIMEOUT_MS", 1000)};
   return t;
 }
 
@@ -277,6 +285,187 @@ int32_t* fuse_counters(hipStream_t s) {
   }
   g_ctr[{dev, s}] = p;  // owned for the life of the process
   return p;
+}
+
+
+// ------------------------------------------------------------------------ persistent factorisation
+// Task order of chain_kernel (gpk_potrf.hip) for one shape: the task graph (D / S / U32 / BLK, see there)
+// list-scheduled on `grid` workers with estimated durations, highest bottom level (longest path to the
+// end) first; the order in which the simulation starts the tasks is a topological order, which the
+// kernel needs (every task waits only for tasks claimed before it), and puts the diagonal chain ahead
+// of the trailing tiles whenever both are ready.
+struct ChainPlan {
+  int32_t* tasks = nullptr;  // device [ntasks][4]
+  int32_t ntasks = 0;
+  int32_t nblk = 0, nsl = 0, nbc = 0;
+};
+std::mutex g_chain_mu;
+std::map<std::tuple<int, int64_t, int64_t, int>, ChainPlan> g_chain_plans;
+std::map<std::pair<int, hipStream_t>, std::pair<int32_t*, size_t>> g_chain_ctl;
+int32_t* g_chain_trace = nullptr;  // GPK_CHAIN_TRACE=1: pinned host words the kernel writes its progress to
+
+enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
+
+std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid) {
+  const int nblk = (int)(n_pad / NB), yb = (int)(y_row / NB), rlast = (int)(y_row / 32);
+  struct Task {
+    int ty, k, r, j;
+    float dur;
+    std::vector<int> deps;
+  };
+  std::vector<Task> T;
+  const int nr = rlast + 1;
+  std::vector<int> D(nblk, -1), S((size_t)nblk * nr, -1), U((size_t)nblk * nr, -1);
+  std::map<std::tuple<int, int, int>, int> B;
+  auto s_of = [&](int k, int r) { return S[(size_t)k * nr + r]; };
+  auto u_of = [&](int k, int r) { return U[(size_t)k * nr + r]; };
+  auto add = [&](Task t) {
+    T.push_back(std::move(t));
+    return (int)T.size() - 1;
+  };
+  for (int k = 0; k < nblk; ++k) {
+    Task d{CHT_D, k, 0, k, 28.f, {}};
+    if (k > 0)
+      for (int s = 4 * k; s <= std::min(4 * k + 3, rlast); ++s) d.deps.push_back(u_of(k - 1, s));
+    D[k] = add(d);
+    for (int r = 4 * (k + 1); r <= rlast; ++r) {
+      Task t{CHT_S, k, r, 0, 7.f, {D[k]}};
+      if (k > 0) t.deps.push_back(u_of(k - 1, r));
+      S[(size_t)k * nr + r] = add(t);
+    }
+    for (int r = 4 * (k + 1); r <= rlast; ++r) {
+      Task t{CHT_U32, k, r, k + 1, 7.f, {s_of(k, r)}};
+      for (int s = 4 * (k + 1); s <= std::min(4 * (k + 1) + 3, rlast); ++s)
+        if (s != r) t.deps.push_back(s_of(k, s));
+      if (k > 0) t.deps.push_back(B.at(std::make_tuple(k - 1, r / 4, k + 1)));
+      U[(size_t)k * nr + r] = add(t);
+    }
+    for (int j = k + 2; j <= yb; ++j)
+      for (int i = j; i <= yb; ++i) {
+        Task t{CHT_BLK, k, i, j, 18.f, {}};
+        for (int s = 4 * i; s <= std::min(4 * i + 3, rlast); ++s) t.deps.push_back(s_of(k, s));
+        if (j != i)
+          for (int s = 4 * j; s <= std::min(4 * j + 3, rlast); ++s) t.deps.push_back(s_of(k, s));
+        if (k > 0) t.deps.push_back(B.at(std::make_tuple(k - 1, i, j)));
+        B[std::make_tuple(k, i, j)] = add(t);
+      }
+  }
+  const int n = (int)T.size();
+  std::vector<std::vector<int>> succ(n);
+  std::vector<int> indeg(n, 0);
+  for (int t = 0; t < n; ++t)
+    for (int d : T[t].deps) {
+      succ[d].push_back(t);
+      ++indeg[t];
+    }
+  std::vector<float> bl(n, 0.f);
+  for (int t = n - 1; t >= 0; --t) {  // the construction order is topological
+    float m = 0.f;
+    for (int s : succ[t]) m = std::max(m, bl[s]);
+    bl[t] = T[t].dur + m;
+  }
+  auto cmp = [&](int a, int b) { return bl[a] != bl[b] ? bl[a] < bl[b] : a > b; };
+  std::priority_queue<int, std::vector<int>, decltype(cmp)> ready(cmp);
+  std::priority_queue<std::pair<float, int>, std::vector<std::pair<float, int>>, std::greater<std::pair<float, int>>> ev;
+  for (int t = 0; t < n; ++t)
+    if (indeg[t] == 0) ready.push(t);
+  std::vector<int32_t> out;
+  out.reserve((size_t)n * 4);
+  int free = std::max(1, grid);
+  float now = 0.f;
+  while ((int)out.size() < 4 * n) {
+    while (free > 0 && !ready.empty()) {
+      const int t = ready.top();
+      ready.pop();
+      out.insert(out.end(), {T[t].ty, T[t].k, T[t].r, T[t].j});
+      ev.push({now + T[t].dur, t});
+      --free;
+    }
+    if (ev.empty()) break;  // (cannot happen for a well-formed graph)
+    const auto e = ev.top();
+    ev.pop();
+    now = e.first;
+    ++free;
+    for (int s : succ[e.second])
+      if (--indeg[s] == 0) ready.push(s);
+  }
+  return out;
+}
+
+// chain_kernel applies to one f64 member without identity or ragged rows, on a stream that is not being
+// captured (the first call of a shape uploads its task list), up to chain_max_p rows
+bool chain_applies(const gpk_layout* lay, bool eye, const int64_t* n_dev, const int64_t* m_dev, const Tune& tn,
+                   hipStream_t s) {
+  if (!tn.chain || lay->dtype != GPK_F64 || lay->batch != 1 || eye || n_dev || m_dev) return false;
+  if (lay->p > tn.chain_max_p || tn.diag_dbg != 0 || tn.diag_version == 1) return false;
+  if (s == hipStreamPerThread) return false;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+}
+
+int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, const Tune& tn, hipStream_t s) {
+  int dev = 0, ncu = 0;
+  GPK_HIP(hipGetDevice(&dev), "device");
+  GPK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "device");
+  const int grid = tn.chain_grid > 0 ? (int)tn.chain_grid : ncu;
+  ChainPlan plan;
+  int32_t* ctl = nullptr;
+  size_t ctl_ints = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid);
+    auto it = g_chain_plans.find(key);
+    if (it == g_chain_plans.end()) {
+      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid);
+      ChainPlan p;
+      p.ntasks = (int32_t)(ord.size() / 4);
+      p.nblk = (int32_t)(lay->n_pad / NB);
+      p.nsl = (int32_t)(lay->y_row / 32 + 1);
+      p.nbc = (int32_t)(lay->y_row / NB + 1);
+      GPK_HIP(hipMalloc(&p.tasks, ord.size() * sizeof(int32_t)), "chain tasks");
+      GPK_HIP(hipMemcpy(p.tasks, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice), "chain tasks");
+      it = g_chain_plans.emplace(key, p).first;  // owned for the life of the process
+    }
+    plan = it->second;
+    ctl_ints = 4 + (size_t)plan.nblk + (size_t)plan.nblk * plan.nsl + (size_t)plan.nsl * plan.nbc;
+    ctl_ints = (ctl_ints + 3) / 4 * 4;
+    auto& c = g_chain_ctl[{dev, s}];
+    if (c.second < ctl_ints) {
+      if (c.first) GPK_HIP(hipFree(c.first), "chain scratch");  // (synchronises the device)
+      c = {nullptr, 0};
+      GPK_HIP(hipMalloc(&c.first, ctl_ints * sizeof(int32_t)), "chain scratch");
+      c.second = ctl_ints;
+    }
+    ctl = c.first;
+  }
+  // every counter starts at zero in every call
+  GPK_HIP(hipMemsetAsync(ctl, 0, ctl_ints * sizeof(int32_t), s), "chain memset");
+  ChainArgs a;
+  memset(&a, 0, sizeof(a));
+  a.W = static_cast<double*>(W);
+  a.ld = lay->ld;
+  a.Winv = static_cast<double*>(Winv);
+  a.info = info_dev;
+  a.tasks = plan.tasks;
+  a.ntasks = env_i64("GPK_CHAIN_MAX_TASKS", 0) > 0 ? (int32_t)std::min<int64_t>(plan.ntasks, env_i64("GPK_CHAIN_MAX_TASKS", 0)) : plan.ntasks;  // (debugging)
+  a.dbg = (int32_t)env_i64("GPK_CHAIN_DBG", 0);
+  a.ctl = ctl;
+  a.dflag = ctl + 4;
+  a.sdone = a.dflag + plan.nblk;
+  a.ucnt = a.sdone + (size_t)plan.nblk * plan.nsl;
+  a.nsl = plan.nsl;
+  a.nbc = plan.nbc;
+  a.row_end = lay->y_row + 1;
+  a.timeout = std::max<int64_t>(1, tn.chain_timeout_ms) * 100000;  // 100 MHz ticks
+  if (env_i64("GPK_CHAIN_TRACE", 0)) {
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    if (!g_chain_trace) GPK_HIP(hipHostMalloc(&g_chain_trace, 4096 * 32 * sizeof(int32_t), hipHostMallocCoherent), "trace");
+    memset(g_chain_trace, 0xff, 4096 * 32 * sizeof(int32_t));
+    a.trace = grid <= 4096 ? g_chain_trace : nullptr;
+  }
+  const double n3 = (double)lay->n_pad;
+  GPK_HIP(timed(3, n3 * n3 * n3 / 3.0, 0.0, s, [&] { return launch_chain(a, grid, s); }), "chain");
+  return 0;
 }
 
 }  // namespace
@@ -426,6 +615,8 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   // one snapshot of the knobs per call: a gpk_tune from another thread (ctypes releases the GIL during
   // the enqueue) must not change the fuse decision between a panel's diag(k) and trsm(k)
   const Tune tn = tune();
+  // a single evaluation: the whole factorisation as one persistent launch (no K build fused into it)
+  if (!kb && chain_applies(lay, eye, n_dev, m_dev, tn, s)) return chain_potrf(lay, W, Winv, info_dev, tn, s);
   // The panel chain (diag, panel solve, thin and look-ahead updates) runs on a high-priority
   // stream, the bulk of each trailing update on a CU-masked stream concurrently with the next
   // panel pair's chain; both fork from and join back into the caller's stream.
@@ -758,6 +949,7 @@ int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, 
   const int64_t G0 = std::max<int64_t>(1, std::min<int64_t>(tn.group_first, G));
   const int op0 = kd ? kd->nodes[0].op : 0;
   if (tn.fuse_kbuild && lay->dtype == GPK_F64 && valid_kdesc(kd, lay->d) && kd->n_nodes == 1 && G0 < nblk &&
+      !chain_applies(lay, false, nullptr, nullptr, tn, s) &&
       (op0 == GPK_OP_SE || op0 == GPK_OP_MAT32 || op0 == GPK_OP_MAT52)) {
     int e = assemble_impl(kd, lay, hyp_dev, hyp_stride, noise_dev, noise_stride, X, x_bstride, nullptr, 0,
                           nullptr, 0, y, y_bstride, W, false, nullptr, nullptr, stream, G0 * NB / ATILE);
@@ -1476,6 +1668,27 @@ int gpk_timing_enable(int on) {
   return 0;
 }
 
+// debugging: the progress words of the last traced chain launch (GPK_CHAIN_TRACE=1), host memory only
+int gpk_chain_trace(int32_t* out, int64_t n) {
+  if (!g_chain_trace || !out) return -1;
+  memcpy(out, g_chain_trace, (size_t)std::min<int64_t>(n, 4096 * 32) * sizeof(int32_t));
+  return 0;
+}
+
+int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_out, int64_t cap, int64_t* ntasks) {
+  if (n_pad <= 0 || n_pad % NB != 0) return fail_arg(1, "n_pad (a positive multiple of 128)");
+  if (y_row < n_pad) return fail_arg(2, "y_row (>= n_pad)");
+  if (grid <= 0) return fail_arg(3, "grid");
+  if (!ntasks) return fail_arg(6, "ntasks");
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid);
+  *ntasks = (int64_t)(ord.size() / 4);
+  if (tasks_out) {
+    if (cap < *ntasks) return fail_arg(5, "cap (fewer than ntasks)");
+    memcpy(tasks_out, ord.data(), ord.size() * sizeof(int32_t));
+  }
+  return 0;
+}
+
 int gpk_tune(const char* key, int64_t value, int64_t* old) {
   if (!key) return fail_arg(1, "key");
   Tune& t = tune();
@@ -1502,6 +1715,10 @@ int gpk_tune(const char* key, int64_t value, int64_t* old) {
   else if (!strcmp(key, "fuse_trsm")) slot = &t.fuse_trsm;
   else if (!strcmp(key, "fuse_trsm_max")) slot = &t.fuse_trsm_max;
   else if (!strcmp(key, "trd_split_m")) slot = &t.trd_split_m;
+  else if (!strcmp(key, "chain")) slot = &t.chain;
+  else if (!strcmp(key, "chain_max_p")) slot = &t.chain_max_p;
+  else if (!strcmp(key, "chain_grid")) slot = &t.chain_grid;
+  else if (!strcmp(key, "chain_timeout_ms")) slot = &t.chain_timeout_ms;
   if (!slot) return fail_arg(1, "key (unknown tuning knob)");
   if (old) *old = *slot;
   *slot = value;

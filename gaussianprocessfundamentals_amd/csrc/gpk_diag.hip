@@ -16,115 +16,13 @@
 // Writes L_kk to W (lower triangle) and L_kk^-1 (zeros above the diagonal) to Winv; the first
 // non-positive pivot (1-based global column) goes to info[b] (LAPACK convention, as the
 // InvalidArgumentError of tf.linalg.cholesky at gpbasics/Statistics/CovarianceMatrix.py:250).
-#include <type_traits>
-
-#include "gpk_internal.h"
+//
+// The device code (block load, potf2, tile operations, inverse, stores) lives in gpk_diag_dev.h, shared
+// with the persistent factorisation of gpk_potrf.hip.
+#include "gpk_diag_dev.h"
 
 namespace gpk {
 namespace {
-
-constexpr int DB = 16;            // tile edge
-constexpr int NTL = NB / DB;      // tiles per block edge (8)
-#ifndef GPK_DIAG_SWIZZLE
-#define GPK_DIAG_SWIZZLE 0
-#endif
-// LDS row stride (doubles).  Default: 130, so the 16 rows of one column that the MFMA operand reads take
-// (lanes along rows) sit on distinct banks; the accumulator-layout accesses (lanes along 16 columns x 2
-// consecutive rows) are then 2-way conflicted.  GPK_DIAG_SWIZZLE=1: rows of 128 with the columns XOR-swizzled
-// per row, c ^ (16 (r & 1) + 2 ((r >> 1) & 7)), conflict-free for both patterns (SQ_LDS_BANK_CONFLICT per LDS
-// instruction 2.12 -> 0.75) but slower: the fused diagonal launch at N = 4096 took 44.8 instead of 40.2 us
-// (the swizzled addresses split the block load's 16-B LDS stores and add VALU work on the potf2 path).
-constexpr int LDA = GPK_DIAG_SWIZZLE ? NB : NB + 2;
-constexpr int DT = 512;           // threads (8 waves)
-constexpr int LDS_A = NB * LDA;
-
-__device__ __forceinline__ int aidx(int r, int c) {
-  return GPK_DIAG_SWIZZLE ? r * LDA + (c ^ (((r & 1) << 4) | (((r >> 1) & 7) << 1))) : r * LDA + c;
-}
-#ifndef GPK_DINV_LD
-#define GPK_DINV_LD 18  // row stride of the inverted pivot tiles: lane (r, k) reads of a tile row hit distinct
-#endif              // banks (stride 16: the 16 rows sat on two banks, an 8-way conflict per read)
-constexpr int DBS = GPK_DINV_LD;   // Dinv tile row stride (doubles)
-constexpr int DTS = DB * DBS;      // Dinv tile stride
-constexpr int LDS_DINV = NTL * DTS;
-constexpr int LDS_COL = 2 * DB;  // potf2 column broadcast, double-buffered
-constexpr size_t DIAG_LDS_BYTES = sizeof(double) * (LDS_A + LDS_DINV + LDS_COL) + 16;
-
-// 1/sqrt(x) from the hardware estimate plus two Newton steps (~1 ulp); NaN for x < 0.
-#ifndef GPK_RSQ_NEWTON
-#define GPK_RSQ_NEWTON 2  // Newton steps after the hardware estimate (A/B builds only)
-#endif
-__device__ __forceinline__ double rsqrt_refined(double x) {
-  double r = __builtin_amdgcn_rsq(x);
-  const double h = 0.5 * x;
-#pragma unroll
-  for (int i = 0; i < GPK_RSQ_NEWTON; ++i) r = r * fma(-h * r, r, 1.5);
-  return r;
-}
-
-__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-// potf2 + inverse of tile (kb, kb), one wave.  Lanes 0..15 hold row r = lane of the tile and
-// factor it (right-looking); lanes 16..31 hold column r = lane - 16 of the identity and turn it
-// into column r of L^-1 (column-oriented forward substitution).  Both run the SAME update per
-// pivot j with w = their 16 values:   a = w[j] / L[j][j];  w[j] = a;  w[c] -= a L[c][j] (c > j)
-// (for a row of A, a = L[r][j]; for a column of the inverse, a = (L^-1)[j][r]).  Column j of L is
-// broadcast through LDS: written by lanes 0..15, read back by every lane with 8 broadcast
-// ds_read_b128.  Lanes 32..63 mirror 0..31 and never store.  (The earlier form -- one readlane
-// per element and a separate substitution -- took 2 x 480 readlanes and spilled SGPRs.)
-__device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf, int kb, int lane,
-                                           int* flag, int64_t col_base) {
-  typedef double dbl2 __attribute__((ext_vector_type(2)));
-  const int r = lane & 15;
-  const bool inv = (lane & 16) != 0;
-  const int c0 = kb * DB;
-  // rows: entries above the diagonal are never used (only c <= r is stored, and column j is
-  // read from rows c >= j only), so the tile row is loaded whole
-  double w[DB];
-#pragma unroll
-  for (int c = 0; c < DB; c += 2) {
-    const dbl2 t = *reinterpret_cast<const dbl2*>(A + aidx(c0 + r, c0 + c));
-    w[c] = inv ? ((c == r) ? 1.0 : 0.0) : t.x;
-    w[c + 1] = inv ? ((c + 1 == r) ? 1.0 : 0.0) : t.y;
-  }
-  int bad = 0;  // first non-positive pivot of this tile (1-based in the tile), wave-uniform
-#pragma unroll
-  for (int j = 0; j < DB; ++j) {
-    double* cb = colbuf + (j & 1) * DB;
-    if (lane < DB) cb[lane] = w[j];            // column j: entry (r, j) of row r
-    // Other lanes' stores are invisible to the per-thread memory model: without a fence hipcc
-    // may serve the reads below from the loads of step j - 2 (same buffer).  The wave's LDS
-    // operations retire in order, so a wave-scope fence is all the hardware needs.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double u[DB];
-#pragma unroll
-    for (int c = j & ~1; c < DB; c += 2) {
-      const dbl2 t = *reinterpret_cast<const dbl2*>(cb + c);
-      u[c] = t.x;
-      u[c + 1] = t.y;
-    }
-    const double piv = u[j];
-    bad = (bad == 0 && !(piv > 0.0)) ? j + 1 : bad;
-    const double ri = rsqrt_refined(piv);      // 1 / L[j][j]
-    const double aj = w[j] * ri;
-    const double g = aj * ri;  // w[c] -= (w[j] / L[j][j]) (u[c] / L[j][j]): one FMA per entry
-    w[j] = aj;
-#pragma unroll
-    for (int c = j + 1; c < DB; ++c) w[c] = fma(-g, u[c], w[c]);
-  }
-  if (bad != 0 && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + bad);
-  if (lane < DB) {
-#pragma unroll
-    for (int c = 0; c < DB; ++c) A[aidx(c0 + r, c0 + c)] = (c <= r) ? w[c] : 0.0;
-  } else if (lane < 2 * DB) {
-#pragma unroll
-    for (int rr = 0; rr < DB; ++rr) Dk[rr * DBS + r] = w[rr];  // Dinv[rr][r]
-  }
-}
 
 template <typename T>
 __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
@@ -259,297 +157,10 @@ __global__ __launch_bounds__(DT) void diag_kernel(DiagArgs a) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Look-ahead form (diag_version 2).  The same tile algebra, scheduled so that the potf2 chain -- the
-// only inherently sequential part -- is the critical path and everything else runs beside it:
-//
-//   P_s  wave 0     : potf2 + inverse of tile (s, s)
-//        waves 1..7 : trailing update of step s-1 for tile columns j >= s + 1; block row I = s - 1
-//                     of L^-1; L's block row s - 1 and L^-1's block row s - 2 to HBM
-//   ---- barrier
-//   QR_s wave w     : row i = s + 1 + w: X_i = A_{i,s} Dinv_s^T and X_{s+1}, both computed transposed
-//                     (Dinv_s A^T), which puts X[r][k = lk + 4q] in the registers of lane (r, lk) --
-//                     the MFMA operand layout -- then A_{i,s+1} -= X_i X_{s+1}^T: tile column s + 1
-//                     is up to date for potf2(s + 1) without waiting for the rest of the update
-//   ---- barrier
-// L^-1 lives in the block's upper tiles, which the factorisation never touches: tile (I, J) of L^-1
-// (J < I) is stored transposed as tile (J, I), its diagonal tiles stay in Dinv -- so no in-place
-// hazard, and each tile of L^-1 goes to HBM from the registers that computed it (the zero tiles in
-// P_0, where waves 1..7 are idle).  Two barriers
-// per step instead of three, the inverse and every HBM store off the critical path, and 16-B loads of
-// the lower tiles only (the upper tiles of the block are never read).
-template <typename T>
-__device__ __forceinline__ void store_l_rows(const double* A, T* Wb, int64_t ld, int I, int t, int nt) {
-  // rows 16 I .. 16 I + 15 of L, columns 0 .. row (lower triangle only, as the phase-serial kernel)
-  constexpr int EPC = 16 / (int)sizeof(T);
-  typedef T vT __attribute__((ext_vector_type(EPC)));
-  const int ppr = (I + 1) * DB / EPC;  // pieces of a row up to the end of its diagonal tile
-  for (int e = t; e < DB * ppr; e += nt) {
-    const int r = I * DB + e / ppr, pc = e % ppr, c0 = pc * EPC;
-    if (c0 + EPC - 1 <= r) {
-      vT v;
-#pragma unroll
-      for (int u = 0; u < EPC; ++u) v[u] = (T)A[aidx(r, c0 + u)];
-      *reinterpret_cast<vT*>(Wb + (int64_t)r * ld + c0) = v;
-    } else {
-#pragma unroll
-      for (int u = 0; u < EPC; ++u)
-        if (c0 + u <= r) Wb[(int64_t)r * ld + c0 + u] = (T)A[aidx(r, c0 + u)];
-    }
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void store_inv_zeros(T* Ib, int t, int nt) {
-  // the tiles right of L^-1's diagonal tiles: zeros (read as such by the panel solve's MFMA chunks)
-  constexpr int EPC = 16 / (int)sizeof(T);
-  typedef T vT __attribute__((ext_vector_type(EPC)));
-  constexpr int PPT = DB / EPC;  // pieces per tile row
-  for (int e = t; e < NB * NB / EPC; e += nt) {
-    const int r = e / (NB / EPC), c0 = (e % (NB / EPC)) * EPC;
-    if (c0 / DB > r / DB) {
-      vT v;
-#pragma unroll
-      for (int u = 0; u < EPC; ++u) v[u] = (T)0;
-      *reinterpret_cast<vT*>(Ib + r * NB + c0) = v;
-    }
-  }
-  (void)PPT;
-}
-
-template <typename T>
-__device__ __forceinline__ void store_inv_diag(const double* Dinv, T* Ib, int I, int t, int nt) {
-  // diagonal tile I of L^-1 (Dinv_I, zeros above its diagonal)
-  for (int e = t; e < DB * DB; e += nt)
-    Ib[(I * DB + e / DB) * NB + I * DB + e % DB] = (T)Dinv[I * DTS + (e / DB) * DBS + e % DB];
-}
-
-// tile (I, J) of L^-1, J < I: -Dinv_I sum_{K=J}^{I-1} L_{I,K} Linv_{K,J}, stored transposed in tile (J, I)
-template <typename T>
-__device__ __forceinline__ void inverse_tile(double* A, const double* Dinv, T* Ib, int I, int J, int lr, int lk,
-                                             bool st = true) {
-  d4 tacc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int s = 0; s < 4; ++s)  // K = J: the diagonal tile Dinv_J
-    tacc = mfma64(A[aidx(I * DB + lr, J * DB + 4 * s + lk)], Dinv[J * DTS + (4 * s + lk) * DBS + lr], tacc);
-  for (int K = J + 1; K < I; ++K) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      tacc = mfma64(A[aidx(I * DB + lr, K * DB + 4 * s + lk)], A[aidx(J * DB + lr, K * DB + 4 * s + lk)], tacc);
-  }
-  const double* Di = Dinv + I * DTS;
-  d4 out = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int s = 0; s < 4; ++s) out = mfma64(-Di[lr * DBS + 4 * s + lk], tacc[s], out);
-  // out[q] = Linv_{I,J}[lk + 4q][lr]  ->  tile (J, I) [lr][lk + 4q] for the later rows, and straight
-  // from the registers to HBM (16 lanes of a row store 128 contiguous bytes)
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    A[aidx(J * DB + lr, I * DB + lk + 4 * q)] = out[q];
-    if (st) Ib[(I * DB + lk + 4 * q) * NB + J * DB + lr] = (T)out[q];
-  }
-}
-
-// rows [r0, r1) of member b are zero in the panel columns [j0, j0 + 128) (gpk_potrf.hip's zero_rows
-// for a panel solve: identity extra rows past the panel, a ragged member's padding / unused test rows)
-__device__ __forceinline__ bool panel_zero_rows(const DiagArgs& a, int b, int64_t r0, int64_t r1) {
-  if (r0 >= a.zlo && r1 <= a.zhi) return true;
-  if (a.nb == nullptr) return false;
-  const int64_t npb = (a.nb[b] + NB - 1) / NB * NB;
-  const int64_t jend = a.j0 + NB;
-  if (a.j0 >= npb) return r0 >= jend && r1 <= a.p;
-  if (r0 >= (npb > jend ? npb : jend) && r1 <= a.n_pad) return true;
-  return a.mb != nullptr && r0 >= a.n_pad + a.mb[b] && r1 <= a.y_row;
-}
-
-// FUSE (f64): a workgroup with ticket t (DiagArgs) also solves the 64 rows R = row0 + 64 t .. +63 of the panel:
-// X = A L_kk^-T with the same MFMA k-order as gemm_kernel<TRSM> (k-step s of chunk kc takes k = 16 kc +
-// 2 q + 8 (s >> 1) + (s & 1) in lane group q; chunks kc > the column block skipped), so X is bitwise
-// the separate panel solve's.  Wave w: 16-row block w & 3, column blocks of half w >> 2 (balanced).  Its A operands (32
-// doubles per lane) are loaded during the last step of the factorisation.
-template <typename T, bool FUSE>
+template <typename T, bool FUSE, bool SC1 = false>
 __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* A = sm;
-  double* Dinv = A + LDS_A;
-  double* colbuf = Dinv + LDS_DINV;
-  int* flag = reinterpret_cast<int*>(colbuf + LDS_COL);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 15;
-  const int lk = lane >> 4;
-  const int b = FUSE ? blockIdx.y : blockIdx.x;
-  int* ticket = flag + 1;
-  T* Wb = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs + a.j0 * a.ld + a.j0;
-  T* Ib = reinterpret_cast<T*>(a.Winv) + (int64_t)b * a.inv_bs + a.kblk * NB * NB;
-  typedef double dbl2 __attribute__((ext_vector_type(2)));
-  dbl2 pa[FUSE ? NTL : 1][2];  // A operands: chunk kc, pieces lk and lk + 4 (k-steps 0, 1 and 2, 3)
-  {
-    // the lower 16-tiles of the block, 16 B per load, every load of a thread in flight at once
-    constexpr int EPC = 16 / (int)sizeof(T);
-    typedef T vT __attribute__((ext_vector_type(EPC)));
-    constexpr int PPR = NB / EPC, RPP = DT / PPR, NPASS = NB / RPP;
-    const int pc = tid % PPR, r0 = tid / PPR;
-    vT v[NPASS];
-#pragma unroll
-    for (int q = 0; q < NPASS; ++q) {
-      const int r = r0 + q * RPP;
-      if (pc * EPC <= (r | (DB - 1))) v[q] = *reinterpret_cast<const vT*>(Wb + (int64_t)r * a.ld + pc * EPC);
-    }
-#pragma unroll
-    for (int q = 0; q < NPASS; ++q) {
-      const int r = r0 + q * RPP;
-      if (pc * EPC <= (r | (DB - 1))) {
-#pragma unroll
-        for (int u = 0; u < EPC; ++u) A[aidx(r, pc * EPC + u)] = (double)v[q][u];
-      }
-    }
-  }
-  if (tid == 0) *flag = 0;
-  __syncthreads();
-  if (FUSE) {
-    // the whole block is in LDS (every load retired into the LDS stores above): draw the ticket
-    // tickets 0 .. grid - 1; the grid's last draw wraps the counter to 0 for the next launch
-    if (tid == 0) *ticket = (int)atomicInc(reinterpret_cast<unsigned*>(&a.ctr[b]), gridDim.x - 1u);
-    __syncthreads();
-  }
-  // FUSE: the last workgroup to load writes (alone, so its HBM stores never sit in front of a tile's
-  // solve); the others solve tile = ticket
-  const int tk = FUSE ? *ticket : 0;
-  const bool wr = !FUSE || tk == (int)gridDim.x - 1;
-  const int64_t R = a.row0 + (int64_t)tk * 64;
-  const bool live = FUSE && !wr && !panel_zero_rows(a, b, R, R + 64);
-
-  // FUSE: the panel rows' A operands (32 doubles per lane) are loaded in the last step -- waves 1..7 at its
-  // start, wave 0 after its potf2 -- so their latency hides under that step; the last step is peeled off
-  // the loop, so they are not live (and do not spill) through the earlier steps
-  bool fetched = false;
-  auto prefetch = [&]() {
-    if (!FUSE || !live) return;
-    const double* Ar = reinterpret_cast<const double*>(a.W) + (int64_t)b * a.w_bs +
-                       (R + (wave & 3) * DB + lr) * a.ld + a.j0 + 2 * lk;
-#pragma unroll
-    for (int kc = 0; kc < NTL; ++kc) {
-      pa[kc][0] = *reinterpret_cast<const dbl2*>(Ar + kc * DB);
-      pa[kc][1] = *reinterpret_cast<const dbl2*>(Ar + kc * DB + 8);
-    }
-    fetched = true;
-  };
-  d4 xs = {0.0, 0.0, 0.0, 0.0};  // wave 0: X_{s+1} (operand layout) from QR_s, stored in P_{s+1}
-  auto step = [&](int s, auto last) {
-    // ---------------------------------------------------------------- P_s
-    if (decltype(last)::value && wave != 0) prefetch();
-    if (wave == 0) {
-      if (s > 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) A[aidx(s * DB + lr, (s - 1) * DB + lk + 4 * q)] = xs[q];
-      }
-      if (!(a.dbg & 2)) potf2_tile(A, Dinv + s * DTS, colbuf, s, lane, flag, a.j0);  // timing ablation
-      if (decltype(last)::value) prefetch();
-    } else if (s == 0) {
-      if (!(a.dbg & 8) && wr) store_inv_zeros(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
-    } else {
-      const int w = wave - 1;
-      const int I = s - 1;
-      if (w < I && !(a.dbg & 1)) inverse_tile(A, Dinv, Ib, I, w, lr, lk, wr);
-      // trailing update of step s - 1 for tile columns j >= s + 1 (column s was done in QR_{s-1});
-      // the last waves take the first tiles (waves 1..I hold an inverse tile)
-      const int m = NTL - 1 - s;
-      const int ntri = m * (m + 1) / 2;
-      for (int t = (NTL - 2) - w; t < ((a.dbg & 4) ? 0 : ntri); t += NTL - 1) {
-        int ti = 0;
-        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-        const int tj = t - ti * (ti + 1) / 2;
-        const int i = s + 1 + ti, j = s + 1 + tj;
-        d4 acc;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = A[aidx(i * DB + lk + 4 * q, j * DB + lr)];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          acc = mfma64(-A[aidx(i * DB + lr, (s - 1) * DB + 4 * k + lk)],
-                       A[aidx(j * DB + lr, (s - 1) * DB + 4 * k + lk)], acc);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) A[aidx(i * DB + lk + 4 * q, j * DB + lr)] = acc[q];
-      }
-      if (!(a.dbg & 8) && wr) {
-        store_l_rows(A, Wb, a.ld, I, tid - 64, DT - 64);
-        store_inv_diag(Dinv, Ib, I, tid - 64, DT - 64);
-      }
-    }
-    __syncthreads();
-    // ---------------------------------------------------------------- QR_s
-    xs = d4{0.0, 0.0, 0.0, 0.0};  // (the old value is dead: nothing keeps it alive across potf2)
-    if (s < NTL - 1 && wave < NTL - 1 - s && !(a.dbg & 4)) {
-      const int i = s + 1 + wave;
-      const double* Dk = Dinv + s * DTS;
-      d4 xi = {0.0, 0.0, 0.0, 0.0}, x1 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double dv = Dk[lr * DBS + 4 * k + lk];
-        xi = mfma64(dv, A[aidx(i * DB + lr, s * DB + 4 * k + lk)], xi);
-        if (wave != 0) x1 = mfma64(dv, A[aidx((s + 1) * DB + lr, s * DB + 4 * k + lk)], x1);
-      }
-      if (wave == 0) x1 = xi;
-      // xi[q] = X_i[lr][lk + 4q]: the A operand of k-step q; x1 likewise the B operand
-      d4 acc;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = A[aidx(i * DB + lk + 4 * q, (s + 1) * DB + lr)];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc = mfma64(-xi[q], x1[q], acc);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) A[aidx(i * DB + lk + 4 * q, (s + 1) * DB + lr)] = acc[q];
-      xs = xi;  // wave 0: tile (s + 1, s) is read by every wave of this phase, stored in P_{s+1}
-      if (wave != 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) A[aidx(i * DB + lr, s * DB + lk + 4 * q)] = xi[q];
-      }
-    }
-    __syncthreads();
-    };
-  const int nsteps = (a.dbg & 16) ? 0 : NTL;
-#pragma unroll 1
-  for (int s = 0; s + 1 < nsteps; ++s) step(s, std::false_type());
-  if (nsteps > 0) step(nsteps - 1, std::integral_constant<bool, FUSE>());
-  // after P_7: block row 7 of L to HBM, rows 6 and 7 of L^-1
-  if (a.dbg & 32) return;  // timing ablation
-  if (!fetched) prefetch();  // (only when the step loop was ablated away)
-  if (wave >= 1) {
-    inverse_tile(A, Dinv, Ib, NTL - 1, wave - 1, lr, lk, wr);
-  } else if (wr) {
-    store_inv_diag(Dinv, Ib, NTL - 1, lane, 64);
-  }
-  if (wr) {
-    store_l_rows(A, Wb, a.ld, NTL - 1, tid, DT);
-    if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
-  }
-  if (!FUSE) return;
-  __syncthreads();  // block row 7 of L^-1 in LDS
-  if (!live) return;
-  // Linv[c][k] (c in tile I, k in tile J <= I): tile (J, I) of A transposed for J < I, Dinv_I for J = I
-  const int rb = wave & 3, ch = wave >> 2;
-  double* Xr = reinterpret_cast<double*>(a.W) + (int64_t)b * a.w_bs + (R + rb * DB + lk) * a.ld + a.j0 + lr;
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    // column block = tile row I of L^-1; block cb takes cb + 1 chunks, so the halves {0, 7, 2, 5} and
-    // {1, 6, 3, 4} carry 18 chunks each (contiguous halves: 10 and 26)
-    const int cb = (n & 1) ? 7 - 2 * (n >> 1) - ch : 2 * (n >> 1) + ch;
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kc = 0; kc < NTL; ++kc) {
-      if (kc > cb) break;
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int x = 2 * lk + 8 * (st >> 1) + (st & 1);  // k within the chunk
-        const double bv = (kc < cb) ? A[aidx(kc * DB + x, cb * DB + lr)] : Dinv[cb * DTS + lr * DBS + x];
-        acc = mfma64(pa[kc][st >> 1][st & 1], bv, acc);
-      }
-    }
-    // C/D layout: col = lr, row = lk + 4 q
-#pragma unroll
-    for (int q = 0; q < 4; ++q) Xr[(int64_t)(4 * q) * a.ld + cb * DB] = acc[q];
-  }
+  diag2_body<T, FUSE, SC1>(a, (int)blockIdx.x, sm);
 }
 
 }  // namespace
@@ -569,7 +180,16 @@ hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t 
     if (e != hipSuccess) return e;
     done = true;
   }
-  if (fuse) {
+  if (a.version == 3 && dtype == GPK_F64 && !fuse) {  // debugging: the write-through (chain_kernel) variant
+    static bool sc1_done = false;
+    if (!sc1_done) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(diag2_kernel<double, false, true>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)DIAG_LDS_BYTES);
+      if (e != hipSuccess) return e;
+      sc1_done = true;
+    }
+    hipLaunchKernelGGL((diag2_kernel<double, false, true>), dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
+  } else if (fuse) {
     hipLaunchKernelGGL((diag2_kernel<double, true>), dim3(a.trsm_tiles + 1, batch), dim3(DT), DIAG_LDS_BYTES, s, a);
   } else if (v2) {
     if (dtype == GPK_F64)

@@ -120,6 +120,25 @@ struct DiagArgs {
   int32_t* ctr;
 };
 
+// persistent factorisation (gpk_potrf.hip chain_kernel): one f64 member, tasks in host-computed order
+struct ChainArgs {
+  double* W;
+  int64_t ld;
+  double* Winv;
+  int32_t* info;
+  const int32_t* tasks;  // [ntasks][4]: type (0 D, 1 S, 2 U32, 3 BLK), panel, slice / block row, block column
+  int32_t ntasks;
+  int32_t* ctl;          // [0] claim counter, [1] timeout flag
+  int32_t* dflag;        // [nblk]: D(k) done
+  int32_t* sdone;        // [nblk][nsl]: S(k, r) done
+  int32_t* ucnt;         // [nsl][nbc]: panels applied to slice r of block column j
+  int32_t nsl, nbc;      // live 32-row slices (the last one holds the y row), live block columns
+  int64_t row_end;       // y_row + 1: rows below are zero
+  int64_t timeout;       // per wait, in s_memrealtime ticks (100 MHz)
+  int32_t* trace;        // debugging (GPK_CHAIN_TRACE=1, else NULL): host-visible [grid][32] progress words
+  int32_t dbg;           // debugging (GPK_CHAIN_DBG): 1 = the diagonal task through the plain-load/store body
+};
+
 struct FinArgs {
   const void* W;
   int64_t ld;
@@ -183,6 +202,7 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s);
 hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream_t s);
+hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s);
 hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_t batch, hipStream_t s);
 size_t vjp_workspace_elems(const gpk_kdesc& kd, int64_t n, int64_t m, int32_t d, bool want_z);
 hipError_t launch_vjp(const gpk_kdesc& kd, const VjpArgs& g, const double* X, int64_t n, const double* Z, int64_t m,

@@ -17,6 +17,7 @@
 // consecutive tiles, which share panel rows in its L2 (xcd_remap).
 #include <math.h>
 
+#include "gpk_diag_dev.h"
 #include "gpk_internal.h"
 #include "gpk_kernels.h"
 
@@ -618,6 +619,344 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
   return hipGetLastError();
 }
 
+
+// ================================================================================ persistent factorisation
+// chain_kernel: the whole blocked factorisation of ONE augmented matrix (f64) in one launch.  Its
+// workgroups (one per CU: the diagonal-block task needs the 150 KB of LDS) claim tasks from a list in
+// the order the host computed by list-scheduling the task graph (a topological order, so every task
+// waits only for tasks claimed before it: the launch finishes whatever the residency), wait for their
+// inputs on per-task counters, and publish their outputs with write-through stores.  Tasks (block =
+// 128 rows / columns, slice = 32 rows, panel k = block column k):
+//   D(k)          diagonal block k, the diag2 body (factor + inverse) on the block as the earlier tasks
+//                 left it; L_kk to W, L_kk^-1 to Winv; dflag[k]
+//   S(k, r)       slice r below block k: X = A(r, k) L_kk^-T, in place; sdone[k][r]
+//   U32(q, r, j)  slice r of block column j = q + 1: C -= X(r, q) X(j, q)^T; ucnt[r][j] = q + 1
+//   BLK(q, i, j)  128 x 128 tile (i, j), j >= q + 2: C -= X(i, q) X(j, q)^T (the trailing update of the
+//                 launch path, one panel deep); ucnt[r][j] = q + 1 for the slices r of block i
+// The chain D(k) -> S(k, block k + 1) -> U32(k, block k + 1, k + 1) -> D(k + 1) runs on slices spread
+// over CUs (a 128-row panel solve or update on one CU would take ~14 us of f64 MFMA), the BLK tiles of
+// older panels fill the rest of the chip -- the look-ahead that launches cannot give a single
+// evaluation (persistent factorisation).  Hand-offs (MI355X guide, inter-workgroup
+// visibility): every byte of W / Winv that a task writes is stored sc1 (write-through) and, after every
+// storing wave's vmcnt(0) and a barrier, one lane sets the counter; D, S and U32 read W / Winv with
+// sc1 loads only, BLK (LDS-DMA staging) behind one agent acquire.  Every wait is bounded: on timeout
+// the task sets ctl[1] and info = -1 and every workgroup drains the list without work.
+enum { CH_D = 0, CH_S = 1, CH_U32 = 2, CH_BLK = 3 };
+constexpr int CHAIN_SLOT_OFF = (int)((DIAG_LDS_BYTES + 15) / 16 * 16);
+constexpr size_t CHAIN_LDS_BYTES = CHAIN_SLOT_OFF + 16;
+
+__device__ __forceinline__ int32_t ld_flag(const int32_t* p) {
+  return __hip_atomic_load((gi32*)const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(int32_t* p, int32_t v) {
+  __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane: wait until *p >= v; false on timeout (which it reports) or after another task's timeout
+__device__ bool chain_wait(const ChainArgs& a, const int32_t* p, int32_t v, uint64_t t0) {
+  while (ld_flag(p) < v) {
+    if (ld_flag(a.ctl + 1) != 0) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout) {
+      st_flag(a.ctl + 1, 1);
+      int32_t zero = 0;
+      __hip_atomic_compare_exchange_strong((gi32*)a.info, &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+// C[32 x 128] = A[32 x 128] B^T (SUB false) or C -= A B^T (SUB true), B [128 x 128]; A, C with row
+// stride ld, B with ldb; every load and store sc1.  Wave w: 16-row block w & 1, 16-column blocks
+// 2 (w >> 1) and 2 (w >> 1) + 1; K permuted so that lane group q takes k = 32 q + 16 h + s (h, s the half
+// and k-step): each lane reads contiguous 16-B pieces of its rows.  diag_off >= 0: the slice is rows
+// diag_off .. +31 of the block whose columns C covers -- column blocks right of each row block's
+// diagonal block are neither computed nor stored.  C may alias A (the panel solve, in place): the
+// stores wait for every wave's reads at a barrier.
+template <bool SUB>
+__device__ __forceinline__ void slab_gemm(const double* A, const double* B, int64_t ldb, double* C, int64_t ld,
+                                          int diag_off) {
+  typedef double dbl2 __attribute__((ext_vector_type(2)));
+  const int lane = threadIdx.x & 63;
+  const int w = wave_uniform((int)threadIdx.x >> 6);
+  const int lr = lane & 15, q = lane >> 4;
+  const int rb = w & 1, cb0 = 2 * (w >> 1);
+  const int cb_last = diag_off < 0 ? 7 : (diag_off >> 4) + rb;
+  const bool live0 = cb0 <= cb_last, live1 = cb0 + 1 <= cb_last;
+  const double* Ar = A + (int64_t)(rb * 16 + lr) * ld + 32 * q;
+  const double* Br = B + (int64_t)(cb0 * 16 + lr) * ldb + 32 * q;
+  double* Cr = C + (int64_t)(rb * 16 + q) * ld + cb0 * 16 + lr;  // C/D layout: row q + 4 i, column lr
+  d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  if (SUB) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (live0) acc0[i] = __builtin_bit_cast(double, (uint64_t)__hip_atomic_load(
+                               (gu64*)(Cr + 4 * i * ld), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (live1) acc1[i] = __builtin_bit_cast(double, (uint64_t)__hip_atomic_load(
+                               (gu64*)(Cr + 4 * i * ld + 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    dbl2 av[8], b0[8], b1[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      av[s] = ldv<true, double>(Ar + 16 * h + 2 * s);
+      if (live0) b0[s] = ldv<true, double>(Br + 16 * h + 2 * s);
+      if (live1) b1[s] = ldv<true, double>(Br + 16 * ldb + 16 * h + 2 * s);
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const double a = av[s >> 1][s & 1];
+      if (live0) acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b0[s >> 1][s & 1], acc0, 0, 0, SUB ? 1 : 0);
+      if (live1) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1[s >> 1][s & 1], acc1, 0, 0, SUB ? 1 : 0);
+    }
+  }
+  __syncthreads();  // in place (S): every wave's A reads are done before the first store
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (live0) sts<true>(Cr + 4 * i * ld, acc0[i]);
+    if (live1) sts<true>(Cr + 4 * i * ld + 16, acc1[i]);
+  }
+}
+
+// BLK: C(R.., Cc..) -= A(R.., Kc..) B(Cc.., Kc..)^T on a 128 x 128 tile, K = 128: gemm_kernel's f64
+// update (8 waves of 64 x 32, LDS-DMA staging of 16-deep chunks in two stages, C first, the next chunk's
+// DMA after the first half of the MFMAs) with write-through C stores.  Rows >= row_end are zero.
+__device__ __noinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64_t Cc, int64_t Kc, int64_t row_end,
+                                         char* smem) {
+  constexpr int TM = 128, TN = 128, WN = 4, WM = 2, NW = 8, MB = 4, NBK = 2, EPC = 2, GBK = 16, KS = 4;
+  constexpr int STAGE = (TM + TN) * ROWB;
+  constexpr int PW = (TM + TN) / (8 * NW);
+  constexpr int NK = NB / GBK;
+  typedef double vec_t __attribute__((ext_vector_type(2)));
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = wave_uniform(tid >> 6);
+  const int wr = wid / WN, wc = wid % WN;
+  const double* Ag = W + R * ld + Kc;
+  const double* Bg = W + Cc * ld + Kc;
+  const double* src[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int g0 = (wid * PW + i) * 8;
+    const int r = g0 + (lane >> 3);
+    src[i] = (g0 < TM) ? Ag + (int64_t)r * ld + swz(r, lane & 7) * EPC
+                       : Bg + (int64_t)(r - TM) * ld + swz(r - TM, lane & 7) * EPC;
+  }
+  double* const C = W + R * ld + Cc;
+  const uint64_t cu = reinterpret_cast<uint64_t>(C);
+  const uint64_t cuu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(cu >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cu);
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(cuu), 0, (int)(TM * ld * (int64_t)sizeof(double)), 0x00020000);
+  const int col = lane & 15;
+  const int cvo = (int)(((int64_t)(wr * (TM / WM) + Mfma<double>::row(lane, 0)) * ld + wc * (TN / WN) + col) *
+                        (int64_t)sizeof(double));
+  const int ldb_s = wave_uniform((int)(ld * (int64_t)sizeof(double)));
+#define GPK_CH_CSOFF(m, n, r) (((m) * 16 + (r) * 4) * ldb_s + (n) * 16 * (int)sizeof(double))
+  d4 acc[MB][NBK];
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < NBK; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[m][n][r] = BufIO<double>::load(crs, cvo, GPK_CH_CSOFF(m, n, r));
+  const int q = lane >> 4, lr = lane & 15;
+  const int aoff = (wr * (TM / WM) + lr) * ROWB;
+  const int boff = (TM + wc * (TN / WN) + lr) * ROWB;
+  const int p0 = swz(lr, q) * 16, p1 = swz(lr, q + 4) * 16;
+#define GPK_CH_GLDS(stage, kc)                                                                   \
+  {                                                                                              \
+    _Pragma("unroll") for (int i = 0; i < PW; ++i)                                               \
+        glds16(src[i] + (int64_t)(kc) * GBK, smem + (stage) * STAGE + (wid * PW + i) * 1024);      \
+  }
+  GPK_CH_GLDS(0, 0);
+  const int64_t wrow0 = R + wr * (TM / WM);
+  const int mact = row_end <= wrow0 ? 0 : ((row_end - wrow0 + 15) / 16 < MB ? (int)((row_end - wrow0 + 15) / 16) : MB);
+#define GPK_CH_STEPS(S0, S1, MLIM)                                                                 \
+  _Pragma("unroll") for (int s = (S0); s < (S1); ++s)                                              \
+  _Pragma("unroll") for (int n = 0; n < NBK; ++n)                                                  \
+  _Pragma("unroll") for (int m = 0; m < (MLIM); ++m)                                               \
+    acc[m][n] = Mfma<double>::op_neg(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]);
+#define GPK_CH_KLOOP(MLIM)                                                                         \
+  for (int kc = 0; kc < NK; ++kc) {                                                                \
+    const int st = kc & 1;                                                                         \
+    __builtin_amdgcn_s_waitcnt(0x0F70);                                                            \
+    __syncthreads();                                                                               \
+    if ((MLIM) > 0) {                                                                              \
+      const char* sb = smem + st * STAGE;                                                          \
+      vec_t fa[MB][2], fb[NBK][2];                                                                 \
+      _Pragma("unroll") for (int h = 0; h < 2; ++h) {                                              \
+        fa[0][h] = *reinterpret_cast<const vec_t*>(sb + aoff + (h ? p1 : p0));                     \
+        _Pragma("unroll") for (int n = 0; n < NBK; ++n)                                            \
+          fb[n][h] = *reinterpret_cast<const vec_t*>(sb + boff + n * 16 * ROWB + (h ? p1 : p0));   \
+        _Pragma("unroll") for (int m = 1; m < (MLIM); ++m)                                         \
+          fa[m][h] = *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + (h ? p1 : p0));   \
+      }                                                                                            \
+      GPK_CH_STEPS(0, KS / 2, MLIM)                                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                           \
+      if (kc + 1 < NK) GPK_CH_GLDS(st ^ 1, kc + 1);                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                           \
+      GPK_CH_STEPS(KS / 2, KS, MLIM)                                                               \
+    } else if (kc + 1 < NK) {                                                                      \
+      GPK_CH_GLDS(st ^ 1, kc + 1);                                                                 \
+    }                                                                                              \
+  }
+  if (mact > 1) {
+    GPK_CH_KLOOP(MB)
+  } else if (mact == 1) {
+    GPK_CH_KLOOP(1)
+  } else {
+    GPK_CH_KLOOP(0)
+  }
+#undef GPK_CH_KLOOP
+#undef GPK_CH_STEPS
+#undef GPK_CH_GLDS
+  typedef decltype(__builtin_amdgcn_raw_buffer_load_b64(__amdgpu_buffer_rsrc_t(), 0, 0, 0)) raw64_t;
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < NBK; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(raw64_t, acc[m][n][r]), crs, cvo,
+                                              GPK_CH_CSOFF(m, n, r), 16 /* sc1: write-through */);
+#undef GPK_CH_CSOFF
+}
+
+// The task bodies are separate (not inlined) functions: each gets its own register allocation, so the
+// diagonal-block body's 250 VGPRs do not force the others -- or the claim loop -- to spill.
+__device__ __noinline__ void chain_d(const ChainArgs& a, int k, double* sm) {
+  DiagArgs da{};
+  da.W = a.W;
+  da.ld = a.ld;
+  da.Winv = a.Winv;
+  da.j0 = (int64_t)k * NB;
+  da.kblk = k;
+  da.info = a.info;
+  da.version = 2;
+  da.ctr = a.trace ? a.trace + 32 * blockIdx.x + 16 : nullptr;  // debugging: per-wave progress
+  if (a.dbg == 1)
+    diag2_body<double, false, false>(da, 0, sm);
+  else
+    diag2_body<double, false, true>(da, 0, sm);
+}
+__device__ __forceinline__ void chain_d_inl(const ChainArgs& a, int k, double* sm) {  // (debugging: GPK_CHAIN_DBG=2)
+  DiagArgs da{};
+  da.W = a.W;
+  da.ld = a.ld;
+  da.Winv = a.Winv;
+  da.j0 = (int64_t)k * NB;
+  da.kblk = k;
+  da.info = a.info;
+  da.version = 2;
+  da.ctr = a.trace ? a.trace + 32 * blockIdx.x + 16 : nullptr;
+  diag2_body<double, false, true>(da, 0, sm);
+}
+__device__ __noinline__ void chain_s(const ChainArgs& a, int k, int r) {
+  double* X = a.W + (int64_t)r * 32 * a.ld + (int64_t)k * NB;
+  slab_gemm<false>(X, a.Winv + (int64_t)k * NB * NB, NB, X, a.ld, -1);
+}
+__device__ __noinline__ void chain_u32(const ChainArgs& a, int q, int r, int j) {
+  const int64_t R = (int64_t)r * 32;
+  const int64_t J = (int64_t)j * NB;
+  slab_gemm<true>(a.W + R * a.ld + (int64_t)q * NB, a.W + J * a.ld + (int64_t)q * NB, a.ld, a.W + R * a.ld + J, a.ld,
+                  (R >= J && R < J + NB) ? (int)(R - J) : -1);
+}
+
+__device__ __forceinline__ void chain_trace(const ChainArgs& a, int slot, int v) {
+  if (a.trace) __hip_atomic_store(a.trace + 32 * blockIdx.x + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  int32_t* slot = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(sm) + CHAIN_SLOT_OFF);
+  const int tid = threadIdx.x;
+  for (;;) {
+    if (tid == 0) {
+      int t = __hip_atomic_fetch_add((gi32*)a.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t < a.ntasks && ld_flag(a.ctl + 1) != 0) t = a.ntasks;  // a wait timed out: drain
+      slot[0] = t;
+      chain_trace(a, 0, t);
+      chain_trace(a, 1, 1);
+    }
+    __syncthreads();
+    // the task and its fields as wave-uniform (SGPR) values: every branch on them is uniform, so the task
+    // bodies -- the diagonal block's barriers included -- sit in uniform control flow as in their own launches
+    const int t = __builtin_amdgcn_readfirstlane(slot[0]);
+    if (t >= a.ntasks) break;
+    const int ty = __builtin_amdgcn_readfirstlane(a.tasks[4 * t]);
+    const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
+    const int r = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 2]);
+    const int j = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 3]);
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      bool ok = true;
+      if (ty == CH_D) {
+        if (k > 0)
+          for (int s = 4 * k; s <= 4 * k + 3 && ok; ++s) ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + k, k, t0);
+      } else if (ty == CH_S) {
+        ok = chain_wait(a, a.dflag + k, 1, t0);
+        if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + k, k, t0);
+      } else if (ty == CH_U32) {
+        const int32_t* sd = a.sdone + (int64_t)k * a.nsl;
+        ok = chain_wait(a, sd + r, 1, t0);
+        for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+        if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + j, k, t0);
+      } else {
+        const int32_t* sd = a.sdone + (int64_t)k * a.nsl;
+        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+        for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok && k > 0; ++s)
+          ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + j, k, t0);
+        if (ok) {  // BLK stages through plain LDS-DMA / buffer loads: one agent acquire for them
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      slot[1] = ok ? 1 : 0;
+      chain_trace(a, 1, ok ? 2 : -2);
+    }
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
+    if ((tid & 63) == 0) chain_trace(a, 2 + (tid >> 6), 1);
+    if (ty == CH_D) {
+      if (a.dbg == 2)
+        chain_d_inl(a, k, sm);
+      else
+        chain_d(a, k, sm);
+    } else if (ty == CH_S) {
+      chain_s(a, k, r);
+    } else if (ty == CH_U32) {
+      chain_u32(a, k, r, j);
+    } else {
+      blk_tile(a.W, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, a.row_end, reinterpret_cast<char*>(sm));
+    }
+    // publish: every storing wave drains its stores, then one lane sets the counter
+    if (tid == 0) chain_trace(a, 1, 3);
+    if ((tid & 63) == 0) chain_trace(a, 2 + (tid >> 6), 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if ((tid & 63) == 0) chain_trace(a, 2 + (tid >> 6), 3);
+    if (tid == 0) {
+      chain_trace(a, 1, 4);
+      if (ty == CH_D) {
+        st_flag(a.dflag + k, 1);
+      } else if (ty == CH_S) {
+        st_flag(a.sdone + (int64_t)k * a.nsl + r, 1);
+      } else if (ty == CH_U32) {
+        st_flag(a.ucnt + (int64_t)r * a.nbc + j, k + 1);
+      } else {
+        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl; ++s) st_flag(a.ucnt + (int64_t)s * a.nbc + j, k + 1);
+      }
+    }
+  }
+  if (tid == 0) chain_trace(a, 1, 9);
+}
+
 }  // namespace
 
 #ifndef GPK_TRSM_WN
@@ -687,6 +1026,34 @@ hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipSt
     hipLaunchKernelGGL(trsv_update_kernel<double>, grid, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(trsv_update_kernel<float>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(DT) void chain_d_only_kernel(ChainArgs a) {  // (debugging: GPK_CHAIN_DBG=4)
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  chain_d(a, 0, sm);
+}
+
+hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {
+  if (a.dbg == 4) {
+    static bool d4 = false;
+    if (!d4) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(chain_d_only_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS_BYTES);
+      if (e != hipSuccess) return e;
+      d4 = true;
+    }
+    hipLaunchKernelGGL(chain_d_only_kernel, dim3(1), dim3(DT), CHAIN_LDS_BYTES, s, a);
+    return hipGetLastError();
+  }
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(chain_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_done = true;
+  }
+  hipLaunchKernelGGL(chain_kernel, dim3(grid), dim3(DT), CHAIN_LDS_BYTES, s, a);
   return hipGetLastError();
 }
 

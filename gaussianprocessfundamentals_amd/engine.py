@@ -280,6 +280,9 @@ class AugmentedFactorization:
         info = self.info.cpu()
         bad = torch.nonzero(info).flatten()
         if bad.numel():
+            if int(info[bad[0]]) < 0:
+                raise RuntimeError("device factorisation aborted: a wait of the persistent factorisation timed "
+                                   "out (gpk_tune chain_timeout_ms)")
             raise CholeskyError(int(info[bad[0]]))
 
 

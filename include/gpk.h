@@ -395,6 +395,14 @@ int gpk_timing_reset(void);
  * key).  Defaults come from the environment (GPK_LOOKAHEAD, GPK_RESERVE_CUS, ...). */
 int gpk_tune(const char* key, int64_t value, int64_t* old);
 
+/* The task list of the persistent single-member factorisation (gpk_tune "chain"; no reference
+ * counterpart): the order in which the workgroups of its one launch claim the tasks, for an augmented
+ * matrix with n_pad training rows, the y row at y_row and `grid` workgroups.  Four int32 per task:
+ * type (0: factor diagonal block k; 1: solve 32-row slice r below block k; 2: slice r of block column
+ * j = k + 1 -= panel k; 3: 128 x 128 tile (r, j) -= panel k), k, r, j.  Host only (no device call):
+ * tasks_out may be NULL to query *ntasks; cap = its capacity in tasks. */
+int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_out, int64_t cap, int64_t* ntasks);
+
 #ifdef __cplusplus
 }
 #endif

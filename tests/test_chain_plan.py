@@ -1,0 +1,203 @@
+"""Host-side checks of the persistent single-member factorisation's task list (gpk_chain_plan; no GPU).
+
+chain_kernel (gaussianprocessfundamentals_amd/csrc/gpk_potrf.hip) claims the tasks in list order and each task
+waits on counters before it runs.  Here, for several augmented shapes and worker counts:
+  * the waits are restated exactly as the kernel makes them, and an event simulation with random task
+    durations checks that every wait is satisfied by a task claimed EARLIER (no deadlock whatever the
+    residency) and that, at its start, every 32 x 128 cell a task reads or rewrites already holds the
+    last version written by the earlier-claimed tasks (the waits cover every data dependency);
+  * the tasks, run in list order on the augmented matrix in numpy, reproduce the blocked factorisation's
+    results -- L, z = L^-1 y, the Schur-complement corner (-z^T z, -mu, Sigma) -- against numpy's
+    Cholesky of K + noise I (the quantities of gpbasics/Statistics/CovarianceMatrix.py:247-265 and
+    Metrics/LogLikelihood.py:30-65).
+"""
+import numpy as np
+import pytest
+
+from gaussianprocessfundamentals_amd import _native as nat
+
+NB, SL = 128, 32
+D, S, U32, BLK = 0, 1, 2, 3
+
+
+def _lib_or_skip():
+    try:
+        nat.load_library()
+    except nat.NativeUnavailable as e:  # pragma: no cover - the build check builds it
+        pytest.skip(str(e))
+
+
+def shape(n, m):
+    n_pad = -(-n // NB) * NB
+    y_row = n_pad + m
+    p = -(-(y_row + 1) // NB) * NB
+    return n_pad, y_row, p
+
+
+def cells(task, nsl):
+    """(reads, writes) of a task as sets of (slice, block column) cells plus ('inv', k)."""
+    ty, k, r, j = (int(v) for v in task)
+
+    def sl(b):
+        return [s for s in range(4 * b, 4 * b + 4) if s < nsl]
+
+    if ty == D:
+        c = {(s, k) for s in sl(k)}
+        return c, c | {("inv", k)}
+    if ty == S:
+        return {(r, k), ("inv", k)}, {(r, k)}
+    if ty == U32:
+        return {(r, k), (r, j)} | {(s, k) for s in sl(j)}, {(r, j)}
+    rd = {(s, k) for s in sl(r) + sl(j)} | {(s, j) for s in sl(r)}
+    return rd, {(s, j) for s in sl(r)}
+
+
+def waits(task, nsl):
+    """The kernel's waits (chain_kernel, dependency section): (counter, index, value >= )."""
+    ty, k, r, j = (int(v) for v in task)
+    out = []
+    if ty == D:
+        if k > 0:
+            out += [("ucnt", (s, k), k) for s in range(4 * k, 4 * k + 4)]
+    elif ty == S:
+        out.append(("dflag", k, 1))
+        if k > 0:
+            out.append(("ucnt", (r, k), k))
+    elif ty == U32:
+        out.append(("sdone", (k, r), 1))
+        out += [("sdone", (k, s), 1) for s in range(4 * j, 4 * j + 4) if s < nsl]
+        if k > 0:
+            out.append(("ucnt", (r, j), k))
+    else:
+        out += [("sdone", (k, s), 1) for s in range(4 * r, 4 * r + 4) if s < nsl]
+        out += [("sdone", (k, s), 1) for s in range(4 * j, 4 * j + 4) if s < nsl]
+        if k > 0:
+            out += [("ucnt", (s, j), k) for s in range(4 * r, 4 * r + 4) if s < nsl]
+    return out
+
+
+def publishes(task, nsl):
+    ty, k, r, j = (int(v) for v in task)
+    if ty == D:
+        return [("dflag", k, 1)]
+    if ty == S:
+        return [("sdone", (k, r), 1)]
+    if ty == U32:
+        return [("ucnt", (r, j), k + 1)]
+    return [("ucnt", (s, j), k + 1) for s in range(4 * r, 4 * r + 4) if s < nsl]
+
+
+def simulate(tasks, nsl, workers, rng):
+    """Claim in list order; start = max(worker free, every wait's publish time); check cell versions."""
+    pub = {}           # (counter, index) -> list of (value, time)
+    last_w = {}        # cell -> finish time of the last earlier-claimed writer
+    readers = {}       # cell -> finish times of earlier-claimed readers since that writer
+    free = [0.0] * workers
+    dur = {D: 28.0, S: 7.0, U32: 7.0, BLK: 18.0}
+    for t, task in enumerate(tasks):
+        w = int(np.argmin(free))
+        start = free[w]
+        for cnt, idx, v in waits(task, nsl):
+            hits = [tm for (val, tm) in pub.get((cnt, idx), []) if val >= v]
+            assert hits, "task %d %s waits on %s%s >= %d, set by no earlier task" % (t, task, cnt, idx, v)
+            start = max(start, min(hits))
+        rd, wr = cells(task, nsl)
+        for c in rd | wr:  # read-after-write / write-after-write: the last writer is done
+            assert start >= last_w.get(c, 0.0), "task %d %s starts before the last writer of %s" % (t, task, c)
+        finish = start + dur[int(task[0])] * rng.uniform(0.3, 3.0)
+        for c in wr:  # write-after-read: earlier readers of the old version are done
+            assert all(f <= finish for f in readers.get(c, [])), "task %d %s overwrites %s under a reader" % (
+                t, task, c)
+        for c in rd - wr:
+            readers.setdefault(c, []).append(finish)
+        for c in wr:
+            last_w[c] = finish
+            readers[c] = []
+        for cnt, idx, v in publishes(task, nsl):
+            pub.setdefault((cnt, idx), []).append((v, finish))
+        free[w] = finish
+
+
+def augmented(n, m, rng):
+    n_pad, y_row, p = shape(n, m)
+    x = np.sort(rng.uniform(0, 1, n + m))
+    xt, xs = x[:n], x[n:]
+    k = lambda a, b: np.exp(-0.5 * (a[:, None] - b[None, :]) ** 2 / 0.1 ** 2)  # noqa: E731
+    noise = 1e-2
+    y = np.sin(6 * xt) + 0.1 * rng.standard_normal(n)
+    W = np.zeros((p, p))
+    W[:n, :n] = k(xt, xt) + noise * np.eye(n)
+    W[n:n_pad, n:n_pad] = np.eye(n_pad - n)
+    if m:
+        W[n_pad:n_pad + m, :n] = k(xs, xt)
+        W[n_pad:n_pad + m, n_pad:n_pad + m] = k(xs, xs)
+    W[y_row, :n] = y
+    return np.tril(W), (xt, xs, y, noise, k)
+
+
+def run_tasks(W, tasks, nblk):
+    inv = {}
+    for ty, k, r, j in tasks:
+        K = slice(NB * k, NB * k + NB)
+        if ty == D:
+            a = np.tril(W[K, K])
+            L = np.linalg.cholesky(a + np.tril(a, -1).T)
+            W[K, K] = L
+            inv[k] = np.linalg.inv(L)
+        elif ty == S:
+            R = slice(SL * r, SL * r + SL)
+            W[R, K] = W[R, K] @ inv[k].T
+        elif ty == U32:
+            R, J = slice(SL * r, SL * r + SL), slice(NB * j, NB * j + NB)
+            W[R, J] -= W[R, K] @ W[J, K].T
+        else:
+            I, J = slice(NB * r, NB * r + NB), slice(NB * j, NB * j + NB)
+            W[I, J] -= W[I, K] @ W[J, K].T
+    return W
+
+
+@pytest.mark.parametrize("n,m", [(1, 0), (128, 0), (300, 0), (700, 37), (1000, 200), (2048, 0)])
+def test_chain_plan_waits_cover_every_dependency(n, m):
+    _lib_or_skip()
+    n_pad, y_row, p = shape(n, m)
+    nsl = y_row // SL + 1
+    rng = np.random.default_rng(n + m)
+    for grid in (1, 3, 16, 256):
+        tasks = nat.chain_plan(n_pad, y_row, grid)
+        nblk = n_pad // NB
+        kinds = np.bincount(tasks[:, 0], minlength=4)
+        assert kinds[D] == nblk
+        assert len({tuple(t) for t in tasks.tolist()}) == len(tasks)
+        for _ in range(3):
+            simulate(tasks, nsl, grid, rng)
+
+
+@pytest.mark.parametrize("n,m", [(200, 0), (600, 50), (1100, 0)])
+def test_chain_plan_reproduces_the_blocked_factorisation(n, m):
+    _lib_or_skip()
+    rng = np.random.default_rng(7)
+    n_pad, y_row, p = shape(n, m)
+    W0, (xt, xs, y, noise, k) = augmented(n, m, rng)
+    tasks = nat.chain_plan(n_pad, y_row, 64)
+    W = run_tasks(W0.copy(), tasks, n_pad // NB)
+    Kn = k(xt, xt) + noise * np.eye(n)
+    L = np.linalg.cholesky(Kn)
+    np.testing.assert_allclose(np.tril(W[:n, :n]), L, rtol=0, atol=1e-12)
+    z = np.linalg.solve(L, y)
+    np.testing.assert_allclose(W[y_row, :n], z, rtol=0, atol=1e-10)
+    assert W[y_row, y_row] == pytest.approx(-z @ z, rel=1e-12)
+    if m:
+        alpha = np.linalg.solve(Kn, y)
+        Ks = k(xs, xt)
+        np.testing.assert_allclose(-W[y_row, n_pad:n_pad + m], Ks @ alpha, rtol=0, atol=1e-9)
+        V = np.linalg.solve(L, Ks.T)
+        sig = k(xs, xs) - V.T @ V
+        np.testing.assert_allclose(np.diag(W[n_pad:n_pad + m, n_pad:n_pad + m]), np.diag(sig), rtol=0, atol=1e-9)
+
+
+def test_chain_plan_rejects_bad_shapes():
+    _lib_or_skip()
+    with pytest.raises(nat.GpkError):
+        nat.chain_plan(100, 100, 8)
+    with pytest.raises(nat.GpkError):
+        nat.chain_plan(128, 100, 8)
