@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--fuse-trsm", type=int, default=None,
                     help="panel solve inside the diagonal-block launch (libgpk fuse_trsm); default 0 when "
                          "--pipeline > 1, else the library default (1)")
+    ap.add_argument("--chain", type=int, default=None,
+                    help="single-member factorisations as one persistent launch (libgpk chain); default 0 when "
+                         "--pipeline > 1, else the library default")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="time without per-kernel HIP events")
@@ -431,6 +434,10 @@ def main():
     # workgroups take CUs from the other batches' updates: C5 at 3 in flight 38.2 -> 36.4 evals/s)
     if args.fuse_trsm is not None or P > 1:
         nat.tune("fuse_trsm", args.fuse_trsm if args.fuse_trsm is not None else 0)
+    # the persistent factorisation keeps one workgroup per CU for the whole evaluation: with P > 1
+    # batches in flight the launch path's kernels share the chip better
+    if args.chain is not None or P > 1:
+        nat.tune("chain", args.chain if args.chain is not None else 0)
     if grad_mode:
         facts = [engine.InverseFactorization(n, d, batch, dt) for _ in range(P)]
     else:

@@ -121,6 +121,7 @@ def _declare(lib):
         "gpk_syevd": (c_int, [c_int64, c_int32, P, c_int64, c_int64, P, P, P, c_size_t, P]),
         "gpk_chain_plan": (c_int, [c_int64, c_int64, c_int32, P, c_int64, POINTER(c_int64)]),
         "gpk_chain_trace": (c_int, [P, c_int64]),
+        "gpk_chain_times": (c_int, [P, c_int64]),
         "gpk_kernel_vjp_workspace_bytes": (c_size_t, [POINTER(GpkKdesc), c_int64, c_int64, c_int32, c_int32]),
         "gpk_kernel_vjp": (c_int, [POINTER(GpkKdesc), P, P, c_int64, P, c_int64, c_int32, P, c_int64, P, P, P, P,
                                    P, c_size_t, P]),

@@ -303,6 +303,8 @@ std::mutex g_chain_mu;
 std::map<std::tuple<int, int64_t, int64_t, int>, ChainPlan> g_chain_plans;
 std::map<std::pair<int, hipStream_t>, std::pair<int32_t*, size_t>> g_chain_ctl;
 int32_t* g_chain_trace = nullptr;  // GPK_CHAIN_TRACE=1: pinned host words the kernel writes its progress to
+uint64_t* g_chain_times = nullptr;  // GPK_CHAIN_TIMES=1: device stamps per task of the last profiled launch
+int64_t g_chain_times_n = 0;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
@@ -457,6 +459,15 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.nbc = plan.nbc;
   a.row_end = lay->y_row + 1;
   a.timeout = std::max<int64_t>(1, tn.chain_timeout_ms) * 100000;  // 100 MHz ticks
+  if (env_i64("GPK_CHAIN_TIMES", 0)) {
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    if (g_chain_times_n < a.ntasks) {
+      if (g_chain_times) hipFree(g_chain_times);
+      GPK_HIP(hipMalloc(&g_chain_times, (size_t)a.ntasks * 3 * sizeof(uint64_t)), "chain times");
+      g_chain_times_n = a.ntasks;
+    }
+    a.times = g_chain_times;
+  }
   if (env_i64("GPK_CHAIN_TRACE", 0)) {
     std::lock_guard<std::mutex> lk(g_chain_mu);
     if (!g_chain_trace) GPK_HIP(hipHostMalloc(&g_chain_trace, 4096 * 32 * sizeof(int32_t), hipHostMallocCoherent), "trace");
@@ -1666,6 +1677,13 @@ int gpk_timing_enable(int on) {
   std::lock_guard<std::mutex> lk(g_timing.mu);
   g_timing.on = on != 0;
   return 0;
+}
+
+// profiling: the per-task stamps of the last chain launch with GPK_CHAIN_TIMES=1 (synchronises the device)
+int gpk_chain_times(uint64_t* out, int64_t ntasks) {
+  if (!g_chain_times || !out || ntasks > g_chain_times_n) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return hipMemcpy(out, g_chain_times, (size_t)ntasks * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
 }
 
 // debugging: the progress words of the last traced chain launch (GPK_CHAIN_TRACE=1), host memory only

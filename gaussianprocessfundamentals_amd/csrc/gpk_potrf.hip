@@ -113,6 +113,10 @@ struct BufIO<double> {
   static __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t rs, int vo, int so, double v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(raw_t, v), rs, vo, so, 0);
   }
+  // write-through (sc1): stores another XCD reads inside the same launch (chain_kernel)
+  static __device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t rs, int vo, int so, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(raw_t, v), rs, vo, so, 16);
+  }
 };
 template <>
 struct BufIO<float> {
@@ -652,10 +656,11 @@ __device__ __forceinline__ void st_flag(int32_t* p, int32_t v) {
   __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one lane: wait until *p >= v; false on timeout (which it reports) or after another task's timeout
-__device__ bool chain_wait(const ChainArgs& a, const int32_t* p, int32_t v, uint64_t t0) {
-  while (ld_flag(p) < v) {
-    if (ld_flag(a.ctl + 1) != 0) return false;
+// wave 0: wait until *p >= v; false on timeout (which it reports) or after another task's timeout
+__device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p, int32_t v, uint64_t t0) {
+  // (polled values through readfirstlane: the loop is wave-uniform, as every branch of chain_kernel)
+  while (__builtin_amdgcn_readfirstlane(ld_flag(p)) < v) {
+    if (__builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) return false;
     if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout) {
       st_flag(a.ctl + 1, 1);
       int32_t zero = 0;
@@ -725,7 +730,7 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
 // BLK: C(R.., Cc..) -= A(R.., Kc..) B(Cc.., Kc..)^T on a 128 x 128 tile, K = 128: gemm_kernel's f64
 // update (8 waves of 64 x 32, LDS-DMA staging of 16-deep chunks in two stages, C first, the next chunk's
 // DMA after the first half of the MFMAs) with write-through C stores.  Rows >= row_end are zero.
-__device__ __noinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64_t Cc, int64_t Kc, int64_t row_end,
+__device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64_t Cc, int64_t Kc, int64_t row_end,
                                          char* smem) {
   constexpr int TM = 128, TN = 128, WN = 4, WM = 2, NW = 8, MB = 4, NBK = 2, EPC = 2, GBK = 16, KS = 4;
   constexpr int STAGE = (TM + TN) * ROWB;
@@ -815,55 +820,47 @@ __device__ __noinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64_t 
 #undef GPK_CH_KLOOP
 #undef GPK_CH_STEPS
 #undef GPK_CH_GLDS
-  typedef decltype(__builtin_amdgcn_raw_buffer_load_b64(__amdgpu_buffer_rsrc_t(), 0, 0, 0)) raw64_t;
+  // (through a double-typed parameter: __builtin_bit_cast of the vector element acc[m][n][r] itself
+  // compiled to four stores of element 0)
 #pragma unroll
   for (int m = 0; m < MB; ++m)
 #pragma unroll
     for (int n = 0; n < NBK; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(raw64_t, acc[m][n][r]), crs, cvo,
-                                              GPK_CH_CSOFF(m, n, r), 16 /* sc1: write-through */);
+      for (int r = 0; r < 4; ++r) BufIO<double>::store_sc1(crs, cvo, GPK_CH_CSOFF(m, n, r), acc[m][n][r]);
 #undef GPK_CH_CSOFF
 }
 
 // The task bodies are separate (not inlined) functions: each gets its own register allocation, so the
-// diagonal-block body's 250 VGPRs do not force the others -- or the claim loop -- to spill.
-__device__ __noinline__ void chain_d(const ChainArgs& a, int k, double* sm) {
+// diagonal-block body's 250 VGPRs do not force the others -- or the claim loop -- to spill.  They take
+// plain values, never the kernel argument by reference: its address taken, the kernel copies ChainArgs to
+// per-lane scratch and every field read becomes a VGPR load -- divergent for the compiler, which then
+// turned the claim loop's exit into an exec-mask-controlled loop whose barriers the waves no longer
+// executed the same number of times (the deadlock of the first versions).
+__device__ __noinline__ void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, int32_t* trace, int dbg, int k,
+                                    double* sm) {
   DiagArgs da{};
-  da.W = a.W;
-  da.ld = a.ld;
-  da.Winv = a.Winv;
+  da.W = W;
+  da.ld = ld;
+  da.Winv = Winv;
   da.j0 = (int64_t)k * NB;
   da.kblk = k;
-  da.info = a.info;
+  da.info = info;
   da.version = 2;
-  da.ctr = a.trace ? a.trace + 32 * blockIdx.x + 16 : nullptr;  // debugging: per-wave progress
-  if (a.dbg == 1)
+  da.ctr = trace ? trace + 32 * blockIdx.x + 16 : nullptr;  // debugging: per-wave progress
+  if (dbg == 1)
     diag2_body<double, false, false>(da, 0, sm);
   else
     diag2_body<double, false, true>(da, 0, sm);
 }
-__device__ __forceinline__ void chain_d_inl(const ChainArgs& a, int k, double* sm) {  // (debugging: GPK_CHAIN_DBG=2)
-  DiagArgs da{};
-  da.W = a.W;
-  da.ld = a.ld;
-  da.Winv = a.Winv;
-  da.j0 = (int64_t)k * NB;
-  da.kblk = k;
-  da.info = a.info;
-  da.version = 2;
-  da.ctr = a.trace ? a.trace + 32 * blockIdx.x + 16 : nullptr;
-  diag2_body<double, false, true>(da, 0, sm);
+__device__ __noinline__ void chain_s(double* W, int64_t ld, const double* Winv, int k, int r) {
+  double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
+  slab_gemm<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1);
 }
-__device__ __noinline__ void chain_s(const ChainArgs& a, int k, int r) {
-  double* X = a.W + (int64_t)r * 32 * a.ld + (int64_t)k * NB;
-  slab_gemm<false>(X, a.Winv + (int64_t)k * NB * NB, NB, X, a.ld, -1);
-}
-__device__ __noinline__ void chain_u32(const ChainArgs& a, int q, int r, int j) {
+__device__ __noinline__ void chain_u32(double* W, int64_t ld, int q, int r, int j) {
   const int64_t R = (int64_t)r * 32;
   const int64_t J = (int64_t)j * NB;
-  slab_gemm<true>(a.W + R * a.ld + (int64_t)q * NB, a.W + J * a.ld + (int64_t)q * NB, a.ld, a.W + R * a.ld + J, a.ld,
+  slab_gemm<true>(W + R * ld + (int64_t)q * NB, W + J * ld + (int64_t)q * NB, ld, W + R * ld + J, ld,
                   (R >= J && R < J + NB) ? (int)(R - J) : -1);
 }
 
@@ -871,78 +868,101 @@ __device__ __forceinline__ void chain_trace(const ChainArgs& a, int slot, int v)
   if (a.trace) __hip_atomic_store(a.trace + 32 * blockIdx.x + slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// One atomic add by lane 0 of the wave, without a lane-divergent branch: the claim loop below keeps every
+// branch wave-uniform.  (With "if (tid == 0) claim" the loop's exit became exec-mask controlled: wave 0
+// then ran the next iteration's barrier once with lane 0 masked off and once for lane 0 -- one barrier
+// more than the other waves -- and the workgroup deadlocked after its first task.)
+__device__ __forceinline__ int claim_ticket(int32_t* p) {
+  int v;
+  uint64_t saved;
+  const int one = 1;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "s_nop 1\n\t"
+      "global_atomic_add %0, %2, %3, off sc0\n\t"
+      "s_waitcnt vmcnt(0)\n\t"
+      "s_mov_b64 exec, %1\n\t"
+      "s_nop 1"
+      : "=&v"(v), "=&s"(saved)
+      : "v"(p), "v"(one)
+      : "memory");
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Wave 0 (all its lanes poll the same words: no lane-divergent branch) waits until the task's inputs are
+// published; false on timeout (reported) or after another task's timeout.
+__device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, int r, int j) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool ok = true;
+  if (ty == CH_D) {
+    if (k > 0)
+      for (int s = 4 * k; s <= 4 * k + 3 && ok; ++s) ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + k, k, t0);
+  } else if (ty == CH_S) {
+    ok = chain_wait(a, a.dflag + k, 1, t0);
+    if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + k, k, t0);
+  } else if (ty == CH_U32) {
+    const int32_t* sd = a.sdone + (int64_t)k * a.nsl;
+    ok = chain_wait(a, sd + r, 1, t0);
+    for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+    if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + j, k, t0);
+  } else {
+    const int32_t* sd = a.sdone + (int64_t)k * a.nsl;
+    for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+    for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+    for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok && k > 0; ++s)
+      ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + j, k, t0);
+    if (ok) {  // BLK stages through plain LDS-DMA / buffer loads: one agent acquire for them
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  return ok;
+}
+
 __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   int32_t* slot = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(sm) + CHAIN_SLOT_OFF);
-  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  // every branch of this loop is wave-uniform (wave; the task fields through readfirstlane)
   for (;;) {
-    if (tid == 0) {
-      int t = __hip_atomic_fetch_add((gi32*)a.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t < a.ntasks && ld_flag(a.ctl + 1) != 0) t = a.ntasks;  // a wait timed out: drain
+    if (wave == 0) {
+      int t = claim_ticket(a.ctl);
+      if (t < a.ntasks && __builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) t = a.ntasks;  // timed out
       slot[0] = t;
       chain_trace(a, 0, t);
-      chain_trace(a, 1, 1);
     }
     __syncthreads();
-    // the task and its fields as wave-uniform (SGPR) values: every branch on them is uniform, so the task
-    // bodies -- the diagonal block's barriers included -- sit in uniform control flow as in their own launches
     const int t = __builtin_amdgcn_readfirstlane(slot[0]);
     if (t >= a.ntasks) break;
     const int ty = __builtin_amdgcn_readfirstlane(a.tasks[4 * t]);
     const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
     const int r = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 2]);
     const int j = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 3]);
-    if (tid == 0) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      bool ok = true;
-      if (ty == CH_D) {
-        if (k > 0)
-          for (int s = 4 * k; s <= 4 * k + 3 && ok; ++s) ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + k, k, t0);
-      } else if (ty == CH_S) {
-        ok = chain_wait(a, a.dflag + k, 1, t0);
-        if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + k, k, t0);
-      } else if (ty == CH_U32) {
-        const int32_t* sd = a.sdone + (int64_t)k * a.nsl;
-        ok = chain_wait(a, sd + r, 1, t0);
-        for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
-        if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + j, k, t0);
-      } else {
-        const int32_t* sd = a.sdone + (int64_t)k * a.nsl;
-        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
-        for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
-        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok && k > 0; ++s)
-          ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + j, k, t0);
-        if (ok) {  // BLK stages through plain LDS-DMA / buffer loads: one agent acquire for them
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-      }
+    if (wave == 0) {
+      if (a.times) a.times[3 * t] = __builtin_amdgcn_s_memrealtime();
+      const bool ok = chain_deps(a, ty, k, r, j);
+      if (a.times) a.times[3 * t + 1] = __builtin_amdgcn_s_memrealtime();
       slot[1] = ok ? 1 : 0;
       chain_trace(a, 1, ok ? 2 : -2);
     }
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
-    if ((tid & 63) == 0) chain_trace(a, 2 + (tid >> 6), 1);
     if (ty == CH_D) {
-      if (a.dbg == 2)
-        chain_d_inl(a, k, sm);
-      else
-        chain_d(a, k, sm);
+      chain_d(a.W, a.ld, a.Winv, a.info, a.trace, a.dbg, k, sm);
     } else if (ty == CH_S) {
-      chain_s(a, k, r);
+      chain_s(a.W, a.ld, a.Winv, k, r);
     } else if (ty == CH_U32) {
-      chain_u32(a, k, r, j);
+      chain_u32(a.W, a.ld, k, r, j);
     } else {
       blk_tile(a.W, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, a.row_end, reinterpret_cast<char*>(sm));
     }
-    // publish: every storing wave drains its stores, then one lane sets the counter
-    if (tid == 0) chain_trace(a, 1, 3);
-    if ((tid & 63) == 0) chain_trace(a, 2 + (tid >> 6), 2);
+    // publish: every storing wave drains its stores, then wave 0 sets the counter
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if ((tid & 63) == 0) chain_trace(a, 2 + (tid >> 6), 3);
-    if (tid == 0) {
+    if (wave == 0) {
       chain_trace(a, 1, 4);
+      if (a.times) a.times[3 * t + 2] = __builtin_amdgcn_s_memrealtime();
       if (ty == CH_D) {
         st_flag(a.dflag + k, 1);
       } else if (ty == CH_S) {
@@ -954,7 +974,7 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       }
     }
   }
-  if (tid == 0) chain_trace(a, 1, 9);
+  if (wave == 0) chain_trace(a, 1, 9);
 }
 
 }  // namespace
@@ -1031,7 +1051,7 @@ hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipSt
 
 __global__ __launch_bounds__(DT) void chain_d_only_kernel(ChainArgs a) {  // (debugging: GPK_CHAIN_DBG=4)
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  chain_d(a, 0, sm);
+  chain_d(a.W, a.ld, a.Winv, a.info, a.trace, a.dbg, 0, sm);
 }
 
 hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {

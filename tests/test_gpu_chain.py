@@ -1,5 +1,5 @@
-"""The persistent single-member factorisation (gpk_tune("chain"), chain_kernel in gpk_potrf.hip) against the
-launch-per-panel schedule and the oracle (needs the MI355X).
+"""The persistent single-member factorisation (gpk_tune("chain"), chain_kernel in gpk_potrf.hip; off by default,
+DESIGN §4) against the launch-per-panel schedule and the oracle (needs the MI355X).
 
 One f64 member without identity / ragged rows runs as ONE launch whose workgroups claim the tasks of
 gpk_chain_plan (tests/test_chain_plan.py checks that list on the host).  Its trailing updates apply one
@@ -7,8 +7,6 @@ panel at a time where the launch path groups eight, so the two agree to summatio
 bit: L and the read-outs to ~1e-13 relative here.  Between runs of the chain itself the arithmetic order
 is fixed (every tile's updates are serialised by its counter), so repeated runs are bitwise equal.
 """
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -18,9 +16,7 @@ from tests.helpers import make_kernel
 
 from gaussianprocessfundamentals_amd import engine
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("GPK_TEST_CHAIN") != "1",
-                                 reason="persistent factorisation under development (GPK_TEST_CHAIN=1 runs it)")]
+pytestmark = pytest.mark.gpu
 
 SE = ("SE", {"ard": False})
 
