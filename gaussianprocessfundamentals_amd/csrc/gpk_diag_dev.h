@@ -131,21 +131,27 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) int32_t gi32;
 
 // Global accesses of the block code.  SC1 (chain_kernel): W / Winv bytes are handed to workgroups on
-// other XCDs inside one launch, so every load and store of them is an agent-scope relaxed atomic
-// (global_load / global_store ... sc1: the load bypasses the CU's L1, the store writes through the XCD's
-// L2) -- the hand-off needs no acquire fence (MI355X guide, inter-workgroup visibility, valid forms).
+// other XCDs inside one launch, so every store of them is an agent-scope relaxed atomic (global_store
+// ... sc1: written through the XCD's L2), and the consumer reads them with plain loads behind one agent
+// acquire (buffer_inv sc1: the CU's L1 and the XCD's L2 drop their stale lines) issued after its waits
+// (MI355X guide, inter-workgroup visibility).  (Until round 3's last measurements the loads were
+// relaxed 8-byte atomics too -- twice the load instructions for the same bytes.)
 template <bool SC1, typename T>
 __device__ __forceinline__ typename Vec16<T>::type ldv(const T* p) {
-  typedef typename Vec16<T>::type V;
+  return *reinterpret_cast<const typename Vec16<T>::type*>(p);
+}
+// Workgroup barrier.  SC1: an LDS-only one -- __syncthreads() also waits for every outstanding global
+// access of the wave (vmcnt(0)), and with write-through stores in flight each of the block's 17 barriers
+// waited for their acknowledgement from beyond the L2.  Nothing in the block body reads back what it
+// stored (the persistent kernel drains the stores before it publishes).
+template <bool SC1>
+__device__ __forceinline__ void wg_sync() {
   if constexpr (SC1) {
-    gu64* q = (gu64*)(const_cast<T*>(p));
-    struct {
-      uint64_t a, b;
-    } w = {__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-           __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
-    return __builtin_bit_cast(V, w);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   } else {
-    return *reinterpret_cast<const V*>(p);
+    __syncthreads();
   }
 }
 template <bool SC1, typename T>
@@ -284,7 +290,6 @@ __device__ __forceinline__ bool panel_zero_rows(const DiagArgs& a, int b, int64_
 template <typename T, bool FUSE, bool SC1 = false>
 __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* sm) {
   const int b = FUSE ? (int)blockIdx.y : b_in;
-  int nbar = 0;  // (debug trace of the write-through variant)
   double* A = sm;
   double* Dinv = A + LDS_A;
   double* colbuf = Dinv + LDS_DINV;
@@ -322,18 +327,12 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
     }
   }
   if (tid == 0) *flag = 0;
-  if constexpr (SC1) {
-    if ((threadIdx.x & 63) == 0 && a.ctr) __hip_atomic_store(a.ctr + (threadIdx.x >> 6), 150, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  { __syncthreads(); if constexpr (SC1) ++nbar; }
-  if constexpr (SC1) {
-    if ((threadIdx.x & 63) == 0 && a.ctr) __hip_atomic_store(a.ctr + (threadIdx.x >> 6), 200, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  wg_sync<SC1>();
   if (FUSE) {
     // the whole block is in LDS (every load retired into the LDS stores above): draw the ticket
     // tickets 0 .. grid - 1; the grid's last draw wraps the counter to 0 for the next launch
     if (tid == 0) *ticket = (int)atomicInc(reinterpret_cast<unsigned*>(&a.ctr[b]), gridDim.x - 1u);
-    { __syncthreads(); if constexpr (SC1) ++nbar; }
+    wg_sync<SC1>();
   }
   // FUSE: the last workgroup to load writes (alone, so its HBM stores never sit in front of a tile's
   // solve); the others solve tile = ticket
@@ -359,9 +358,6 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
   };
   d4 xs = {0.0, 0.0, 0.0, 0.0};  // wave 0: X_{s+1} (operand layout) from QR_s, stored in P_{s+1}
   auto step = [&](int s, auto last) {
-  if constexpr (SC1) {
-    if ((threadIdx.x & 63) == 0 && a.ctr) __hip_atomic_store(a.ctr + (threadIdx.x >> 6), 300 + 10 * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
     // ---------------------------------------------------------------- P_s
     if (decltype(last)::value && wave != 0) prefetch();
     if (wave == 0) {
@@ -401,10 +397,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
         store_inv_diag<T, SC1>(Dinv, Ib, I, tid - 64, DT - 64);
       }
     }
-    { __syncthreads(); if constexpr (SC1) ++nbar; }
-  if constexpr (SC1) {
-    if ((threadIdx.x & 63) == 0 && a.ctr) __hip_atomic_store(a.ctr + (threadIdx.x >> 6), 301 + 10 * s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+    wg_sync<SC1>();
     // ---------------------------------------------------------------- QR_s
     xs = d4{0.0, 0.0, 0.0, 0.0};  // (the old value is dead: nothing keeps it alive across potf2)
     if (s < NTL - 1 && wave < NTL - 1 - s && !(a.dbg & 4)) {
@@ -432,7 +425,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
         for (int q = 0; q < 4; ++q) A[aidx(i * DB + lr, s * DB + lk + 4 * q)] = xi[q];
       }
     }
-    { __syncthreads(); if constexpr (SC1) ++nbar; }
+    wg_sync<SC1>();
     };
   const int nsteps = (a.dbg & 16) ? 0 : NTL;
 #pragma unroll 1
@@ -450,11 +443,8 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
     store_l_rows<T, SC1>(A, Wb, a.ld, NTL - 1, tid, DT);
     if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
   }
-  if constexpr (SC1) {
-    if ((threadIdx.x & 63) == 0 && a.ctr) __hip_atomic_store(a.ctr + (threadIdx.x >> 6), 900 + 1000 * nbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
   if (!FUSE) return;
-  { __syncthreads(); if constexpr (SC1) ++nbar; }  // block row 7 of L^-1 in LDS
+  wg_sync<SC1>();  // block row 7 of L^-1 in LDS
   if (!live) return;
   // Linv[c][k] (c in tile I, k in tile J <= I): tile (J, I) of A transposed for J < I, Dinv_I for J = I
   const int rb = wave & 3, ch = wave >> 2;

@@ -643,7 +643,7 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 // evaluation (persistent factorisation).  Hand-offs (MI355X guide, inter-workgroup
 // visibility): every byte of W / Winv that a task writes is stored sc1 (write-through) and, after every
 // storing wave's vmcnt(0) and a barrier, one lane sets the counter; D, S and U32 read W / Winv with
-// sc1 loads only, BLK (LDS-DMA staging) behind one agent acquire.  Every wait is bounded: on timeout
+// plain loads behind one agent acquire per task.  Every wait is bounded: on timeout
 // the task sets ctl[1] and info = -1 and every workgroup drains the list without work.
 enum { CH_D = 0, CH_S = 1, CH_U32 = 2, CH_BLK = 3 };
 constexpr int CHAIN_SLOT_OFF = (int)((DIAG_LDS_BYTES + 15) / 16 * 16);
@@ -674,7 +674,7 @@ __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p,
 }
 
 // C[32 x 128] = A[32 x 128] B^T (SUB false) or C -= A B^T (SUB true), B [128 x 128]; A, C with row
-// stride ld, B with ldb; every load and store sc1.  Wave w: 16-row block w & 1, 16-column blocks
+// stride ld, B with ldb; plain loads (behind the task's acquire), sc1 stores.  Wave w: 16-row block w & 1, 16-column blocks
 // 2 (w >> 1) and 2 (w >> 1) + 1; K permuted so that lane group q takes k = 32 q + 16 h + s (h, s the half
 // and k-step): each lane reads contiguous 16-B pieces of its rows.  diag_off >= 0: the slice is rows
 // diag_off .. +31 of the block whose columns C covers -- column blocks right of each row block's
@@ -697,10 +697,8 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
   if (SUB) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (live0) acc0[i] = __builtin_bit_cast(double, (uint64_t)__hip_atomic_load(
-                               (gu64*)(Cr + 4 * i * ld), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (live1) acc1[i] = __builtin_bit_cast(double, (uint64_t)__hip_atomic_load(
-                               (gu64*)(Cr + 4 * i * ld + 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (live0) acc0[i] = Cr[4 * i * ld];
+      if (live1) acc1[i] = Cr[4 * i * ld + 16];
     }
   }
 #pragma unroll
@@ -831,13 +829,18 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
 #undef GPK_CH_CSOFF
 }
 
+#ifndef GPK_CHAIN_NOINLINE
+#define GPK_CHAIN_FN __device__ __forceinline__
+#else
+#define GPK_CHAIN_FN __device__ __noinline__
+#endif
 // The task bodies are separate (not inlined) functions: each gets its own register allocation, so the
 // diagonal-block body's 250 VGPRs do not force the others -- or the claim loop -- to spill.  They take
 // plain values, never the kernel argument by reference: its address taken, the kernel copies ChainArgs to
 // per-lane scratch and every field read becomes a VGPR load -- divergent for the compiler, which then
 // turned the claim loop's exit into an exec-mask-controlled loop whose barriers the waves no longer
 // executed the same number of times (the deadlock of the first versions).
-__device__ __noinline__ void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, int32_t* trace, int dbg, int k,
+GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, int dbg, int k,
                                     double* sm) {
   DiagArgs da{};
   da.W = W;
@@ -847,17 +850,14 @@ __device__ __noinline__ void chain_d(double* W, int64_t ld, double* Winv, int32_
   da.kblk = k;
   da.info = info;
   da.version = 2;
-  da.ctr = trace ? trace + 32 * blockIdx.x + 16 : nullptr;  // debugging: per-wave progress
-  if (dbg == 1)
-    diag2_body<double, false, false>(da, 0, sm);
-  else
-    diag2_body<double, false, true>(da, 0, sm);
+  (void)dbg;
+  diag2_body<double, false, true>(da, 0, sm);
 }
-__device__ __noinline__ void chain_s(double* W, int64_t ld, const double* Winv, int k, int r) {
+GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r) {
   double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
   slab_gemm<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1);
 }
-__device__ __noinline__ void chain_u32(double* W, int64_t ld, int q, int r, int j) {
+GPK_CHAIN_FN void chain_u32(double* W, int64_t ld, int q, int r, int j) {
   const int64_t R = (int64_t)r * 32;
   const int64_t J = (int64_t)j * NB;
   slab_gemm<true>(W + R * ld + (int64_t)q * NB, W + J * ld + (int64_t)q * NB, ld, W + R * ld + J, ld,
@@ -912,10 +912,10 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, in
     for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
     for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok && k > 0; ++s)
       ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + j, k, t0);
-    if (ok) {  // BLK stages through plain LDS-DMA / buffer loads: one agent acquire for them
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+  }
+  if (ok) {  // every task reads W / Winv with plain loads (BLK: LDS-DMA / buffer loads): one agent acquire
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   return ok;
 }
@@ -949,7 +949,7 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
     if (ty == CH_D) {
-      chain_d(a.W, a.ld, a.Winv, a.info, a.trace, a.dbg, k, sm);
+      chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, k, sm);
     } else if (ty == CH_S) {
       chain_s(a.W, a.ld, a.Winv, k, r);
     } else if (ty == CH_U32) {
@@ -1051,7 +1051,7 @@ hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipSt
 
 __global__ __launch_bounds__(DT) void chain_d_only_kernel(ChainArgs a) {  // (debugging: GPK_CHAIN_DBG=4)
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  chain_d(a.W, a.ld, a.Winv, a.info, a.trace, a.dbg, 0, sm);
+  chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, 0, sm);
 }
 
 hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {

@@ -82,10 +82,12 @@ def test_value_is_the_same_with_and_without_autograd(handling):
     assert h.grad is not None and math.isfinite(float(h.grad))
 
 
-def test_linear_cg_refuses_gradients():
+def test_linear_cg_differentiates():
+    # round 3: LINEAR_CONJUGATE_GRADIENT carries a CG tape instead of refusing requires_grad
     x, y = o.make_inputs("C1", n=100, seed=2)
     m = get_metric_by_type(MetricType.LL, build_gp(SE, x, y), numerical_matrix_handling=H.LINEAR_CONJUGATE_GRADIENT)
     assert math.isfinite(float(m.get_metric(hyp_list([0.15]), _nz(2e-2))))
     h = torch.tensor(0.15, dtype=torch.float64, requires_grad=True)
-    with pytest.raises(NotImplementedError):
-        m.get_metric([h], _nz(2e-2))
+    v = m.get_metric([h], _nz(2e-2))
+    (g,) = torch.autograd.grad(v, [h])
+    assert math.isfinite(float(g)) and float(g) != 0.0
