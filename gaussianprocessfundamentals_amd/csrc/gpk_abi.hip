@@ -463,7 +463,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     std::lock_guard<std::mutex> lk(g_chain_mu);
     if (g_chain_times_n < a.ntasks) {
       if (g_chain_times) hipFree(g_chain_times);
-      GPK_HIP(hipMalloc(&g_chain_times, (size_t)a.ntasks * 3 * sizeof(uint64_t)), "chain times");
+      GPK_HIP(hipMalloc(&g_chain_times, (size_t)a.ntasks * 6 * sizeof(uint64_t)), "chain times");
       g_chain_times_n = a.ntasks;
     }
     a.times = g_chain_times;
@@ -1683,7 +1683,7 @@ int gpk_timing_enable(int on) {
 int gpk_chain_times(uint64_t* out, int64_t ntasks) {
   if (!g_chain_times || !out || ntasks > g_chain_times_n) return -1;
   if (hipDeviceSynchronize() != hipSuccess) return -2;
-  return hipMemcpy(out, g_chain_times, (size_t)ntasks * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+  return hipMemcpy(out, g_chain_times, (size_t)ntasks * 6 * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
 }
 
 // debugging: the progress words of the last traced chain launch (GPK_CHAIN_TRACE=1), host memory only

@@ -140,13 +140,38 @@ template <bool SC1, typename T>
 __device__ __forceinline__ typename Vec16<T>::type ldv(const T* p) {
   return *reinterpret_cast<const typename Vec16<T>::type*>(p);
 }
+#ifdef GPK_CHAIN_SC1LD
+constexpr bool kChainSc1Ld = true;  // (A/B: chain tasks read through 16-B sc1 buffer loads, no acquire)
+#else
+constexpr bool kChainSc1Ld = false;
+#endif
+// a buffer resource over a wave-uniform base (readfirstlane: the compiler cannot prove it uniform)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint64_t uu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uu), 0, 0x7fffffff, 0x00020000);
+}
+// 16-B / 8-B buffer loads: one VGPR offset per lane, the wave-uniform part in soffset (an SGPR), so a
+// batch of loads needs no per-load 64-bit address registers (hoisted and spilled in chain_kernel, each
+// reload then waited vmcnt(0) -- the diagonal task's 16 block loads went out one at a time).  aux 16: sc1.
+constexpr int kLdAux = kChainSc1Ld ? 16 : 0;
+__device__ __forceinline__ Vec16<double>::type ld16_buf(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
+  return __builtin_bit_cast(Vec16<double>::type, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, kLdAux));
+}
+__device__ __forceinline__ double ld8_buf(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, kLdAux));
+}
 // Workgroup barrier.  SC1: an LDS-only one -- __syncthreads() also waits for every outstanding global
 // access of the wave (vmcnt(0)), and with write-through stores in flight each of the block's 17 barriers
 // waited for their acknowledgement from beyond the L2.  Nothing in the block body reads back what it
 // stored (the persistent kernel drains the stores before it publishes).
+#ifndef GPK_DIAG_LDS_BARRIER
+#define GPK_DIAG_LDS_BARRIER 0  // 1: the LDS-only barrier in the launch path's diagonal kernels too (A/B)
+#endif
 template <bool SC1>
 __device__ __forceinline__ void wg_sync() {
-  if constexpr (SC1) {
+  if constexpr (SC1 || GPK_DIAG_LDS_BARRIER) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -315,7 +340,13 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
 #pragma unroll
     for (int q = 0; q < NPASS; ++q) {
       const int r = r0 + q * RPP;
-      if (pc * EPC <= (r | (DB - 1))) v[q] = ldv<SC1, T>(Wb + (int64_t)r * a.ld + pc * EPC);
+      if (pc * EPC <= (r | (DB - 1))) {
+        if constexpr (SC1)
+          v[q] = ld16_buf(uniform_rsrc(Wb), (int)(((int64_t)r0 * a.ld + pc * EPC) * 8),
+                          __builtin_amdgcn_readfirstlane((int)((int64_t)q * RPP * a.ld * 8)));
+        else
+          v[q] = ldv<SC1, T>(Wb + (int64_t)r * a.ld + pc * EPC);
+      }
     }
 #pragma unroll
     for (int q = 0; q < NPASS; ++q) {

@@ -137,7 +137,7 @@ struct ChainArgs {
   int64_t timeout;       // per wait, in s_memrealtime ticks (100 MHz)
   int32_t* trace;        // debugging (GPK_CHAIN_TRACE=1, else NULL): host-visible [grid][32] progress words
   int32_t dbg;           // debugging (GPK_CHAIN_DBG): 4 = one diagonal task alone (chain_d_only_kernel)
-  uint64_t* times;       // profiling (GPK_CHAIN_TIMES=1, else NULL): per task [claimed, inputs ready, done] (100 MHz)
+  uint64_t* times;       // profiling (GPK_CHAIN_TIMES=1, else NULL): per task [claimed, inputs ready, wave 0's body done, published, S / U32: loads returned, MFMAs retired] (100 MHz)
 };
 
 struct FinArgs {

@@ -99,6 +99,10 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_base, 16, 0, 0);
 }
+template <int AUX>  // cache-policy bits (16: sc1)
+__device__ __forceinline__ void glds16a(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_base, 16, 0, AUX);
+}
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // buffer loads / stores of one element (voffset per lane, soffset wave-uniform)
@@ -675,14 +679,16 @@ __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p,
 
 // C[32 x 128] = A[32 x 128] B^T (SUB false) or C -= A B^T (SUB true), B [128 x 128]; A, C with row
 // stride ld, B with ldb; plain loads (behind the task's acquire), sc1 stores.  Wave w: 16-row block w & 1, 16-column blocks
-// 2 (w >> 1) and 2 (w >> 1) + 1; K permuted so that lane group q takes k = 32 q + 16 h + s (h, s the half
-// and k-step): each lane reads contiguous 16-B pieces of its rows.  diag_off >= 0: the slice is rows
+// 2 (w >> 1) and 2 (w >> 1) + 1; K permuted so that in k-step pair j = 0..15 lane group q takes the 16-B
+// piece k = 8 j + 2 q (+0, +1): the four lane groups of a row read one contiguous 64-B line per load
+// instruction (16 lines per instruction; with k = 32 q + 16 h + s they touched 64 lines each, and the
+// S / U32 tasks spent 16 us in the texture path for 1 MFLOP).  diag_off >= 0: the slice is rows
 // diag_off .. +31 of the block whose columns C covers -- column blocks right of each row block's
 // diagonal block are neither computed nor stored.  C may alias A (the panel solve, in place): the
 // stores wait for every wave's reads at a barrier.
 template <bool SUB>
 __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int64_t ldb, double* C, int64_t ld,
-                                          int diag_off) {
+                                          int diag_off, uint64_t* st) {
   typedef double dbl2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
   const int w = wave_uniform((int)threadIdx.x >> 6);
@@ -690,32 +696,51 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
   const int rb = w & 1, cb0 = 2 * (w >> 1);
   const int cb_last = diag_off < 0 ? 7 : (diag_off >> 4) + rb;
   const bool live0 = cb0 <= cb_last, live1 = cb0 + 1 <= cb_last;
-  const double* Ar = A + (int64_t)(rb * 16 + lr) * ld + 32 * q;
-  const double* Br = B + (int64_t)(cb0 * 16 + lr) * ldb + 32 * q;
+  const double* Ar = A + (int64_t)(rb * 16 + lr) * ld + 2 * q;
+  const double* Br = B + (int64_t)(cb0 * 16 + lr) * ldb + 2 * q;
   double* Cr = C + (int64_t)(rb * 16 + q) * ld + cb0 * 16 + lr;  // C/D layout: row q + 4 i, column lr
   d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  // Every load and MFMA is unconditional (the column blocks right of the diagonal are valid rows of W, only
+  // their stores are skipped): with the loads under the wave-uniform live0 / live1 branches, hipcc could
+  // not count them across the joins and waited vmcnt(0) before every MFMA -- one round trip to the
+  // Infinity Cache per k-step pair, 16 us per task.
+  const __amdgpu_buffer_rsrc_t ars = uniform_rsrc(A), brs = uniform_rsrc(B), crs = uniform_rsrc(C);
+  const int avo = (int)((Ar - A) * 8), bvo = (int)((Br - B) * 8), cvo = (int)((Cr - C) * 8);
+  const int ldc4 = __builtin_amdgcn_readfirstlane((int)(4 * ld * 8)), ldb16 = __builtin_amdgcn_readfirstlane((int)(16 * ldb * 8));
   if (SUB) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (live0) acc0[i] = Cr[4 * i * ld];
-      if (live1) acc1[i] = Cr[4 * i * ld + 16];
+      acc0[i] = ld8_buf(crs, cvo, i * ldc4);
+      acc1[i] = ld8_buf(crs, cvo + 16 * 8, i * ldc4);
     }
+  }
+  dbl2 av[2][8], b0[2][8], b1[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      av[h][s] = ld16_buf(ars, avo + (8 * h + s) * 64, 0);
+      b0[h][s] = ld16_buf(brs, bvo + (8 * h + s) * 64, 0);
+      b1[h][s] = ld16_buf(brs, bvo + (8 * h + s) * 64, ldb16);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all 48 (+8) loads in flight before the first MFMA
+  if (st && w == 0) {  // (profiling: wave 0's loads returned)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st[4] = __builtin_amdgcn_s_memrealtime();
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    dbl2 av[8], b0[8], b1[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      av[s] = ldv<true, double>(Ar + 16 * h + 2 * s);
-      if (live0) b0[s] = ldv<true, double>(Br + 16 * h + 2 * s);
-      if (live1) b1[s] = ldv<true, double>(Br + 16 * ldb + 16 * h + 2 * s);
-    }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const double a = av[s >> 1][s & 1];
-      if (live0) acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b0[s >> 1][s & 1], acc0, 0, 0, SUB ? 1 : 0);
-      if (live1) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1[s >> 1][s & 1], acc1, 0, 0, SUB ? 1 : 0);
+      const double a = av[h][s >> 1][s & 1];
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b0[h][s >> 1][s & 1], acc0, 0, 0, SUB ? 1 : 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1[h][s >> 1][s & 1], acc1, 0, 0, SUB ? 1 : 0);
     }
+  }
+  if (st && w == 0) {  // (profiling: wave 0's MFMAs retired -- the readfirstlane waits for the last one)
+    const int dep = __builtin_amdgcn_readfirstlane((int)acc0[3] + (int)acc1[3]);
+    st[5] = __builtin_amdgcn_s_memrealtime() + (dep == 0x7fffffff ? 1 : 0);
   }
   __syncthreads();  // in place (S): every wave's A reads are done before the first store
 #pragma unroll
@@ -766,7 +791,7 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
 #pragma unroll
     for (int n = 0; n < NBK; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[m][n][r] = BufIO<double>::load(crs, cvo, GPK_CH_CSOFF(m, n, r));
+      for (int r = 0; r < 4; ++r) acc[m][n][r] = ld8_buf(crs, cvo, GPK_CH_CSOFF(m, n, r));
   const int q = lane >> 4, lr = lane & 15;
   const int aoff = (wr * (TM / WM) + lr) * ROWB;
   const int boff = (TM + wc * (TN / WN) + lr) * ROWB;
@@ -774,7 +799,7 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
 #define GPK_CH_GLDS(stage, kc)                                                                   \
   {                                                                                              \
     _Pragma("unroll") for (int i = 0; i < PW; ++i)                                               \
-        glds16(src[i] + (int64_t)(kc) * GBK, smem + (stage) * STAGE + (wid * PW + i) * 1024);      \
+        glds16a<kLdAux>(src[i] + (int64_t)(kc) * GBK, smem + (stage) * STAGE + (wid * PW + i) * 1024); \
   }
   GPK_CH_GLDS(0, 0);
   const int64_t wrow0 = R + wr * (TM / WM);
@@ -853,15 +878,15 @@ GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, in
   (void)dbg;
   diag2_body<double, false, true>(da, 0, sm);
 }
-GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r) {
+GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st) {
   double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
-  slab_gemm<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1);
+  slab_gemm<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st);
 }
-GPK_CHAIN_FN void chain_u32(double* W, int64_t ld, int q, int r, int j) {
+GPK_CHAIN_FN void chain_u32(double* W, int64_t ld, int q, int r, int j, uint64_t* st) {
   const int64_t R = (int64_t)r * 32;
   const int64_t J = (int64_t)j * NB;
   slab_gemm<true>(W + R * ld + (int64_t)q * NB, W + J * ld + (int64_t)q * NB, ld, W + R * ld + J, ld,
-                  (R >= J && R < J + NB) ? (int)(R - J) : -1);
+                  (R >= J && R < J + NB) ? (int)(R - J) : -1, st);
 }
 
 __device__ __forceinline__ void chain_trace(const ChainArgs& a, int slot, int v) {
@@ -913,10 +938,6 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, in
     for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok && k > 0; ++s)
       ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + j, k, t0);
   }
-  if (ok) {  // every task reads W / Winv with plain loads (BLK: LDS-DMA / buffer loads): one agent acquire
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
   return ok;
 }
 
@@ -940,9 +961,17 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     const int r = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 2]);
     const int j = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 3]);
     if (wave == 0) {
-      if (a.times) a.times[3 * t] = __builtin_amdgcn_s_memrealtime();
+      if (a.times) a.times[6 * t] = __builtin_amdgcn_s_memrealtime();
       const bool ok = chain_deps(a, ty, k, r, j);
-      if (a.times) a.times[3 * t + 1] = __builtin_amdgcn_s_memrealtime();
+      if (a.times) {
+        a.times[6 * t + 1] = __builtin_amdgcn_s_memrealtime();
+        if (ty == CH_D || ty == CH_BLK) a.times[6 * t + 4] = __builtin_amdgcn_s_memtime();  // shader clock
+      }
+      if (ok && !kChainSc1Ld) {
+        // the task reads W / Winv with plain loads (BLK: LDS-DMA / buffer loads): one agent acquire
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       slot[1] = ok ? 1 : 0;
       chain_trace(a, 1, ok ? 2 : -2);
     }
@@ -951,18 +980,22 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     if (ty == CH_D) {
       chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, k, sm);
     } else if (ty == CH_S) {
-      chain_s(a.W, a.ld, a.Winv, k, r);
+      chain_s(a.W, a.ld, a.Winv, k, r, a.times ? a.times + 6 * t : nullptr);
     } else if (ty == CH_U32) {
-      chain_u32(a.W, a.ld, k, r, j);
+      chain_u32(a.W, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr);
     } else {
       blk_tile(a.W, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, a.row_end, reinterpret_cast<char*>(sm));
+    }
+    if (wave == 0 && a.times) {
+      a.times[6 * t + 2] = __builtin_amdgcn_s_memrealtime();  // wave 0's body done
+      if (ty == CH_D || ty == CH_BLK) a.times[6 * t + 5] = __builtin_amdgcn_s_memtime();
     }
     // publish: every storing wave drains its stores, then wave 0 sets the counter
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (wave == 0) {
       chain_trace(a, 1, 4);
-      if (a.times) a.times[3 * t + 2] = __builtin_amdgcn_s_memrealtime();
+      if (a.times) a.times[6 * t + 3] = __builtin_amdgcn_s_memrealtime();
       if (ty == CH_D) {
         st_flag(a.dflag + k, 1);
       } else if (ty == CH_S) {

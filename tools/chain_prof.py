@@ -34,26 +34,55 @@ torch.cuda.synchronize()
 lay = f.layout
 tasks = nat.chain_plan(lay.n_pad, lay.y_row, grid if grid > 0 else torch.cuda.get_device_properties(0).multi_processor_count)
 nt = len(tasks)
-buf = (ctypes.c_uint64 * (3 * nt))()
+buf = (ctypes.c_uint64 * (6 * nt))()
 rc = nat.load_library().gpk_chain_times(buf, nt)
-T = np.frombuffer(buf, dtype=np.uint64).reshape(nt, 3).astype(np.float64) / 100.0  # us
+Traw = np.frombuffer(buf, dtype=np.uint64).reshape(nt, 6).astype(np.float64)
+T = Traw / 100.0  # us
 t0 = T[:, 0].min()
-T -= t0
-print("rc", rc, "tasks", nt, "span %.1f us" % (T[:, 2].max()), flush=True)
+T[:, :4] -= t0
+T[:, 4:] = np.where((T[:, 4:] > 0) & (tasks[:, :1] != 0) & (tasks[:, :1] != 3), T[:, 4:] - t0, np.nan)
+print("rc", rc, "tasks", nt, "span %.1f us" % (T[:, 3].max()), flush=True)
 names = ["D", "S", "U32", "BLK"]
 for ty in range(4):
     m = tasks[:, 0] == ty
     if m.any():
         w = T[m, 1] - T[m, 0]
-        r = T[m, 2] - T[m, 1]
-        print("%-4s n %5d  wait mean %.1f  run mean %.1f  min %.1f  max %.1f us" % (names[ty], m.sum(), w.mean(), r.mean(),
-                                                                             r.min(), r.max()), flush=True)
+        r = T[m, 3] - T[m, 1]
+        b = T[m, 2] - T[m, 1]
+        print("%-4s n %5d  wait mean %.1f  run mean %.1f  min %.1f  max %.1f us (wave 0 body %.1f, drain + barrier %.1f)" % (
+            names[ty], m.sum(), w.mean(), r.mean(), r.min(), r.max(), b.mean(), (r - b).mean()), flush=True)
+        if ty in (1, 2):
+            print("     wave 0: loads returned %.1f, MFMAs retired %.1f, body done %.1f us after ready" % (
+                np.nanmean(T[m, 4] - T[m, 1]), np.nanmean(T[m, 5] - T[m, 1]), b.mean()), flush=True)
 d = np.where(tasks[:, 0] == 0)[0]
-print("D(k) ready / done (us):", [(int(tasks[i, 1]), round(T[i, 1], 1), round(T[i, 2], 1)) for i in d[:8]], flush=True)
-gaps = np.diff(T[d, 2])
+print("D(k) ready / done (us):", [(int(tasks[i, 1]), round(T[i, 1], 1), round(T[i, 3], 1)) for i in d[:8]], flush=True)
+gaps = np.diff(T[d, 3])
 print("D done spacing mean %.1f us, first %s" % (gaps.mean(), np.round(gaps[:10], 1).tolist()), flush=True)
 # for step 5: the chain tasks' ready/done
 k = min(5, len(d) - 1)
 for ty in (1, 2):
     m = (tasks[:, 0] == ty) & (tasks[:, 1] == k) & (tasks[:, 2] // 4 == k + 1)
-    print(names[ty], "k=%d block k+1 slices: ready %s done %s" % (k, np.round(T[m, 1], 1).tolist(), np.round(T[m, 2], 1).tolist()))
+    print(names[ty], "k=%d block k+1 slices: ready %s done %s" % (k, np.round(T[m, 1], 1).tolist(), np.round(T[m, 3], 1).tolist()))
+
+# the critical chain of steps 4..9: D(k) run, hand-off to the first S of block k + 1, S run, hand-off to
+# the U32 of those slices, U32 run, hand-off to D(k + 1)
+idx = {tuple(t[:4]): i for i, t in enumerate(tasks.tolist())}
+for k in range(4, min(10, len(d) - 1)):
+    i_d, i_d1 = d[k], d[k + 1]
+    sl = [idx.get((1, k, s, 0)) for s in range(4 * (k + 1), 4 * (k + 1) + 4)]
+    ul = [idx.get((2, k, s, k + 1)) for s in range(4 * (k + 1), 4 * (k + 1) + 4)]
+    if None in sl or None in ul:
+        continue
+    s_rdy, s_done = max(T[sl, 1]), max(T[sl, 3])
+    u_rdy, u_done = max(T[ul, 1]), max(T[ul, 3])
+    print("step %d: D %.1f | ->S %.1f | S %.1f | ->U %.1f | U %.1f | ->D %.1f  (total %.1f)" % (
+        k, T[i_d, 3] - T[i_d, 1], s_rdy - T[i_d, 3], s_done - s_rdy, u_rdy - s_done, u_done - u_rdy,
+        T[i_d1, 1] - u_done, T[i_d1, 1] - T[i_d, 1]), flush=True)
+
+# effective shader clock over the D and BLK bodies (s_memtime cycles / s_memrealtime at 100 MHz)
+for ty in (0, 3):
+    m = tasks[:, 0] == ty
+    cyc = Traw[m, 5] - Traw[m, 4]
+    us = (Traw[m, 2] - Traw[m, 1]) / 100.0
+    ok = (cyc > 0) & (us > 0)
+    print("%s body: shader clock %.2f GHz (median over %d tasks)" % (names[ty], np.median(cyc[ok] / us[ok]) / 1e3, ok.sum()), flush=True)
