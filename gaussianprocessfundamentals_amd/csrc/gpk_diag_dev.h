@@ -145,12 +145,14 @@ constexpr bool kChainSc1Ld = true;  // (A/B: chain tasks read through 16-B sc1 b
 #else
 constexpr bool kChainSc1Ld = false;
 #endif
-// a buffer resource over a wave-uniform base (readfirstlane: the compiler cannot prove it uniform)
+// a buffer resource over a wave-uniform base (readfirstlane: the compiler cannot prove it uniform), 1 GiB
+// long: an offset of kRsrcBytes or more is out of range -- the load returns 0 and touches no memory
+constexpr int kRsrcBytes = 0x40000000;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
   const uint64_t u = reinterpret_cast<uint64_t>(p);
   const uint64_t uu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uu), 0, 0x7fffffff, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uu), 0, kRsrcBytes, 0x00020000);
 }
 // 16-B / 8-B buffer loads: one VGPR offset per lane, the wave-uniform part in soffset (an SGPR), so a
 // batch of loads needs no per-load 64-bit address registers (hoisted and spilled in chain_kernel, each

@@ -714,14 +714,21 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
       acc1[i] = ld8_buf(crs, cvo + 16 * 8, i * ldc4);
     }
   }
+  // k-step pairs j > jm of a column block contribute nothing: the upper triangle of L^-1 (S: column block
+  // cb needs k <= 16 cb + 15, j <= 2 cb + 1) or a column block right of the diagonal (U32).  Their loads go
+  // out of the buffer's range (zeros, no memory traffic), so S moves ~60 % of the bytes without a branch.
+  const int jm0 = SUB ? (live0 ? 15 : -1) : 2 * cb0 + 1;
+  const int jm1 = SUB ? (live1 ? 15 : -1) : 2 * cb0 + 3;
+  const int jma = jm0 > jm1 ? jm0 : jm1;
   dbl2 av[2][8], b0[2][8], b1[2][8];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      av[h][s] = ld16_buf(ars, avo + (8 * h + s) * 64, 0);
-      b0[h][s] = ld16_buf(brs, bvo + (8 * h + s) * 64, 0);
-      b1[h][s] = ld16_buf(brs, bvo + (8 * h + s) * 64, ldb16);
+      const int j = 8 * h + s;
+      av[h][s] = ld16_buf(ars, j <= jma ? avo + j * 64 : kRsrcBytes, 0);
+      b0[h][s] = ld16_buf(brs, j <= jm0 ? bvo + j * 64 : kRsrcBytes, 0);
+      b1[h][s] = ld16_buf(brs, j <= jm1 ? bvo + j * 64 : kRsrcBytes, ldb16);
     }
   }
   __builtin_amdgcn_sched_barrier(0);  // all 48 (+8) loads in flight before the first MFMA
