@@ -678,82 +678,77 @@ __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p,
 }
 
 // C[32 x 128] = A[32 x 128] B^T (SUB false) or C -= A B^T (SUB true), B [128 x 128]; A, C with row
-// stride ld, B with ldb; plain loads (behind the task's acquire), sc1 stores.  Wave w: 16-row block w & 1, 16-column blocks
-// 2 (w >> 1) and 2 (w >> 1) + 1; K permuted so that in k-step pair j = 0..15 lane group q takes the 16-B
-// piece k = 8 j + 2 q (+0, +1): the four lane groups of a row read one contiguous 64-B line per load
-// instruction (16 lines per instruction; with k = 32 q + 16 h + s they touched 64 lines each, and the
-// S / U32 tasks spent 16 us in the texture path for 1 MFLOP).  diag_off >= 0: the slice is rows
-// diag_off .. +31 of the block whose columns C covers -- column blocks right of each row block's
-// diagonal block are neither computed nor stored.  C may alias A (the panel solve, in place): the
-// stores wait for every wave's reads at a barrier.
+// stride ld, B with ldb.  These tasks are bound by the bytes one CU pulls from the Infinity Cache, so every
+// operand byte is fetched once: A (32 rows, 32 KB) is staged into LDS by LDS-DMA (row stride 1040 B: the
+// quarter-wave's 16 rows land on distinct bank groups), and each wave owns one column block (16 columns,
+// both 16-row blocks), loading its 16 rows of B straight into registers.  In k-step pair j = 0..15 lane group q
+// takes the 16-B piece k = 8 j + 2 q (+0, +1), so the four lane groups of a row read one 64-B line.  Pieces
+// that contribute nothing -- the upper triangle of L^-1 (S: column block cb needs k <= 16 cb + 15) or a
+// column block right of the diagonal (U32, diag_off >= 0: rows diag_off .. +31 of the block whose columns C
+// covers) -- are loaded out of the buffer's range (zeros, no memory traffic).  C may alias A (the panel
+// solve, in place): A is in LDS behind the barrier before any store.  Plain loads behind the task's
+// acquire, sc1 stores.  (The first form -- 2 x 4 waves of 16 x 32, A and B loaded per wave from HBM / L2 --
+// moved 384 KB per task: 16 us against 11-12 us for the same work with the zero pieces skipped.)
+constexpr int SLAB_LDS_ROW = 1040;
 template <bool SUB>
 __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int64_t ldb, double* C, int64_t ld,
-                                          int diag_off, uint64_t* st) {
+                                          int diag_off, uint64_t* st, char* smem) {
   typedef double dbl2 __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
   const int w = wave_uniform((int)threadIdx.x >> 6);
   const int lr = lane & 15, q = lane >> 4;
-  const int rb = w & 1, cb0 = 2 * (w >> 1);
-  const int cb_last = diag_off < 0 ? 7 : (diag_off >> 4) + rb;
-  const bool live0 = cb0 <= cb_last, live1 = cb0 + 1 <= cb_last;
-  const double* Ar = A + (int64_t)(rb * 16 + lr) * ld + 2 * q;
-  const double* Br = B + (int64_t)(cb0 * 16 + lr) * ldb + 2 * q;
-  double* Cr = C + (int64_t)(rb * 16 + q) * ld + cb0 * 16 + lr;  // C/D layout: row q + 4 i, column lr
+  // column block of wave w: waves w and w + 4 share a SIMD, so pair the blocks (0, 7), (1, 6), (2, 5),
+  // (3, 4) -- S's work per block grows with the block index (the triangle of L^-1)
+  const int cb = w < 4 ? w : 11 - w;
+  // live row blocks of this wave's column block (U32 on the diagonal block: columns <= the rows' block)
+  const bool live0 = diag_off < 0 || cb <= (diag_off >> 4), live1 = diag_off < 0 || cb <= (diag_off >> 4) + 1;
+  // A rows 4 w .. 4 w + 3 into LDS, one 1-KB row per instruction
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 4 * w + i;
+    glds16a<kLdAux>(A + (int64_t)row * ld + 2 * lane, smem + row * SLAB_LDS_ROW);
+  }
+  const __amdgpu_buffer_rsrc_t brs = uniform_rsrc(B), crs = uniform_rsrc(C);
+  const int bvo = (int)(((int64_t)(cb * 16 + lr) * ldb + 2 * q) * 8);
+  const int cvo = (int)(((int64_t)q * ld + cb * 16 + lr) * 8);  // C/D layout: row q + 4 i, column lr
+  const int ldc4 = __builtin_amdgcn_readfirstlane((int)(4 * ld * 8)), ldc16 = __builtin_amdgcn_readfirstlane((int)(16 * ld * 8));
+  const int jm = SUB ? (live1 ? 15 : -1) : 2 * cb + 1;
   d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-  // Every load and MFMA is unconditional (the column blocks right of the diagonal are valid rows of W, only
-  // their stores are skipped): with the loads under the wave-uniform live0 / live1 branches, hipcc could
-  // not count them across the joins and waited vmcnt(0) before every MFMA -- one round trip to the
-  // Infinity Cache per k-step pair, 16 us per task.
-  const __amdgpu_buffer_rsrc_t ars = uniform_rsrc(A), brs = uniform_rsrc(B), crs = uniform_rsrc(C);
-  const int avo = (int)((Ar - A) * 8), bvo = (int)((Br - B) * 8), cvo = (int)((Cr - C) * 8);
-  const int ldc4 = __builtin_amdgcn_readfirstlane((int)(4 * ld * 8)), ldb16 = __builtin_amdgcn_readfirstlane((int)(16 * ldb * 8));
   if (SUB) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       acc0[i] = ld8_buf(crs, cvo, i * ldc4);
-      acc1[i] = ld8_buf(crs, cvo + 16 * 8, i * ldc4);
+      acc1[i] = ld8_buf(crs, cvo, ldc16 + i * ldc4);
     }
   }
-  // k-step pairs j > jm of a column block contribute nothing: the upper triangle of L^-1 (S: column block
-  // cb needs k <= 16 cb + 15, j <= 2 cb + 1) or a column block right of the diagonal (U32).  Their loads go
-  // out of the buffer's range (zeros, no memory traffic), so S moves ~60 % of the bytes without a branch.
-  const int jm0 = SUB ? (live0 ? 15 : -1) : 2 * cb0 + 1;
-  const int jm1 = SUB ? (live1 ? 15 : -1) : 2 * cb0 + 3;
-  const int jma = jm0 > jm1 ? jm0 : jm1;
-  dbl2 av[2][8], b0[2][8], b1[2][8];
+  dbl2 bv[16];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int j = 0; j < 16; ++j) bv[j] = ld16_buf(brs, j <= jm ? bvo + j * 64 : kRsrcBytes, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA writes are not tracked by hipcc)
+  __syncthreads();
+  if (st && w == 0) st[4] = __builtin_amdgcn_s_memrealtime();  // (profiling: operands in place)
+  const char* a0 = smem + lr * SLAB_LDS_ROW + q * 16;
+  const char* a1 = a0 + 16 * SLAB_LDS_ROW;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int j = 8 * h + s;
-      av[h][s] = ld16_buf(ars, j <= jma ? avo + j * 64 : kRsrcBytes, 0);
-      b0[h][s] = ld16_buf(brs, j <= jm0 ? bvo + j * 64 : kRsrcBytes, 0);
-      b1[h][s] = ld16_buf(brs, j <= jm1 ? bvo + j * 64 : kRsrcBytes, ldb16);
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);  // all 48 (+8) loads in flight before the first MFMA
-  if (st && w == 0) {  // (profiling: wave 0's loads returned)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st[4] = __builtin_amdgcn_s_memrealtime();
-  }
+  for (int j = 0; j < 16; ++j) {
+    if (j > jm) break;  // (wave-uniform)
+    const dbl2 x0 = *reinterpret_cast<const dbl2*>(a0 + j * 64);
+    const dbl2 x1 = *reinterpret_cast<const dbl2*>(a1 + j * 64);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const double a = av[h][s >> 1][s & 1];
-      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b0[h][s >> 1][s & 1], acc0, 0, 0, SUB ? 1 : 0);
-      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1[h][s >> 1][s & 1], acc1, 0, 0, SUB ? 1 : 0);
+    for (int e = 0; e < 2; ++e) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[e], bv[j][e], acc0, 0, 0, SUB ? 1 : 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[e], bv[j][e], acc1, 0, 0, SUB ? 1 : 0);
     }
   }
   if (st && w == 0) {  // (profiling: wave 0's MFMAs retired -- the readfirstlane waits for the last one)
     const int dep = __builtin_amdgcn_readfirstlane((int)acc0[3] + (int)acc1[3]);
     st[5] = __builtin_amdgcn_s_memrealtime() + (dep == 0x7fffffff ? 1 : 0);
   }
-  __syncthreads();  // in place (S): every wave's A reads are done before the first store
+  double* Cr = C + (int64_t)q * ld + cb * 16 + lr;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (live0) sts<true>(Cr + 4 * i * ld, acc0[i]);
-    if (live1) sts<true>(Cr + 4 * i * ld + 16, acc1[i]);
+    if (live1) sts<true>(Cr + (16 + 4 * i) * ld, acc1[i]);
   }
 }
 
@@ -885,15 +880,15 @@ GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, in
   (void)dbg;
   diag2_body<double, false, true>(da, 0, sm);
 }
-GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st) {
+GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
   double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
-  slab_gemm<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st);
+  slab_gemm<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem);
 }
-GPK_CHAIN_FN void chain_u32(double* W, int64_t ld, int q, int r, int j, uint64_t* st) {
+GPK_CHAIN_FN void chain_u32(double* W, int64_t ld, int q, int r, int j, uint64_t* st, char* smem) {
   const int64_t R = (int64_t)r * 32;
   const int64_t J = (int64_t)j * NB;
   slab_gemm<true>(W + R * ld + (int64_t)q * NB, W + J * ld + (int64_t)q * NB, ld, W + R * ld + J, ld,
-                  (R >= J && R < J + NB) ? (int)(R - J) : -1, st);
+                  (R >= J && R < J + NB) ? (int)(R - J) : -1, st, smem);
 }
 
 __device__ __forceinline__ void chain_trace(const ChainArgs& a, int slot, int v) {
@@ -987,9 +982,9 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     if (ty == CH_D) {
       chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, k, sm);
     } else if (ty == CH_S) {
-      chain_s(a.W, a.ld, a.Winv, k, r, a.times ? a.times + 6 * t : nullptr);
+      chain_s(a.W, a.ld, a.Winv, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
     } else if (ty == CH_U32) {
-      chain_u32(a.W, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr);
+      chain_u32(a.W, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
     } else {
       blk_tile(a.W, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, a.row_end, reinterpret_cast<char*>(sm));
     }

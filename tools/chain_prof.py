@@ -52,7 +52,7 @@ for ty in range(4):
         print("%-4s n %5d  wait mean %.1f  run mean %.1f  min %.1f  max %.1f us (wave 0 body %.1f, drain + barrier %.1f)" % (
             names[ty], m.sum(), w.mean(), r.mean(), r.min(), r.max(), b.mean(), (r - b).mean()), flush=True)
         if ty in (1, 2):
-            print("     wave 0: loads returned %.1f, MFMAs retired %.1f, body done %.1f us after ready" % (
+            print("     wave 0: operands in place %.1f, MFMAs retired %.1f, body done %.1f us after ready" % (
                 np.nanmean(T[m, 4] - T[m, 1]), np.nanmean(T[m, 5] - T[m, 1]), b.mean()), flush=True)
 d = np.where(tasks[:, 0] == 0)[0]
 print("D(k) ready / done (us):", [(int(tasks[i, 1]), round(T[i, 1], 1), round(T[i, 3], 1)) for i in d[:8]], flush=True)
