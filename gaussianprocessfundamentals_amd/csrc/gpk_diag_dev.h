@@ -164,6 +164,14 @@ __device__ __forceinline__ Vec16<double>::type ld16_buf(__amdgpu_buffer_rsrc_t r
 __device__ __forceinline__ double ld8_buf(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, kLdAux));
 }
+// threadIdx.x behind an empty volatile asm: in chain_kernel's task loop every task body then recomputes
+// its per-lane addresses instead of the compiler hoisting them out of the loop for all task types at
+// once and spilling them (their scratch reloads waited behind the write-through stores)
+__device__ __forceinline__ int opaque_tid() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
 // Workgroup barrier.  SC1: an LDS-only one -- __syncthreads() also waits for every outstanding global
 // access of the wave (vmcnt(0)), and with write-through stores in flight each of the block's 17 barriers
 // waited for their acknowledgement from beyond the L2.  Nothing in the block body reads back what it
@@ -322,7 +330,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
   double* colbuf = Dinv + LDS_DINV;
   int* flag = reinterpret_cast<int*>(colbuf + LDS_COL);
 
-  const int tid = threadIdx.x;
+  const int tid = SC1 ? opaque_tid() : (int)threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15;

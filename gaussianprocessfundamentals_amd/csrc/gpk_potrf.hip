@@ -694,8 +694,9 @@ template <bool SUB>
 __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int64_t ldb, double* C, int64_t ld,
                                           int diag_off, uint64_t* st, char* smem) {
   typedef double dbl2 __attribute__((ext_vector_type(2)));
-  const int lane = threadIdx.x & 63;
-  const int w = wave_uniform((int)threadIdx.x >> 6);
+  const int tid = opaque_tid();
+  const int lane = tid & 63;
+  const int w = wave_uniform(tid >> 6);
   const int lr = lane & 15, q = lane >> 4;
   // column block of wave w: waves w and w + 4 share a SIMD, so pair the blocks (0, 7), (1, 6), (2, 5),
   // (3, 4) -- S's work per block grows with the block index (the triangle of L^-1)
@@ -731,13 +732,14 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
   const char* a1 = a0 + 16 * SLAB_LDS_ROW;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    if (j > jm) break;  // (wave-uniform)
-    const dbl2 x0 = *reinterpret_cast<const dbl2*>(a0 + j * 64);
-    const dbl2 x1 = *reinterpret_cast<const dbl2*>(a1 + j * 64);
+    if (j <= jm) {  // (wave-uniform; a break here left bv dynamically indexed, i.e. in scratch)
+      const dbl2 x0 = *reinterpret_cast<const dbl2*>(a0 + j * 64);
+      const dbl2 x1 = *reinterpret_cast<const dbl2*>(a1 + j * 64);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[e], bv[j][e], acc0, 0, 0, SUB ? 1 : 0);
-      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[e], bv[j][e], acc1, 0, 0, SUB ? 1 : 0);
+      for (int e = 0; e < 2; ++e) {
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0[e], bv[j][e], acc0, 0, 0, SUB ? 1 : 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1[e], bv[j][e], acc1, 0, 0, SUB ? 1 : 0);
+      }
     }
   }
   if (st && w == 0) {  // (profiling: wave 0's MFMAs retired -- the readfirstlane waits for the last one)
@@ -762,7 +764,7 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
   constexpr int PW = (TM + TN) / (8 * NW);
   constexpr int NK = NB / GBK;
   typedef double vec_t __attribute__((ext_vector_type(2)));
-  const int tid = threadIdx.x;
+  const int tid = opaque_tid();
   const int lane = tid & 63;
   const int wid = wave_uniform(tid >> 6);
   const int wr = wid / WN, wc = wid % WN;

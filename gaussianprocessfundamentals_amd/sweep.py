@@ -65,7 +65,7 @@ def native_batched_evaluator(kernel, X: torch.Tensor, y: torch.Tensor, noise, dt
         slots = [caller] + streams
         for st in streams:
             st.wait_stream(caller)
-        old_la = old_fuse = None
+        old_la = old_fuse = old_chain = None
         if P > 1:
             # the chunks' factorisations overlap on P streams: no look-ahead side streams, and no panel
             # solve fused into the diagonal-block launch (its redundant workgroups would take CUs from
@@ -73,6 +73,7 @@ def native_batched_evaluator(kernel, X: torch.Tensor, y: torch.Tensor, noise, dt
             from . import _native as nat
             old_la = nat.tune("lookahead", 0)
             old_fuse = nat.tune("fuse_trsm", 0)
+            old_chain = nat.tune("chain", 0)  # (a persistent launch per chunk would claim every CU)
         try:
             for i, s0 in enumerate(range(0, c, step)):
                 s1 = min(c, s0 + step)
@@ -90,6 +91,7 @@ def native_batched_evaluator(kernel, X: torch.Tensor, y: torch.Tensor, noise, dt
             if old_la is not None:
                 nat.tune("lookahead", old_la)
                 nat.tune("fuse_trsm", old_fuse)
+                nat.tune("chain", old_chain)
         for st in streams:
             caller.wait_stream(st)
         return out

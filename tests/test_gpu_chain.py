@@ -1,4 +1,4 @@
-"""The persistent single-member factorisation (gpk_tune("chain"), chain_kernel in gpk_potrf.hip; off by default,
+"""The persistent single-member factorisation (gpk_tune("chain"), chain_kernel in gpk_potrf.hip; on by default for single f64 evaluations since it measured faster,
 DESIGN §4) against the launch-per-panel schedule and the oracle (needs the MI355X).
 
 One f64 member without identity / ragged rows runs as ONE launch whose workgroups claim the tasks of
