@@ -185,7 +185,7 @@ Tune& tune() {
                          env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1),
                          env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0),
                          env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024),
-                         env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 4480), env_i64("GPK_CHAIN_GRID", 0),
+                         env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 7424), env_i64("GPK_CHAIN_GRID", 0),
                          env_i64("GPK_CHAIN_TIMEOUT_MS", 1000)};
   return t;
 }

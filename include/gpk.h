@@ -391,7 +391,7 @@ int gpk_timing_reset(void);
  * same bits, slower -- for A/B checks), "trd_split_m" (gpk_syevd: above this m, at most 1024, the
  * tridiagonalisation's A22 v runs over the chip, three launches per column, instead of one workgroup per
  * panel; default 1024), "chain" (1, the default: every f64, batch-1, non-ragged factorisation with at
- * most "chain_max_p" (4480) rows that is not being captured runs as ONE persistent launch --
+ * most "chain_max_p" (7424) rows that is not being captured runs as ONE persistent launch --
  * "chain_grid" workgroups (0: one per CU), every wait bounded by "chain_timeout_ms" (a timeout sets
  * info = -1); callers that overlap factorisations on several streams set 0).
  * Stores the value and returns the previous one through *old (may be NULL); 0 or -1 (unknown

@@ -49,7 +49,7 @@ def _lower(f):
 
 
 @pytest.mark.parametrize("n,m", [(1, 0), (100, 0), (128, 0), (257, 0), (1000, 37), (2048, 0), (3000, 300),
-                                 (4096, 0), (4096, 100)])
+                                 (4096, 0), (4096, 100), (6144, 0)])
 def test_chain_matches_the_launch_path(n, m):
     fc, _ = _run(n, m, 1)
     fl, _ = _run(n, m, 0)
