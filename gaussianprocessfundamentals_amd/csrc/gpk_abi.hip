@@ -321,7 +321,12 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid) {
   std::map<std::tuple<int, int, int>, int> B;
   auto s_of = [&](int k, int r) { return S[(size_t)k * nr + r]; };
   auto u_of = [&](int k, int r) { return U[(size_t)k * nr + r]; };
+  // list-scheduling durations (us) of D / S / U32 / BLK: the measured per-task run times
+  // (profiles/r03p_chain_task_profile_n4096.txt); GPK_CHAIN_DUR="d,s,u,b" overrides them (A/B)
+  float dur[4] = {32.f, 7.f, 10.f, 24.f};
+  if (const char* e = getenv("GPK_CHAIN_DUR")) sscanf(e, "%f,%f,%f,%f", &dur[0], &dur[1], &dur[2], &dur[3]);
   auto add = [&](Task t) {
+    t.dur = dur[t.ty];
     T.push_back(std::move(t));
     return (int)T.size() - 1;
   };
