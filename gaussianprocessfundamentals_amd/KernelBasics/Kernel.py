@@ -107,7 +107,11 @@ class Kernel(bgpc.Component):
         raise _abstract(self, 'get_number_of_child_nodes')
 
     def get_derivative_matrices(self, hyper_parameter: List, x_vector, x_vector_) -> List:
-        raise NotImplementedError("analytic derivative matrices are SURVEY §8f 'next' (LML gradient)")
+        # not rebuilt: nothing in the reference calls them (its fitter differentiates through
+        # tf.linalg.cholesky), SE's is wrong (K/BaseKernels.py:383-399), and the LML gradient is computed by
+        # the fused device pass of gpk_nlml_grad without any dK/dtheta matrix (LogLikelihood.get_metric_and_gradient)
+        raise NotImplementedError("analytic derivative matrices are not provided: use "
+                                  "LogLikelihood.get_metric_and_gradient or autograd through get_metric")
 
     def get_hyper_parameter_names(self, kernel_id: int = -1) -> List[str]:
         raise _abstract(self, 'get_hyper_parameter_names')

@@ -164,6 +164,10 @@ class LogLikelihood(AbstractLogLikelihood):
                                 reset=True)
         f = self.covariance_matrix.inverse_factorization(hyper_parameter, noise, gradient=True,
                                                          y_scale=(1.0 / math.sqrt(B)) if chol else 1.0)
+        # a member that is not positive definite has no gradient here (the reference raises from
+        # tf.linalg.cholesky under CHOLESKY_BASED; the batched STRICT / PSEUDO value needs K^-1 of every
+        # member as well): raise CholeskyError instead of returning NaN gradients beside an +inf value
+        f.check_info()
         g = f.gradient().sum(0)
         if chol:
             g = g * (float(B) if agg is torch.sum else 1.0)

@@ -28,10 +28,10 @@ def _hipcc() -> str:
 
 
 def _inputs():
+    """Every file the build reads: the sources, every header under csrc/ and include/."""
     files = [os.path.join(CSRC, s) for s in SOURCES]
-    files.append(os.path.join(CSRC, "gpk_internal.h"))
-    files.append(os.path.join(CSRC, "gpk_kernels.h"))
-    files.append(os.path.join(INCLUDE, "gpk.h"))
+    for d in (CSRC, INCLUDE):
+        files += sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hpp", ".inc")))
     return files
 
 

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must be loaded first: libgpk binds to torch's HIP r
 
 from . import _build
 
-GPK_ABI_VERSION = 4
+GPK_ABI_VERSION = 5
 GPK_F64, GPK_F32 = 0, 1
 OP_PER, OP_SE, OP_MAT32, OP_MAT52, OP_ADD, OP_MUL = 104, 105, 107, 108, 201, 202
 NODE_SCALED, NODE_ARD, NODE_SE_EXPANDED, NODE_STANDARD = 1, 2, 4, 8
@@ -33,7 +33,7 @@ EXPORTS = (
     "gpk_assemble_dense", "gpk_dgemm", "gpk_syevj_workspace_bytes", "gpk_syevj", "gpk_pinv_factor",
     "gpk_ski_weights", "gpk_add_diagonal", "gpk_distance_matrix", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower", "gpk_trsv_lower", "gpk_posterior",
     "gpk_kernel_vjp_workspace_bytes", "gpk_kernel_vjp", "gpk_pinv_backward_scale", "gpk_syevd_workspace_bytes",
-    "gpk_syevd", "gpk_chain_plan",
+    "gpk_syevd", "gpk_chain_plan", "gpk_tune_thread", "gpk_chain_stats",
 )
 
 
@@ -120,6 +120,8 @@ def _declare(lib):
         "gpk_syevd_workspace_bytes": (c_size_t, [c_int64]),
         "gpk_syevd": (c_int, [c_int64, c_int32, P, c_int64, c_int64, P, P, P, c_size_t, P]),
         "gpk_chain_plan": (c_int, [c_int64, c_int64, c_int32, P, c_int64, POINTER(c_int64)]),
+        "gpk_tune_thread": (c_int, [ctypes.c_char_p, c_int64, c_int32, POINTER(c_int64), POINTER(c_int32)]),
+        "gpk_chain_stats": (c_int, [POINTER(c_int64), c_int32]),
         "gpk_chain_trace": (c_int, [P, c_int64]),
         "gpk_chain_times": (c_int, [P, c_int64]),
         "gpk_kernel_vjp_workspace_bytes": (c_size_t, [POINTER(GpkKdesc), c_int64, c_int64, c_int32, c_int32]),
@@ -203,6 +205,45 @@ def tune(key: str, value: int) -> int:
     old = c_int64(0)
     check(load_library().gpk_tune(key.encode(), int(value), ctypes.byref(old)), "gpk_tune")
     return int(old.value)
+
+
+class thread_tune:
+    """Context manager pinning libgpk knobs for the calling thread only (gpk_tune_thread), e.g.
+    ``with thread_tune(chain=0, lookahead=0): ...``; the thread's previous overrides come back on exit."""
+
+    def __init__(self, **knobs):
+        self.knobs = {k: int(v) for k, v in knobs.items()}
+        self.saved = []
+
+    def __enter__(self):
+        L = load_library()
+        for k, v in self.knobs.items():
+            ov, os_ = c_int64(0), c_int32(0)
+            check(L.gpk_tune_thread(k.encode(), v, 1, ctypes.byref(ov), ctypes.byref(os_)), "gpk_tune_thread")
+            self.saved.append((k, int(ov.value), int(os_.value)))
+        return self
+
+    def __exit__(self, *exc):
+        L = load_library()
+        for k, v, was_set in reversed(self.saved):
+            check(L.gpk_tune_thread(k.encode(), v, was_set, None, None), "gpk_tune_thread")
+        self.saved = []
+        return False
+
+
+def chain_stats() -> dict:
+    """gpk_chain_stats: persistent launches, launch-path decisions while another stream was busy, whether
+    this thread's last factorisation was persistent, forced timeouts pending."""
+    out = (c_int64 * 4)()
+    check(load_library().gpk_chain_stats(out, 4), "gpk_chain_stats")
+    return {"launches": int(out[0]), "declined_busy": int(out[1]), "last_was_chain": bool(out[2]),
+            "forced_pending": int(out[3])}
+
+
+def last_factorisation_was_chain() -> bool:
+    out = (c_int64 * 3)()
+    check(load_library().gpk_chain_stats(out, 3), "gpk_chain_stats")
+    return bool(out[2])
 
 
 def chain_plan(n_pad: int, y_row: int, grid: int):

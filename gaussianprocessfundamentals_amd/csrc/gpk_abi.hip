@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <initializer_list>
 #include <map>
 #include <queue>
@@ -163,7 +164,10 @@ struct Tune {
                           // 2 normal-priority side stream
   int64_t trd_split_m;    // gpk_syevd: above this m the tridiagonalisation's A22 v runs over the chip (three
                           // launches per column) instead of inside one workgroup per panel
-  int64_t chain;          // single f64 factorisations as ONE persistent launch (chain_kernel): 1 on (default: 13 % faster at N = 4096), 0 off
+  int64_t chain;          // single f64 factorisations as ONE persistent launch (chain_kernel): 1 auto (default: on
+                          // unless a factorisation enqueued on another stream of the device is still in flight --
+                          // each persistent launch claims every CU, so overlapped factorisations keep the launch
+                          // path: C2 at 4 in flight 1315 vs 779 evals/s), 2 always, 0 off
   int64_t chain_max_p;    //   ... while the augmented matrix has at most this many rows
   int64_t chain_grid;     //   workgroups of that launch (0: one per CU)
   int64_t chain_timeout_ms;  // bound of every wait inside it (then info = -1)
@@ -187,6 +191,46 @@ Tune& tune() {
                          env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024),
                          env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 7424), env_i64("GPK_CHAIN_GRID", 0),
                          env_i64("GPK_CHAIN_TIMEOUT_MS", 1000)};
+  return t;
+}
+
+// Knob names of gpk_tune / gpk_tune_thread.
+struct Knob {
+  const char* name;
+  int64_t Tune::*field;
+};
+const Knob kKnobs[] = {
+    {"lookahead", &Tune::lookahead},         {"reserve_cus", &Tune::reserve_cus},
+    {"upd_t128_min", &Tune::upd_t128_min},   {"trsm_t128_min", &Tune::trsm_t128_min},
+    {"diag_debug", &Tune::diag_dbg},         {"group", &Tune::group},
+    {"group_first", &Tune::group_first},     {"fuse_kbuild", &Tune::fuse_kbuild},
+    {"upd_band", &Tune::upd_band},           {"skip_zero_rows", &Tune::skip_zero_rows},
+    {"syevj_abs_tol_e3", &Tune::syevj_abs_tol_e3}, {"diag_version", &Tune::diag_version},
+    {"ingroup", &Tune::ingroup},             {"rl_max_tiles", &Tune::rl_max_tiles},
+    {"band_skip", &Tune::band_skip},         {"group_eye", &Tune::group_eye},
+    {"asm_generic", &Tune::asm_generic},     {"panel_stream", &Tune::panel_stream},
+    {"la_min_blocks", &Tune::la_min_blocks}, {"fuse_trsm", &Tune::fuse_trsm},
+    {"fuse_trsm_max", &Tune::fuse_trsm_max}, {"trd_split_m", &Tune::trd_split_m},
+    {"chain", &Tune::chain},                 {"chain_max_p", &Tune::chain_max_p},
+    {"chain_grid", &Tune::chain_grid},       {"chain_timeout_ms", &Tune::chain_timeout_ms},
+};
+
+int64_t Tune::*knob_field(const char* key) {
+  for (const Knob& k : kKnobs)
+    if (!strcmp(key, k.name)) return k.field;
+  return nullptr;
+}
+
+// Per-host-thread overrides (gpk_tune_thread): a caller that runs its own schedule -- e.g. the
+// pipelined sweep's factorisations on several streams -- pins knobs for its own calls without
+// changing them for other threads.
+thread_local std::vector<std::pair<int64_t Tune::*, int64_t>> t_tune_over;
+
+// The knobs in effect for one call on this thread: one snapshot per call, so a gpk_tune from
+// another thread (ctypes releases the GIL during the enqueue) cannot change a decision midway.
+Tune tune_now() {
+  Tune t = tune();
+  for (const auto& o : t_tune_over) t.*(o.first) = o.second;
   return t;
 }
 
@@ -301,7 +345,51 @@ struct ChainPlan {
 };
 std::mutex g_chain_mu;
 std::map<std::tuple<int, int64_t, int64_t, int>, ChainPlan> g_chain_plans;
-std::map<std::pair<int, hipStream_t>, std::pair<int32_t*, size_t>> g_chain_ctl;
+// Counter scratch of the persistent launch, per (host thread, device, stream): the counters are zeroed
+// by a memset enqueued before each launch, so two threads enqueueing on one stream (torch's null stream
+// is shared by every thread) must never share them -- memset A, memset B, launch A, launch B would hand
+// launch B counters already past its task count.  A thread's own calls on one stream are stream-ordered.
+thread_local std::map<std::pair<int, hipStream_t>, std::pair<int32_t*, size_t>> t_chain_ctl;
+std::atomic<int64_t> g_chain_launches{0};      // persistent launches enqueued
+std::atomic<int64_t> g_chain_declined{0};      // auto mode: launch path taken, another stream busy
+std::atomic<int64_t> g_chain_force_timeout{0};  // testing: the next N persistent launches time out
+thread_local bool t_chain_last = false;         // this thread's last factorisation was the persistent one
+
+// Factorisations in flight per (device, stream): an event recorded on the caller's stream after every
+// factorisation this library enqueues.  chain = 1 (auto) takes the launch path while a factorisation on
+// another stream of the device has not finished: the persistent launch claims every CU and would
+// serialise overlapped factorisations (C2 at 4 in flight: 1315 evals/s on the launch path, 779 with
+// persistent launches).
+std::mutex g_busy_mu;
+std::map<std::pair<int, hipStream_t>, hipEvent_t> g_busy;
+
+bool plain_stream(hipStream_t s) {
+  if (s == hipStreamPerThread) return false;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+}
+
+void note_factorisation(hipStream_t s) {
+  int dev = 0;
+  if (!plain_stream(s) || hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lk(g_busy_mu);
+  hipEvent_t& e = g_busy[{dev, s}];
+  if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    e = nullptr;
+    return;
+  }
+  hipEventRecord(e, s);
+}
+
+bool other_stream_busy(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return true;
+  std::lock_guard<std::mutex> lk(g_busy_mu);
+  for (const auto& kv : g_busy)
+    if (kv.first.first == dev && kv.first.second != s && kv.second && hipEventQuery(kv.second) == hipErrorNotReady)
+      return true;
+  return false;
+}
 int32_t* g_chain_trace = nullptr;  // GPK_CHAIN_TRACE=1: pinned host words the kernel writes its progress to
 uint64_t* g_chain_times = nullptr;  // GPK_CHAIN_TIMES=1: device stamps per task of the last profiled launch
 int64_t g_chain_times_n = 0;
@@ -405,9 +493,12 @@ bool chain_applies(const gpk_layout* lay, bool eye, const int64_t* n_dev, const 
                    hipStream_t s) {
   if (!tn.chain || lay->dtype != GPK_F64 || lay->batch != 1 || eye || n_dev || m_dev) return false;
   if (lay->p > tn.chain_max_p || tn.diag_dbg != 0 || tn.diag_version == 1) return false;
-  if (s == hipStreamPerThread) return false;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  return hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+  if (!plain_stream(s)) return false;
+  if (tn.chain == 1 && other_stream_busy(s)) {
+    ++g_chain_declined;
+    return false;
+  }
+  return true;
 }
 
 int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, const Tune& tn, hipStream_t s) {
@@ -436,9 +527,12 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     plan = it->second;
     ctl_ints = 4 + (size_t)plan.nblk + (size_t)plan.nblk * plan.nsl + (size_t)plan.nsl * plan.nbc;
     ctl_ints = (ctl_ints + 3) / 4 * 4;
-    auto& c = g_chain_ctl[{dev, s}];
+  }
+  {
+    auto& c = t_chain_ctl[{dev, s}];  // this thread's own (see t_chain_ctl)
     if (c.second < ctl_ints) {
-      if (c.first) GPK_HIP(hipFree(c.first), "chain scratch");  // (synchronises the device)
+      // (hipFree synchronises the device: no launch of this thread still uses the old block)
+      if (c.first) GPK_HIP(hipFree(c.first), "chain scratch");
       c = {nullptr, 0};
       GPK_HIP(hipMalloc(&c.first, ctl_ints * sizeof(int32_t)), "chain scratch");
       c.second = ctl_ints;
@@ -464,6 +558,11 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.nbc = plan.nbc;
   a.row_end = lay->y_row + 1;
   a.timeout = std::max<int64_t>(1, tn.chain_timeout_ms) * 100000;  // 100 MHz ticks
+  for (int64_t f = g_chain_force_timeout.load(); f > 0;)
+    if (g_chain_force_timeout.compare_exchange_weak(f, f - 1)) {
+      a.force_abort = 1;
+      break;
+    }
   if (env_i64("GPK_CHAIN_TIMES", 0)) {
     std::lock_guard<std::mutex> lk(g_chain_mu);
     if (g_chain_times_n < a.ntasks) {
@@ -481,6 +580,8 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   }
   const double n3 = (double)lay->n_pad;
   GPK_HIP(timed(3, n3 * n3 * n3 / 3.0, 0.0, s, [&] { return launch_chain(a, grid, s); }), "chain");
+  ++g_chain_launches;
+  t_chain_last = true;
   return 0;
 }
 
@@ -545,7 +646,7 @@ static int assemble_impl(const gpk_kdesc* kd, const gpk_layout* lay, const doubl
   if (!W) return fail_arg(15, "W");
   AsmArgs a;
   memset(&a, 0, sizeof(a));
-  a.generic = tune().asm_generic != 0 ? 1 : 0;
+  a.generic = tune_now().asm_generic != 0 ? 1 : 0;
   a.hyp = hyp_dev;
   a.hyp_stride = hyp_stride;
   a.noise = noise_dev;
@@ -630,9 +731,14 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
 
   // one snapshot of the knobs per call: a gpk_tune from another thread (ctypes releases the GIL during
   // the enqueue) must not change the fuse decision between a panel's diag(k) and trsm(k)
-  const Tune tn = tune();
+  const Tune tn = tune_now();
+  t_chain_last = false;
   // a single evaluation: the whole factorisation as one persistent launch (no K build fused into it)
-  if (!kb && chain_applies(lay, eye, n_dev, m_dev, tn, s)) return chain_potrf(lay, W, Winv, info_dev, tn, s);
+  if (!kb && chain_applies(lay, eye, n_dev, m_dev, tn, s)) {
+    const int e = chain_potrf(lay, W, Winv, info_dev, tn, s);
+    if (!e) note_factorisation(s);
+    return e;
+  }
   // The panel chain (diag, panel solve, thin and look-ahead updates) runs on a high-priority
   // stream, the bulk of each trailing update on a CU-masked stream concurrently with the next
   // panel pair's chain; both fork from and join back into the caller's stream.
@@ -874,6 +980,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
     GPK_HIP(hipStreamWaitEvent(s, ss->join_p, 0), "event");
     GPK_HIP(hipStreamWaitEvent(s, ss->join_b, 0), "event");
   }
+  note_factorisation(s);
   return 0;
 }
 
@@ -959,7 +1066,7 @@ int gpk_nlml(const gpk_kdesc* kd, const gpk_layout* lay, const double* hyp_dev, 
   // Fused K build (single-base-node kernels): only the first panel group's block columns are
   // assembled; the first trailing update evaluates its C tiles instead of reading them, so the
   // trailing part of K is never written to HBM and read back.
-  const Tune tn = tune();
+  const Tune tn = tune_now();
   const int64_t nblk = lay->n_pad / NB;
   const int64_t G = std::max<int64_t>(1, std::min<int64_t>(tn.group, 16));
   const int64_t G0 = std::max<int64_t>(1, std::min<int64_t>(tn.group_first, G));
@@ -1430,7 +1537,7 @@ int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
   double host_dmax = 0.0;
   GPK_HIP(hipMemcpyAsync(&host_dmax, dmax, sizeof(double), hipMemcpyDeviceToHost, s), "syevj scale read");
   GPK_HIP(hipStreamSynchronize(s), "syevj sync");
-  const double tol_abs = (double)tune().syevj_abs_tol_e3 * 1e-3 * 2.220446049250313e-16 * host_dmax;
+  const double tol_abs = (double)tune_now().syevj_abs_tol_e3 * 1e-3 * 2.220446049250313e-16 * host_dmax;
   const int mm = (int)(m + (m & 1));
   int cur = 0, sweeps = 0;
   for (; sweeps < (max_sweeps > 0 ? max_sweeps : 60); ++sweeps) {
@@ -1536,7 +1643,7 @@ int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
   if (!work || work_bytes < gpk_syevd_workspace_bytes(m)) return fail_arg(8, "work (gpk_syevd_workspace_bytes)");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   EigWs ws = eig_carve(m, work);
-  const Tune tn = tune();
+  const Tune tn = tune_now();
   const int mi = (int)m;
   const int64_t mm = m * m;
   for (int32_t b = 0; b < batch; ++b) {
@@ -1714,37 +1821,37 @@ int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_ou
 
 int gpk_tune(const char* key, int64_t value, int64_t* old) {
   if (!key) return fail_arg(1, "key");
+  if (!strcmp(key, "chain_force_timeout")) {  // (testing: the next `value` persistent launches time out)
+    const int64_t prev = g_chain_force_timeout.exchange(value);
+    if (old) *old = prev;
+    return 0;
+  }
+  int64_t Tune::*f = knob_field(key);
+  if (!f) return fail_arg(1, "key (unknown tuning knob)");
   Tune& t = tune();
-  int64_t* slot = nullptr;
-  if (!strcmp(key, "lookahead")) slot = &t.lookahead;
-  else if (!strcmp(key, "reserve_cus")) slot = &t.reserve_cus;
-  else if (!strcmp(key, "upd_t128_min")) slot = &t.upd_t128_min;
-  else if (!strcmp(key, "trsm_t128_min")) slot = &t.trsm_t128_min;
-  else if (!strcmp(key, "diag_debug")) slot = &t.diag_dbg;
-  else if (!strcmp(key, "group")) slot = &t.group;
-  else if (!strcmp(key, "group_first")) slot = &t.group_first;
-  else if (!strcmp(key, "fuse_kbuild")) slot = &t.fuse_kbuild;
-  else if (!strcmp(key, "upd_band")) slot = &t.upd_band;
-  else if (!strcmp(key, "skip_zero_rows")) slot = &t.skip_zero_rows;
-  else if (!strcmp(key, "syevj_abs_tol_e3")) slot = &t.syevj_abs_tol_e3;
-  else if (!strcmp(key, "diag_version")) slot = &t.diag_version;
-  else if (!strcmp(key, "ingroup")) slot = &t.ingroup;
-  else if (!strcmp(key, "rl_max_tiles")) slot = &t.rl_max_tiles;
-  else if (!strcmp(key, "band_skip")) slot = &t.band_skip;
-  else if (!strcmp(key, "group_eye")) slot = &t.group_eye;
-  else if (!strcmp(key, "asm_generic")) slot = &t.asm_generic;
-  else if (!strcmp(key, "panel_stream")) slot = &t.panel_stream;
-  else if (!strcmp(key, "la_min_blocks")) slot = &t.la_min_blocks;
-  else if (!strcmp(key, "fuse_trsm")) slot = &t.fuse_trsm;
-  else if (!strcmp(key, "fuse_trsm_max")) slot = &t.fuse_trsm_max;
-  else if (!strcmp(key, "trd_split_m")) slot = &t.trd_split_m;
-  else if (!strcmp(key, "chain")) slot = &t.chain;
-  else if (!strcmp(key, "chain_max_p")) slot = &t.chain_max_p;
-  else if (!strcmp(key, "chain_grid")) slot = &t.chain_grid;
-  else if (!strcmp(key, "chain_timeout_ms")) slot = &t.chain_timeout_ms;
-  if (!slot) return fail_arg(1, "key (unknown tuning knob)");
-  if (old) *old = *slot;
-  *slot = value;
+  if (old) *old = t.*f;
+  t.*f = value;
+  return 0;
+}
+
+int gpk_tune_thread(const char* key, int64_t value, int32_t set, int64_t* old_value, int32_t* old_set) {
+  if (!key) return fail_arg(1, "key");
+  int64_t Tune::*f = knob_field(key);
+  if (!f) return fail_arg(1, "key (unknown tuning knob)");
+  auto it = std::find_if(t_tune_over.begin(), t_tune_over.end(),
+                         [&](const std::pair<int64_t Tune::*, int64_t>& o) { return o.first == f; });
+  if (old_set) *old_set = it != t_tune_over.end() ? 1 : 0;
+  if (old_value) *old_value = it != t_tune_over.end() ? it->second : tune().*f;
+  if (it != t_tune_over.end()) t_tune_over.erase(it);
+  if (set) t_tune_over.emplace_back(f, value);
+  return 0;
+}
+
+int gpk_chain_stats(int64_t* out, int32_t n) {
+  if (!out || n < 1) return fail_arg(1, "out");
+  const int64_t v[4] = {g_chain_launches.load(), g_chain_declined.load(), t_chain_last ? 1 : 0,
+                        g_chain_force_timeout.load()};
+  for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
   return 0;
 }
 

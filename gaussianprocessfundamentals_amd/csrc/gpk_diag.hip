@@ -166,7 +166,6 @@ __global__ __launch_bounds__(DT) void diag2_kernel(DiagArgs a) {
 }  // namespace
 
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s) {
-  static bool attr_done[5] = {false, false, false, false, false};
   const bool v2 = a.version != 1;
   const bool fuse = v2 && dtype == GPK_F64 && a.trsm_tiles > 0;
   const void* fn = fuse ? reinterpret_cast<const void*>(diag2_kernel<double, true>)
@@ -174,20 +173,13 @@ hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t 
                                           : reinterpret_cast<const void*>(diag2_kernel<float, false>))
                       : (dtype == GPK_F64 ? reinterpret_cast<const void*>(diag_kernel<double>)
                                           : reinterpret_cast<const void*>(diag_kernel<float>));
-  bool& done = attr_done[fuse ? 4 : (dtype == GPK_F64 ? 0 : 1) + (v2 ? 2 : 0)];
-  if (!done) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DIAG_LDS_BYTES);
+  {
+    hipError_t e = ensure_dyn_lds(fn, DIAG_LDS_BYTES);
     if (e != hipSuccess) return e;
-    done = true;
   }
   if (a.version == 3 && dtype == GPK_F64 && !fuse) {  // debugging: the write-through (chain_kernel) variant
-    static bool sc1_done = false;
-    if (!sc1_done) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(diag2_kernel<double, false, true>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)DIAG_LDS_BYTES);
-      if (e != hipSuccess) return e;
-      sc1_done = true;
-    }
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(diag2_kernel<double, false, true>), DIAG_LDS_BYTES);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((diag2_kernel<double, false, true>), dim3(batch), dim3(DT), DIAG_LDS_BYTES, s, a);
   } else if (fuse) {
     hipLaunchKernelGGL((diag2_kernel<double, true>), dim3(a.trsm_tiles + 1, batch), dim3(DT), DIAG_LDS_BYTES, s, a);

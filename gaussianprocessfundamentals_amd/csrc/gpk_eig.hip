@@ -753,13 +753,9 @@ static size_t trd_panel_lds(int m) { return sizeof(double) * (18 * (size_t)m + 4
 
 hipError_t launch_eig_tridiag(double* W, int m, double* d, double* e, double* tau, double* PV, double* vg,
                               double* yg, int split_m, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(trd_panel_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)trd_panel_lds(TRD_PANEL_MAX_M));
+  {
+    hipError_t err = ensure_dyn_lds(reinterpret_cast<const void*>(trd_panel_kernel), trd_panel_lds(TRD_PANEL_MAX_M));
     if (err != hipSuccess) return err;
-    attr = true;
   }
   static unsigned long long* prof = nullptr;
   if (getenv("GPK_TRD_PROF") && !prof) {
@@ -812,15 +808,10 @@ static size_t dc_deflate_lds(int k) {
 
 hipError_t launch_eig_dc(const double* d, const double* e, int m, const DcLevel& L, double* Q, double* Qg, double* U,
                          hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(dc_deflate_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)dc_deflate_lds(4096));
-    if (err == hipSuccess)
-      err = hipFuncSetAttribute(reinterpret_cast<const void*>(dc_gather_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 8);
+  {
+    hipError_t err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_deflate_kernel), dc_deflate_lds(4096));
+    if (err == hipSuccess) err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_gather_kernel), 4096 * 8);
     if (err != hipSuccess) return err;
-    attr = true;
   }
   const int64_t mm = (int64_t)m * m;
   hipLaunchKernelGGL(dc_init_kernel, dim3((unsigned)((mm + 255) / 256)), dim3(256), 0, s, d, e, m, L.lam, Q);
@@ -882,14 +873,11 @@ bool eig_bt_fused(int m) { return m <= BT_MAX_M; }
 
 hipError_t launch_eig_backtransform(const double* W, const double* tau, int m, double* Sall, double* V,
                                     hipStream_t s) {
-  static bool attr = false;
   const size_t lds = sizeof(double) * ((size_t)BT_MAX_M * BT_CW + BT_RC * (BT_NB + 1) + 2 * BT_NB * BT_CW +
                                        BT_NB * BT_NB);
-  if (!attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(bt_apply_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  {
+    hipError_t err = ensure_dyn_lds(reinterpret_cast<const void*>(bt_apply_kernel), lds);
     if (err != hipSuccess) return err;
-    attr = true;
   }
   const int nblk = (m - 1 + BT_NB - 1) / BT_NB;
   if (nblk == 0) return hipSuccess;

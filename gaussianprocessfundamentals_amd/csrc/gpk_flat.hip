@@ -114,12 +114,9 @@ hipError_t launch_unpack_lower(int dtype, const void* W, int64_t ld, int64_t n, 
 size_t trtri_blocks_lds() { return sizeof(double) * ((size_t)NB * (NB + 1) / 2 + (size_t)NB * 64); }
 
 hipError_t launch_trtri_blocks(const double* L, int64_t ldl, int64_t n, double* Winv, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(trtri_blocks_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)trtri_blocks_lds());
+  {
+    hipError_t err = ensure_dyn_lds(reinterpret_cast<const void*>(trtri_blocks_kernel), trtri_blocks_lds());
     if (err != hipSuccess) return err;
-    attr = true;
   }
   const int64_t nblk = (n + NB - 1) / NB;
   hipLaunchKernelGGL(trtri_blocks_kernel, dim3((unsigned)(2 * nblk)), dim3(64), trtri_blocks_lds(), s, L, ldl, n, Winv);

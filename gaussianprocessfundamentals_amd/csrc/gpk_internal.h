@@ -4,12 +4,32 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <set>
+#include <tuple>
+
 #include "gpk.h"
 
 namespace gpk {
 
 constexpr int NB = 128;     // panel width == update tile edge == diagonal block edge
 constexpr int ATILE = 64;   // assemble tile edge
+
+// Dynamic LDS above 64 KB needs hipFuncAttributeMaxDynamicSharedMemorySize, which is a per-device
+// attribute of the kernel: set it once per (device, kernel, size) before the first launch on a device.
+inline hipError_t ensure_dyn_lds(const void* fn, size_t bytes) {
+  static std::mutex mu;
+  static std::set<std::tuple<int, const void*, size_t>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_tuple(dev, fn, bytes);
+  if (done.count(key)) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) done.insert(key);
+  return e;
+}
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -137,6 +157,7 @@ struct ChainArgs {
   int64_t timeout;       // per wait, in s_memrealtime ticks (100 MHz)
   int32_t* trace;        // debugging (GPK_CHAIN_TRACE=1, else NULL): host-visible [grid][32] progress words
   int32_t dbg;           // debugging (GPK_CHAIN_DBG): 4 = one diagonal task alone (chain_d_only_kernel)
+  int32_t force_abort;   // testing (gpk_tune "chain_force_timeout"): the first wait reports a timeout
   uint64_t* times;       // profiling (GPK_CHAIN_TIMES=1, else NULL): per task [claimed, inputs ready, wave 0's body done, published, S / U32: loads returned, MFMAs retired] (100 MHz)
 };
 

@@ -663,9 +663,9 @@ __device__ __forceinline__ void st_flag(int32_t* p, int32_t v) {
 // wave 0: wait until *p >= v; false on timeout (which it reports) or after another task's timeout
 __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p, int32_t v, uint64_t t0) {
   // (polled values through readfirstlane: the loop is wave-uniform, as every branch of chain_kernel)
-  while (__builtin_amdgcn_readfirstlane(ld_flag(p)) < v) {
+  while (a.force_abort || __builtin_amdgcn_readfirstlane(ld_flag(p)) < v) {
     if (__builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) return false;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout) {
+    if (a.force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout) {
       st_flag(a.ctl + 1, 1);
       int32_t zero = 0;
       __hip_atomic_compare_exchange_strong((gi32*)a.info, &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
@@ -1093,22 +1093,14 @@ __global__ __launch_bounds__(DT) void chain_d_only_kernel(ChainArgs a) {  // (de
 
 hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {
   if (a.dbg == 4) {
-    static bool d4 = false;
-    if (!d4) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(chain_d_only_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS_BYTES);
-      if (e != hipSuccess) return e;
-      d4 = true;
-    }
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(chain_d_only_kernel), CHAIN_LDS_BYTES);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(chain_d_only_kernel, dim3(1), dim3(DT), CHAIN_LDS_BYTES, s, a);
     return hipGetLastError();
   }
-  static bool attr_done = false;
-  if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(chain_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS_BYTES);
+  {
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(chain_kernel), CHAIN_LDS_BYTES);
     if (e != hipSuccess) return e;
-    attr_done = true;
   }
   hipLaunchKernelGGL(chain_kernel, dim3(grid), dim3(DT), CHAIN_LDS_BYTES, s, a);
   return hipGetLastError();

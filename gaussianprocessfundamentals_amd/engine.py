@@ -12,12 +12,23 @@ All arithmetic runs in libgpk on the GPU; torch only allocates and views device 
 from __future__ import annotations
 
 import ctypes
+import logging
 from typing import List, Optional, Sequence
 
 import torch
 
 from . import _native as nat
 from . import global_parameters as gp
+
+# A single f64 factorisation may run as ONE persistent launch (gpk_tune "chain", include/gpk.h).  Its
+# inter-workgroup waits are bounded; a wait that times out (the device shared with another process past
+# chain_timeout_ms, a preempted workgroup) leaves info = -1 and the factorisation incomplete.  With
+# CHAIN_VERIFY (default) every run that took the persistent launch reads its info back (one 4-byte
+# device-to-host copy) and, on -1, assembles and factors again on the launch path in the same call;
+# CHAIN_FALLBACKS counts those re-runs.  The reference's tf.linalg.cholesky never fails spuriously
+# (gpbasics/Statistics/CovarianceMatrix.py:250), so neither may this.
+CHAIN_VERIFY = True
+CHAIN_FALLBACKS = 0
 
 
 class CholeskyError(RuntimeError):
@@ -174,10 +185,31 @@ class AugmentedFactorization:
         self.shape_key = None
 
     # -- launches ---------------------------------------------------------------------------
+    def _verify_chain(self, rerun) -> None:
+        """After a run: if libgpk took the persistent launch for it and a wait timed out (info = -1), run
+        it again on the launch path (same call, same buffers) and count the fallback."""
+        global CHAIN_FALLBACKS
+        if not CHAIN_VERIFY or not nat.last_factorisation_was_chain():
+            return
+        if int(self.info[0]) != -1:   # (synchronises the stream)
+            return
+        CHAIN_FALLBACKS += 1
+        logging.warning("persistent factorisation timed out (gpk_tune chain_timeout_ms): re-running it on the "
+                        "launch path (%d fallbacks so far)", CHAIN_FALLBACKS)
+        with nat.thread_tune(chain=0):
+            rerun()
+
     def run(self, kd: nat.GpkKdesc, hyp: torch.Tensor, hyp_stride: int, noise: torch.Tensor,
             noise_stride: int, X: torch.Tensor, x_bstride: int, y: torch.Tensor, y_bstride: int,
             Xs: Optional[torch.Tensor] = None, xs_bstride: int = 0,
             E: Optional[torch.Tensor] = None, e_bstride: int = 0):
+        args = (kd, hyp, hyp_stride, noise, noise_stride, X, x_bstride, y, y_bstride, Xs, xs_bstride, E, e_bstride)
+        self._run_once(*args)
+        self._verify_chain(lambda: self._run_once(*args))
+        return self
+
+    def _run_once(self, kd, hyp, hyp_stride, noise, noise_stride, X, x_bstride, y, y_bstride, Xs, xs_bstride,
+                  E, e_bstride):
         lay = self.layout
         B, n, m, d = self.batch, self.n, self.m, self.d
         self._alphas = None
@@ -281,6 +313,8 @@ class AugmentedFactorization:
         bad = torch.nonzero(info).flatten()
         if bad.numel():
             if int(info[bad[0]]) < 0:
+                # (run() re-runs a timed-out persistent launch on the launch path, so this is reached only
+                # with CHAIN_VERIFY off: an infrastructure failure, never "not positive definite")
                 raise RuntimeError("device factorisation aborted: a wait of the persistent factorisation timed "
                                    "out (gpk_tune chain_timeout_ms)")
             raise CholeskyError(int(info[bad[0]]))
@@ -572,9 +606,9 @@ def syevj(A: torch.Tensor, max_sweeps: int = 60):
 
 def syevd(A: torch.Tensor):
     """Eigendecomposition of a symmetric [m, m] (or [B, m, m]) device matrix by the tridiagonal route
-    (gpk_syevd: Householder tridiagonalisation, compact-WY Q, implicit QL): returns (lam, V with the
-    eigenvectors in its columns), eigenvalues in no particular order.  m > 4096 or a QL iteration that does
-    not converge go to the Jacobi solver (gpk_syevj)."""
+    (gpk_syevd: blocked Householder tridiagonalisation, divide and conquer on the tridiagonal matrix,
+    compact-WY back-transformation): returns (lam, V with the eigenvectors in its columns), eigenvalues in no
+    particular order.  m > 4096 goes to the Jacobi solver (gpk_syevj)."""
     A3, lda, abs_ = _mat_args(A, "A")
     batch, m = A3.shape[0], A3.shape[1]
     if A3.shape[2] != m:
@@ -587,12 +621,8 @@ def syevd(A: torch.Tensor):
     lam = torch.empty((batch, m), dtype=torch.float64, device=A.device)
     wb = int(L.gpk_syevd_workspace_bytes(m))
     work = torch.empty(max(1, (wb + 7) // 8), dtype=torch.float64, device=A.device)
-    rc = L.gpk_syevd(m, batch, nat.ptr(A3), lda, abs_, nat.ptr(V), nat.ptr(lam), nat.ptr(work), wb,
-                     nat.stream_handle(A.device))
-    if rc > 1000:
-        lam, V, _ = syevj(A)
-        return lam, V
-    nat.check(rc, "gpk_syevd")
+    nat.check(L.gpk_syevd(m, batch, nat.ptr(A3), lda, abs_, nat.ptr(V), nat.ptr(lam), nat.ptr(work), wb,
+                          nat.stream_handle(A.device)), "gpk_syevd")
     if A.dim() == 2:
         return lam[0], V[0]
     return lam, V
@@ -714,6 +744,11 @@ class DenseFactorization(AugmentedFactorization):
         super().__init__(n, 1, n if inverse else m, batch, torch.float64)
 
     def run(self, A: torch.Tensor, noise, y: Optional[torch.Tensor] = None, E: Optional[torch.Tensor] = None):
+        self._run_once(A, noise, y, E)
+        self._verify_chain(lambda: self._run_once(A, noise, y, E))
+        return self
+
+    def _run_once(self, A, noise, y, E):
         A3, lda, abs_ = _mat_args(A, "A")
         B, n = self.batch, self.n
         if A3.shape[1] < n or A3.shape[2] < n or A3.shape[0] not in (1, B):

@@ -65,16 +65,13 @@ def native_batched_evaluator(kernel, X: torch.Tensor, y: torch.Tensor, noise, dt
         slots = [caller] + streams
         for st in streams:
             st.wait_stream(caller)
-        old_la = old_fuse = old_chain = None
-        if P > 1:
-            # the chunks' factorisations overlap on P streams: no look-ahead side streams, and no panel
-            # solve fused into the diagonal-block launch (its redundant workgroups would take CUs from
-            # the other chunks' updates: C5 38.2 -> 36.4 evals/s at 3 in flight)
-            from . import _native as nat
-            old_la = nat.tune("lookahead", 0)
-            old_fuse = nat.tune("fuse_trsm", 0)
-            old_chain = nat.tune("chain", 0)  # (a persistent launch per chunk would claim every CU)
-        try:
+        # the chunks' factorisations overlap on P streams: no look-ahead side streams, no panel solve fused
+        # into the diagonal-block launch (its redundant workgroups would take CUs from the other chunks'
+        # updates: C5 38.2 -> 36.4 evals/s at 3 in flight) and no persistent launch (it would claim every
+        # CU) -- pinned for this thread's calls only (gpk_tune_thread), not for other threads
+        from . import _native as nat
+        knobs = nat.thread_tune(lookahead=0, fuse_trsm=0, chain=0) if P > 1 else nat.thread_tune()
+        with knobs:
             for i, s0 in enumerate(range(0, c, step)):
                 s1 = min(c, s0 + step)
                 b = s1 - s0
@@ -87,11 +84,6 @@ def native_batched_evaluator(kernel, X: torch.Tensor, y: torch.Tensor, noise, dt
                     f.run(kd, cands[s0:s1], kd.n_hyp, nv, 0, X, 0, yv, 0)
                     out[s0:s1, 0] = f.nlml()
                     out[s0:s1, 1] = f.info.to(torch.float64)
-        finally:
-            if old_la is not None:
-                nat.tune("lookahead", old_la)
-                nat.tune("fuse_trsm", old_fuse)
-                nat.tune("chain", old_chain)
         for st in streams:
             caller.wait_stream(st)
         return out

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define GPK_ABI_VERSION 4
+#define GPK_ABI_VERSION 5
 
 /* arithmetic types of the factorisation */
 enum { GPK_F64 = 0, GPK_F32 = 1 };
@@ -390,13 +390,30 @@ int gpk_timing_reset(void);
  * "asm_generic" (1: the K build's interior tiles through the generic per-element loop as well; the
  * same bits, slower -- for A/B checks), "trd_split_m" (gpk_syevd: above this m, at most 1024, the
  * tridiagonalisation's A22 v runs over the chip, three launches per column, instead of one workgroup per
- * panel; default 1024), "chain" (1, the default: every f64, batch-1, non-ragged factorisation with at
- * most "chain_max_p" (7424) rows that is not being captured runs as ONE persistent launch --
- * "chain_grid" workgroups (0: one per CU), every wait bounded by "chain_timeout_ms" (a timeout sets
- * info = -1); callers that overlap factorisations on several streams set 0).
+ * panel; default 1024), "chain" (every f64, batch-1, non-ragged factorisation with at most
+ * "chain_max_p" (7424) rows that is not being captured runs as ONE persistent launch -- "chain_grid"
+ * workgroups (0: one per CU), every wait bounded by "chain_timeout_ms": 1, the default, auto: unless a
+ * factorisation this library enqueued on another stream of the device is still in flight (each
+ * persistent launch claims every CU); 2 always; 0 never).  A persistent launch whose wait timed out
+ * sets info = -1 -- an infrastructure failure, not a non-positive pivot: the factorisation is
+ * incomplete and W undefined; re-assemble and re-run it with "chain" 0 (the Python layer does,
+ * engine.AugmentedFactorization).  "chain_force_timeout" (testing) makes the next `value` persistent
+ * launches report a timeout at their first wait.
  * Stores the value and returns the previous one through *old (may be NULL); 0 or -1 (unknown
  * key).  Defaults come from the environment (GPK_LOOKAHEAD, GPK_RESERVE_CUS, ...). */
 int gpk_tune(const char* key, int64_t value, int64_t* old);
+
+/* Per-host-thread override of a gpk_tune knob (no reference counterpart): set = 1 pins `value` for
+ * the calls of the calling thread only, set = 0 removes the thread's override (the global knob applies
+ * again).  *old_value / *old_set (may be NULL) return the override in effect before the call (old_set
+ * 0: none, *old_value is then the global value).  0 or -1 (unknown key). */
+int gpk_tune_thread(const char* key, int64_t value, int32_t set, int64_t* old_value, int32_t* old_set);
+
+/* Counters of the persistent factorisation: out[0] persistent launches enqueued (all threads),
+ * out[1] factorisations that took the launch path because another stream was busy (chain = 1),
+ * out[2] 1 if the calling thread's last factorisation was a persistent launch (its info must then be
+ * checked for -1, see gpk_tune "chain"), out[3] forced timeouts still pending.  Writes min(n, 4). */
+int gpk_chain_stats(int64_t* out, int32_t n);
 
 /* The task list of the persistent single-member factorisation (gpk_tune "chain"; no reference
  * counterpart): the order in which the workgroups of its one launch claim the tasks, for an augmented

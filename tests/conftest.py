@@ -39,9 +39,9 @@ def _reset_globals():
 # Modules that test the launch path's own schedules (fused panel solve, diagonal-kernel versions, K-build
 # variants, group / look-ahead / fused-K-build knobs, gradient schedules) against each other, often bit for
 # bit: the persistent factorisation (on by default for single f64 evaluations) would stand in for both
-# sides, so they run with it off; tests/test_gpu_chain.py compares it with the launch path and the oracle.
-_LAUNCH_PATH_MODULES = {"test_gpu_fused_panel", "test_gpu_diag_versions", "test_gpu_kbuild", "test_gpu_parity",
-                        "test_gpu_grad"}
+# sides, so they run with it off.  tests/test_gpu_parity.py runs its golden-fixture and size tests through
+# BOTH paths (fixture `factor_path`), tests/test_gpu_chain.py compares the two paths with each other.
+_LAUNCH_PATH_MODULES = {"test_gpu_fused_panel", "test_gpu_diag_versions", "test_gpu_kbuild", "test_gpu_grad"}
 
 
 @pytest.fixture(autouse=True)
@@ -56,3 +56,20 @@ def _launch_path_only(request):
         yield
     finally:
         nat.tune("chain", old)
+
+
+@pytest.fixture(params=["launch", "chain"])
+def factor_path(request):
+    """Single f64 factorisations through the launch-per-panel path (gpk_tune chain 0) or the persistent
+    launch (chain 2: always, even if another stream still has work in flight).  Yields the path name;
+    the chain variant asserts on exit that the persistent launch really ran."""
+    from gaussianprocessfundamentals_amd import _native as nat
+    mode = 0 if request.param == "launch" else 2
+    before = nat.chain_stats()["launches"]
+    with nat.thread_tune(chain=mode):
+        yield request.param
+    launched = nat.chain_stats()["launches"] - before
+    if request.param == "chain":
+        assert launched > 0, "the persistent factorisation did not run"
+    else:
+        assert launched == 0

@@ -94,3 +94,34 @@ def test_tune_keys_and_scheduling_defaults(lib):
     assert out.stdout.strip().splitlines()[-1] == "[2, 64, 1, 256, 0]"
     with pytest.raises(Exception):
         _native.tune("no_such_knob", 1)
+
+
+def test_thread_tune_is_per_thread(lib):
+    """gpk_tune_thread pins a knob for the calling thread only (host-only calls): another thread still sees
+    the global value, and leaving the context restores the thread's previous state."""
+    import ctypes
+    import threading
+
+    def probe():
+        ov, os_ = ctypes.c_int64(0), ctypes.c_int32(0)
+        _native.check(lib.gpk_tune_thread(b"chain", 123, 1, ctypes.byref(ov), ctypes.byref(os_)), "probe")
+        _native.check(lib.gpk_tune_thread(b"chain", ov.value, os_.value, None, None), "probe")  # restore
+        return int(ov.value), int(os_.value)
+
+    glob = _native.tune("chain", 1)
+    _native.tune("chain", glob)
+    with _native.thread_tune(chain=0, lookahead=0):
+        assert probe() == (0, 1)        # this thread: overridden
+        seen = []
+        t = threading.Thread(target=lambda: seen.append(probe()))
+        t.start()
+        t.join()
+        assert seen == [(glob, 0)]      # another thread: the global value, no override
+        with _native.thread_tune(chain=2):
+            assert probe() == (2, 1)
+        assert probe() == (0, 1)        # nested context restored
+    assert probe() == (glob, 0)
+    assert _native.chain_stats()["launches"] == 0
+    with pytest.raises(Exception):
+        with _native.thread_tune(no_such_knob=1):
+            pass

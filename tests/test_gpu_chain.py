@@ -2,11 +2,15 @@
 DESIGN §4) against the launch-per-panel schedule and the oracle (needs the MI355X).
 
 One f64 member without identity / ragged rows runs as ONE launch whose workgroups claim the tasks of
-gpk_chain_plan (tests/test_chain_plan.py checks that list on the host).  Its trailing updates apply one
-panel at a time where the launch path groups eight, so the two agree to summation order, not bit for
-bit: L and the read-outs to ~1e-13 relative here.  Between runs of the chain itself the arithmetic order
-is fixed (every tile's updates are serialised by its counter), so repeated runs are bitwise equal.
+gpk_chain_plan (tests/test_chain_plan.py checks that list on the host).  Contract with the launch path:
+agreement to 1e-12 relative in L, z, -LML, mu and Sigma at every size up to the chain_max_p edge (N = 7296:
+7424 augmented rows), at the reference's 1e-8 jitter as well; test_chain_bitwise_vs_launch_path records
+whether the two are also bit-identical.  Between runs of the chain itself the arithmetic order is fixed
+(every tile's updates are serialised by its counter), so repeated runs are bitwise equal.  A wait that
+times out is recovered in the same call on the launch path (engine.AugmentedFactorization._verify_chain).
 """
+import threading
+
 import numpy as np
 import pytest
 import torch
@@ -30,15 +34,13 @@ def _run(n, m, chain, hyp=0.1, noise=1e-2, seed=3, sync=True):
     X = torch.tensor(x, dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
     Y = torch.tensor(y, dtype=torch.float64, device=dev).reshape(1, -1).contiguous()
     Xs = torch.linspace(-0.1, 1.1, max(m, 1), dtype=torch.float64, device=dev).reshape(-1, 1) if m else None
-    old = engine.nat.tune("chain", chain)
-    try:
+    # chain 1 -> 2: the persistent launch even if another stream still has work in flight
+    with engine.nat.thread_tune(chain=2 if chain else 0):
         f = engine.AugmentedFactorization(n, 1, m, 1)
         f.W.zero_()
         f.run(kd, H, 1, NZ, 0, X, 0, Y, 0, Xs, 0)
         if sync:
             torch.cuda.synchronize()
-    finally:
-        engine.nat.tune("chain", old)
     return f, (x, y)
 
 
@@ -48,11 +50,14 @@ def _lower(f):
     return np.tril(w[: lay.y_row + 1, : lay.y_row + 1])
 
 
-@pytest.mark.parametrize("n,m", [(1, 0), (100, 0), (128, 0), (257, 0), (1000, 37), (2048, 0), (3000, 300),
-                                 (4096, 0), (4096, 100), (6144, 0)])
-def test_chain_matches_the_launch_path(n, m):
-    fc, _ = _run(n, m, 1)
-    fl, _ = _run(n, m, 0)
+@pytest.mark.parametrize("n,m,noise", [(1, 0, 1e-2), (100, 0, 1e-2), (128, 0, 1e-2), (257, 0, 1e-2),
+                                       (1000, 37, 1e-2), (2048, 0, 1e-2), (3000, 300, 1e-2), (4096, 0, 1e-2),
+                                       (4096, 100, 1e-2), (6144, 0, 1e-2), (7168, 0, 1e-2), (7168, 100, 1e-2),
+                                       (7296, 0, 1e-2), (1000, 0, 1e-8), (4096, 0, 1e-8)])
+def test_chain_matches_the_launch_path(n, m, noise):
+    fc, _ = _run(n, m, 1, noise=noise)
+    fl, _ = _run(n, m, 0, noise=noise)
+    assert fc.layout.p <= 7424  # (inside chain_max_p: the persistent launch ran)
     assert int(fc.info.cpu()[0]) == 0 and int(fl.info.cpu()[0]) == 0
     a, b = _lower(fc), _lower(fl)
     scale = np.abs(b).max()
@@ -64,7 +69,26 @@ def test_chain_matches_the_launch_path(n, m):
         np.testing.assert_allclose(fc.var.cpu().numpy(), fl.var.cpu().numpy(), rtol=0, atol=1e-10)
 
 
-@pytest.mark.parametrize("n", [300, 4096])
+@pytest.mark.parametrize("n,m", [(257, 0), (3000, 300), (4096, 0), (7296, 0)])
+def test_chain_bitwise_vs_launch_path(n, m):
+    """Same MFMA k-order in every tile update and panel solve, and an f64 accumulator stored and reloaded
+    between panels rounds nothing: the persistent launch reproduces the launch path bit for bit."""
+    fc, _ = _run(n, m, 1)
+    fl, _ = _run(n, m, 0)
+    a, b = _lower(fc), _lower(fl)
+    diff = int(np.count_nonzero(a.view(np.uint64) != b.view(np.uint64)))
+    assert diff == 0, "%d of %d lower-triangle words differ" % (diff, a.size)
+    assert fc.out.cpu()[0].item() == fl.out.cpu()[0].item()
+
+
+def test_chain_noise_1e8_matches_the_oracle():
+    """The reference's default jitter (1e-8, cond(K) ~ 1e10 at N = 256) through the persistent launch."""
+    f, (x, y) = _run(1000, 0, 1, noise=1e-8)
+    ref = o.nlml(SE, [0.1], 1e-8, x, y)
+    assert float(f.nlml().cpu()[0]) == pytest.approx(ref, rel=1e-6)
+
+
+@pytest.mark.parametrize("n", [300, 4096, 7296])
 def test_chain_nlml_matches_the_oracle(n):
     f, (x, y) = _run(n, 0, 1)
     ref = o.nlml(SE, [0.1], 1e-2, x, y)
@@ -108,3 +132,113 @@ def test_chain_on_concurrent_streams():
     torch.cuda.synchronize()
     for n in (1500, 2600):
         assert np.array_equal(_lower(out[n]).view(np.uint64), ref[n].view(np.uint64))
+
+
+def test_timed_out_wait_falls_back_to_the_launch_path():
+    """gpk_tune("chain_force_timeout", 1): the next persistent launch reports a timeout at its first wait
+    (info = -1, W left half factored).  The same run() call re-assembles and factors on the launch path and
+    counts the fallback; the result is the oracle's -LML."""
+    before = engine.CHAIN_FALLBACKS
+    engine.nat.tune("chain_force_timeout", 1)
+    try:
+        f, (x, y) = _run(2000, 0, 1)
+    finally:
+        engine.nat.tune("chain_force_timeout", 0)
+    assert engine.CHAIN_FALLBACKS == before + 1
+    assert int(f.info.cpu()[0]) == 0
+    assert float(f.nlml().cpu()[0]) == pytest.approx(o.nlml(SE, [0.1], 1e-2, x, y), rel=1e-9)
+    # with verification off the timeout surfaces as an infrastructure error, never as "not PD"
+    engine.CHAIN_VERIFY = False
+    engine.nat.tune("chain_force_timeout", 1)
+    try:
+        f, _ = _run(2000, 0, 1)
+        assert int(f.info.cpu()[0]) == -1
+        with pytest.raises(RuntimeError, match="timed out"):
+            f.check_info()
+    finally:
+        engine.CHAIN_VERIFY = True
+        engine.nat.tune("chain_force_timeout", 0)
+
+
+def test_timed_out_wait_through_get_metric():
+    """The drop-in API: get_metric / get_metric_checked give the oracle value although the persistent launch
+    behind them timed out."""
+    from gaussianprocessfundamentals_amd.DataHandling.DataInput import DataInput
+    from gaussianprocessfundamentals_amd.Metrics.Auxiliary import get_metric_by_type
+    from gaussianprocessfundamentals_amd.Metrics.Metrics import MetricType
+    from gaussianprocessfundamentals_amd.MeanFunctionBasics.BaseMeanFunctions import ZeroMeanFunction
+    from gaussianprocessfundamentals_amd.Statistics.GaussianProcess import GaussianProcess
+    x, y = o.make_inputs("C1", n=1500, seed=8)
+    di = DataInput(x.reshape(-1, 1), y.reshape(-1, 1), x.reshape(-1, 1), y.reshape(-1, 1))
+    di.set_mean_function(ZeroMeanFunction(1))
+    g = GaussianProcess(make_kernel(SE, 1), ZeroMeanFunction(1))
+    g.set_data_input(di)
+    met = get_metric_by_type(MetricType.LL, g)
+    before = engine.CHAIN_FALLBACKS
+    engine.nat.tune("chain_force_timeout", 1)
+    try:
+        with engine.nat.thread_tune(chain=2):
+            got = float(met.get_metric_checked([torch.tensor(0.1, dtype=torch.float64)],
+                                               torch.tensor(1e-2, dtype=torch.float64)))
+    finally:
+        engine.nat.tune("chain_force_timeout", 0)
+    assert engine.CHAIN_FALLBACKS == before + 1
+    assert got == pytest.approx(o.nlml(SE, [0.1], 1e-2, x, y), rel=1e-9)
+
+
+def test_two_host_threads_on_the_default_stream():
+    """Two Python threads (ctypes releases the GIL) run single f64 evaluations of different sizes on the same
+    default stream: each thread's persistent launches use their own counter scratch, so every result is
+    bitwise the launch path's result for its size."""
+    sizes = (1500, 2600)
+    ref = {n: _lower(_run(n, 0, 0, hyp=0.05 + 1e-4 * n)[0]) for n in sizes}
+    out, errors = {}, []
+
+    def work(n):
+        try:
+            for rep in range(6):
+                f = _run(n, 0, 1, hyp=0.05 + 1e-4 * n, sync=False)[0]
+                out[(n, rep)] = f
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    ts = [threading.Thread(target=work, args=(n,)) for n in sizes]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for (n, rep), f in out.items():
+        assert int(f.info.cpu()[0]) == 0
+        assert np.array_equal(_lower(f).view(np.uint64), ref[n].view(np.uint64)), (n, rep)
+
+
+def test_auto_mode_declines_while_another_stream_is_busy():
+    """chain = 1 (auto): while a factorisation enqueued on another stream is still running, a single f64
+    evaluation takes the launch path (the persistent launch would claim every CU); once the device is idle
+    it takes the persistent launch again."""
+    dev = engine.device()
+    kd = engine.kernel_descriptor(make_kernel(SE, 1), 1)
+    x, y = o.make_inputs("C1", n=4096, seed=3)
+    X = torch.tensor(x, dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+    Y = torch.tensor(y, dtype=torch.float64, device=dev).reshape(1, -1).contiguous()
+    NZ = torch.tensor([1e-2], dtype=torch.float64, device=dev)
+    big = engine.AugmentedFactorization(4096, 1, 0, 16)
+    Hb = torch.linspace(0.05, 0.2, 16, dtype=torch.float64, device=dev).reshape(16, 1).contiguous()
+    H = torch.tensor([[0.1]], dtype=torch.float64, device=dev)
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with engine.nat.thread_tune(chain=1):
+        with torch.cuda.stream(side):
+            big.run(kd, Hb, 1, NZ, 0, X, 0, Y, 0)     # ~10 ms of work on the side stream
+        s0 = engine.nat.chain_stats()
+        one = engine.AugmentedFactorization(4096, 1, 0, 1)
+        one.run(kd, H, 1, NZ, 0, X, 0, Y, 0)            # default stream, side stream still busy
+        s1 = engine.nat.chain_stats()
+        torch.cuda.synchronize()
+        one.run(kd, H, 1, NZ, 0, X, 0, Y, 0)            # idle device
+        s2 = engine.nat.chain_stats()
+    assert s1["declined_busy"] > s0["declined_busy"] and s1["launches"] == s0["launches"]
+    assert s2["launches"] == s1["launches"] + 1 and s2["last_was_chain"]
+    assert float(one.nlml().cpu()[0]) == pytest.approx(o.nlml(SE, [0.1], 1e-2, x, y), rel=1e-9)

@@ -114,3 +114,18 @@ def test_lcg_gradient_matches_oracle(noise):
     _close([float(h[0].grad), float(nz.grad)], [float(gh[0]), gn], 1e-6)
     v, g2, gn2 = met.get_metric_and_gradient(hyp_list([0.1]), torch.tensor(noise, dtype=F64))
     _close([float(g2[0]), float(gn2)], [float(gh[0]), gn], 1e-6)
+
+
+@pytest.mark.parametrize("handling", [H.CHOLESKY_BASED, H.STRICT_INVERSE])
+def test_batch_gradient_with_an_indefinite_member_raises(handling):
+    """BatchDataInput whose second member is not positive definite at noise -0.05 (dense SE inputs) while the
+    first is (points 10 apart, K ~ I): the batched gradient raises CholeskyError -- as the reference's
+    tf.linalg.cholesky does -- instead of returning NaN gradients beside an +inf value."""
+    from gaussianprocessfundamentals_amd.engine import CholeskyError
+    n = 120
+    xb = np.stack([np.arange(n, dtype=np.float64).reshape(-1, 1) * 10.0,
+                   np.sort(np.random.default_rng(2).uniform(0, 1, (n, 1)), axis=0)])
+    yb = np.sin(3 * xb[..., 0])
+    met = get_metric_by_type(MetricType.LL, build_gp(("SE", {}), xb, yb), numerical_matrix_handling=handling)
+    with pytest.raises(CholeskyError):
+        met.get_metric_and_gradient(hyp_list([0.2]), torch.tensor(-0.05, dtype=F64))

@@ -1,5 +1,9 @@
 """HIP path vs the CPU oracle and the golden vectors (needs the MI355X).
 
+The golden-fixture, size and small-tree tests run through both factorisation paths of a single f64
+evaluation (fixture ``factor_path``, tests/conftest.py): the launch-per-panel schedule and the persistent
+launch (chain_kernel), which is the default for single evaluations up to 7424 augmented rows.
+
 Tolerances (fp64 unless stated):
   kernel matrices       |dK| <= 1e-13 + 1e-12 |K|          (transcendental ulp differences)
   NLL                   rel <= 1e-9 (C2-C5, noise >= 1e-2);  rel <= 1e-6 for C1 (noise 1e-8,
@@ -156,14 +160,14 @@ def test_kernel_matrix_fp32_output():
 
 # ------------------------------------------------------------------------------ likelihood
 @pytest.mark.parametrize("n", [1, 2, 5, 127, 128, 129, 300, 1000])
-def test_nlml_sizes_match_oracle(n):
+def test_nlml_sizes_match_oracle(n, factor_path):
     x, y = o.make_inputs("C1", n=n, seed=n)
     got = gpu_nlml(SE, [0.1], 1e-2, x, y)
     exp = o.nlml(SE, [0.1], 1e-2, x, y)
     assert rel(got, exp) < 1e-10, (got, exp)
 
 
-def test_known_answers_on_gpu():
+def test_known_answers_on_gpu(factor_path):
     for y0, s2 in ((0.7, 0.01), (-1.3, 0.5)):
         got = gpu_nlml(SE, [0.3], s2, np.array([[0.2]]), np.array([y0]))
         exp = 0.5 * y0 * y0 / (1 + s2) + 0.5 * math.log(1 + s2) + 0.5 * math.log(2 * math.pi)
@@ -174,13 +178,13 @@ def test_known_answers_on_gpu():
     assert rel(gpu_nlml(SE, [0.5], 0.1, xf, yf), exp) < 1e-13
 
 
-def test_golden_c1_n256_jitter():
+def test_golden_c1_n256_jitter(factor_path):
     g = golden("c1_se_n256")
     got = gpu_nlml(SE, [0.1], 1e-8, g["x"], g["y"])
     assert rel(got, float(g["nlml"])) < 1e-6, (got, float(g["nlml"]))
 
 
-def test_golden_c1_factor_and_alpha():
+def test_golden_c1_factor_and_alpha(factor_path):
     """At the reference's default jitter (1e-8, cond ~1e10) two correct Cholesky codes agree
     only to ~cond * eps in L; the meaningful checks are the backward error of L and the
     residual of alpha.  At noise 1e-2 L itself is compared elementwise."""
@@ -203,7 +207,7 @@ def test_golden_c1_factor_and_alpha():
     np.testing.assert_allclose(L2, o.cholesky_lower(o.k_noised(SE, [0.1], 1e-2, x)), rtol=0, atol=1e-13)
 
 
-def test_golden_c2_n4096_nlml_and_posterior():
+def test_golden_c2_n4096_nlml_and_posterior(factor_path):
     g = golden("c2_se_n4096")
     gpr = build_gp(SE, g["x"], g["y"], g["xs"])
     m = get_metric_by_type(MetricType.LL, gpr)
@@ -256,7 +260,7 @@ def test_golden_c5_sum_ard_n16384():
     assert rel(got, float(g["nlml"])) < 1e-8
 
 
-def test_small_trees_scaled_expanded_batch():
+def test_small_trees_scaled_expanded_batch(factor_path):
     g = golden("small_trees")
     tree = ("MUL", [("ADD", [SE, ("MAT32", {})]), ("PER", {})])
     set_flags(scaled=True)
@@ -320,7 +324,7 @@ def test_not_positive_definite_reports_info():
     assert rel(out[0, 0], o.nlml(SE, [0.1], 1e-2, x, y)) < 1e-10
 
 
-def test_trsv_forward_backward():
+def test_trsv_forward_backward(factor_path):
     x, y = o.make_inputs("C1", n=333, seed=2)
     gpr = build_gp(SE, x, y)
     f = gpr.covariance_matrix.factorization(hyp_list([0.1]), torch.tensor(1e-2, dtype=torch.float64))
