@@ -171,6 +171,7 @@ struct Tune {
   int64_t chain_max_p;    //   ... while the augmented matrix has at most this many rows
   int64_t chain_grid;     //   workgroups of that launch (0: one per CU)
   int64_t chain_timeout_ms;  // bound of every wait inside it (then info = -1)
+  int64_t chain_group;    //   panels per deferred tile update (1: every tile update one panel deep)
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -190,7 +191,7 @@ Tune& tune() {
                          env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0),
                          env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024),
                          env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 7424), env_i64("GPK_CHAIN_GRID", 0),
-                         env_i64("GPK_CHAIN_TIMEOUT_MS", 1000)};
+                         env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 4)};
   return t;
 }
 
@@ -213,6 +214,7 @@ const Knob kKnobs[] = {
     {"fuse_trsm_max", &Tune::fuse_trsm_max}, {"trd_split_m", &Tune::trd_split_m},
     {"chain", &Tune::chain},                 {"chain_max_p", &Tune::chain_max_p},
     {"chain_grid", &Tune::chain_grid},       {"chain_timeout_ms", &Tune::chain_timeout_ms},
+    {"chain_group", &Tune::chain_group},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -344,7 +346,7 @@ struct ChainPlan {
   int32_t nblk = 0, nsl = 0, nbc = 0;
 };
 std::mutex g_chain_mu;
-std::map<std::tuple<int, int64_t, int64_t, int>, ChainPlan> g_chain_plans;
+std::map<std::tuple<int, int64_t, int64_t, int, int>, ChainPlan> g_chain_plans;
 // Counter scratch of the persistent launch, per (host thread, device, stream): the counters are zeroed
 // by a memset enqueued before each launch, so two threads enqueueing on one stream (torch's null stream
 // is shared by every thread) must never share them -- memset A, memset B, launch A, launch B would hand
@@ -396,7 +398,7 @@ int64_t g_chain_times_n = 0;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
-std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid) {
+std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group) {
   const int nblk = (int)(n_pad / NB), yb = (int)(y_row / NB), rlast = (int)(y_row / 32);
   struct Task {
     int ty, k, r, j;
@@ -406,44 +408,65 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid) {
   std::vector<Task> T;
   const int nr = rlast + 1;
   std::vector<int> D(nblk, -1), S((size_t)nblk * nr, -1), U((size_t)nblk * nr, -1);
-  std::map<std::tuple<int, int, int>, int> B;
+  std::map<std::pair<int, int>, int> last_upd;  // tile (i, j) -> its latest update task so far
   auto s_of = [&](int k, int r) { return S[(size_t)k * nr + r]; };
   auto u_of = [&](int k, int r) { return U[(size_t)k * nr + r]; };
   // list-scheduling durations (us) of D / S / U32 / BLK: the measured per-task run times
-  // (profiles/r03p_chain_task_profile_n4096.txt); GPK_CHAIN_DUR="d,s,u,b" overrides them (A/B)
+  // (profiles/r03p_chain_task_profile_n4096.txt); GPK_CHAIN_DUR="d,s,u,b" overrides them (A/B).  A tile
+  // update over g panels is estimated at b (0.25 + 0.75 g): the C read / write and the pipeline fill are
+  // paid once per task.
   float dur[4] = {32.f, 7.f, 10.f, 24.f};
   if (const char* e = getenv("GPK_CHAIN_DUR")) sscanf(e, "%f,%f,%f,%f", &dur[0], &dur[1], &dur[2], &dur[3]);
+  // Deferred tile updates: the panels of group [q0, q1) (G panels) are applied to a tile of block column j
+  // by ONE task of depth 128 (q1 - q0) when j >= q1 + L -- the column is not needed until L steps after
+  // the group's last panel solve; the columns nearer the diagonal take each panel on its own (depth 128),
+  // so the diagonal chain never waits for a deep update.  G = 1 disables it.
+  const int G = std::max(1, std::min(group, 16));
+  const int LA = (int)std::max<int64_t>(1, env_i64("GPK_CHAIN_GROUP_LA", 2));
   auto add = [&](Task t) {
-    t.dur = dur[t.ty];
     T.push_back(std::move(t));
     return (int)T.size() - 1;
   };
+  // BLK tasks carry ty = 3 | (g - 1) << 2 for an update over the g panels k .. k + g - 1
+  auto blk = [&](int q0, int g, int i, int jj) {
+    Task t{CHT_BLK | ((g - 1) << 2), q0, i, jj, dur[3] * (0.25f + 0.75f * (float)g), {}};
+    const int ql = q0 + g - 1;  // (S(ql, r) done implies S(q, r) done for every q < ql)
+    for (int s = 4 * i; s <= std::min(4 * i + 3, rlast); ++s) t.deps.push_back(s_of(ql, s));
+    if (jj != i)
+      for (int s = 4 * jj; s <= std::min(4 * jj + 3, rlast); ++s) t.deps.push_back(s_of(ql, s));
+    auto it = last_upd.find({i, jj});
+    if (it != last_upd.end()) t.deps.push_back(it->second);
+    last_upd[{i, jj}] = add(t);
+  };
   for (int k = 0; k < nblk; ++k) {
-    Task d{CHT_D, k, 0, k, 28.f, {}};
+    Task d{CHT_D, k, 0, k, dur[0], {}};
     if (k > 0)
       for (int s = 4 * k; s <= std::min(4 * k + 3, rlast); ++s) d.deps.push_back(u_of(k - 1, s));
     D[k] = add(d);
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
-      Task t{CHT_S, k, r, 0, 7.f, {D[k]}};
+      Task t{CHT_S, k, r, 0, dur[1], {D[k]}};
       if (k > 0) t.deps.push_back(u_of(k - 1, r));
       S[(size_t)k * nr + r] = add(t);
     }
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
-      Task t{CHT_U32, k, r, k + 1, 7.f, {s_of(k, r)}};
+      Task t{CHT_U32, k, r, k + 1, dur[2], {s_of(k, r)}};
       for (int s = 4 * (k + 1); s <= std::min(4 * (k + 1) + 3, rlast); ++s)
         if (s != r) t.deps.push_back(s_of(k, s));
-      if (k > 0) t.deps.push_back(B.at(std::make_tuple(k - 1, r / 4, k + 1)));
+      auto it = last_upd.find({r / 4, k + 1});
+      if (it != last_upd.end()) t.deps.push_back(it->second);
       U[(size_t)k * nr + r] = add(t);
     }
-    for (int j = k + 2; j <= yb; ++j)
-      for (int i = j; i <= yb; ++i) {
-        Task t{CHT_BLK, k, i, j, 18.f, {}};
-        for (int s = 4 * i; s <= std::min(4 * i + 3, rlast); ++s) t.deps.push_back(s_of(k, s));
-        if (j != i)
-          for (int s = 4 * j; s <= std::min(4 * j + 3, rlast); ++s) t.deps.push_back(s_of(k, s));
-        if (k > 0) t.deps.push_back(B.at(std::make_tuple(k - 1, i, j)));
-        B[std::make_tuple(k, i, j)] = add(t);
+    const int q0 = k / G * G, q1 = std::min(q0 + G, nblk);
+    for (int jj = k + 2; jj <= yb; ++jj) {
+      const bool grouped = G > 1 && jj >= q1 + LA;
+      if (grouped && k != q1 - 1) continue;  // the group's one task comes with its last panel
+      for (int i = jj; i <= yb; ++i) {
+        if (grouped)
+          blk(q0, q1 - q0, i, jj);
+        else
+          blk(k, 1, i, jj);
       }
+    }
   }
   const int n = (int)T.size();
   std::vector<std::vector<int>> succ(n);
@@ -511,10 +534,11 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   size_t ctl_ints = 0;
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
-    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid);
+    const int group = (int)tn.chain_group;
+    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
-      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid);
+      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, group);
       ChainPlan p;
       p.ntasks = (int32_t)(ord.size() / 4);
       p.nblk = (int32_t)(lay->n_pad / NB);
@@ -1810,7 +1834,7 @@ int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_ou
   if (y_row < n_pad) return fail_arg(2, "y_row (>= n_pad)");
   if (grid <= 0) return fail_arg(3, "grid");
   if (!ntasks) return fail_arg(6, "ntasks");
-  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid);
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, (int)tune_now().chain_group);
   *ntasks = (int64_t)(ord.size() / 4);
   if (tasks_out) {
     if (cap < *ntasks) return fail_arg(5, "cap (fewer than ntasks)");

@@ -639,8 +639,9 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 //                 left it; L_kk to W, L_kk^-1 to Winv; dflag[k]
 //   S(k, r)       slice r below block k: X = A(r, k) L_kk^-T, in place; sdone[k][r]
 //   U32(q, r, j)  slice r of block column j = q + 1: C -= X(r, q) X(j, q)^T; ucnt[r][j] = q + 1
-//   BLK(q, i, j)  128 x 128 tile (i, j), j >= q + 2: C -= X(i, q) X(j, q)^T (the trailing update of the
-//                 launch path, one panel deep); ucnt[r][j] = q + 1 for the slices r of block i
+//   BLK(q, i, j)  128 x 128 tile (i, j), j >= q + 2: C -= X(i, q..) X(j, q..)^T over g panels q .. q + g - 1
+//                 (g = 1 for the columns the diagonal chain needs soon, g = the planner's group for the deferred
+//                 ones: the launch path's deep group update); ucnt[r][j] = q + g for the slices r of block i
 // The chain D(k) -> S(k, block k + 1) -> U32(k, block k + 1, k + 1) -> D(k + 1) runs on slices spread
 // over CUs (a 128-row panel solve or update on one CU would take ~14 us of f64 MFMA), the BLK tiles of
 // older panels fill the rest of the chip -- the look-ahead that launches cannot give a single
@@ -754,15 +755,15 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
   }
 }
 
-// BLK: C(R.., Cc..) -= A(R.., Kc..) B(Cc.., Kc..)^T on a 128 x 128 tile, K = 128: gemm_kernel's f64
+// BLK: C(R.., Cc..) -= A(R.., Kc..) B(Cc.., Kc..)^T on a 128 x 128 tile, K = 128 g: gemm_kernel's f64
 // update (8 waves of 64 x 32, LDS-DMA staging of 16-deep chunks in two stages, C first, the next chunk's
 // DMA after the first half of the MFMAs) with write-through C stores.  Rows >= row_end are zero.
-__device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64_t Cc, int64_t Kc, int64_t row_end,
-                                         char* smem) {
+__device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64_t Cc, int64_t Kc, int g,
+                                         int64_t row_end, char* smem) {
   constexpr int TM = 128, TN = 128, WN = 4, WM = 2, NW = 8, MB = 4, NBK = 2, EPC = 2, GBK = 16, KS = 4;
   constexpr int STAGE = (TM + TN) * ROWB;
   constexpr int PW = (TM + TN) / (8 * NW);
-  constexpr int NK = NB / GBK;
+  const int NK = wave_uniform(g * (NB / GBK));  // depth 128 g: the g panels Kc / 128 .. + g - 1
   typedef double vec_t __attribute__((ext_vector_type(2)));
   const int tid = opaque_tid();
   const int lane = tid & 63;
@@ -921,7 +922,7 @@ __device__ __forceinline__ int claim_ticket(int32_t* p) {
 
 // Wave 0 (all its lanes poll the same words: no lane-divergent branch) waits until the task's inputs are
 // published; false on timeout (reported) or after another task's timeout.
-__device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, int r, int j) {
+__device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, int r, int j, int g) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   bool ok = true;
   if (ty == CH_D) {
@@ -936,7 +937,10 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, in
     for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
     if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + j, k, t0);
   } else {
-    const int32_t* sd = a.sdone + (int64_t)k * a.nsl;
+    // BLK over the g panels k .. k + g - 1: the last panel's solves of both blocks' slices (S(q, r) done
+    // implies S(q', r) done for q' < q: S(q, r) waited for the update of panel q - 1, which waited for
+    // S(q - 1, r)), and the tile's previous update
+    const int32_t* sd = a.sdone + (int64_t)(k + g - 1) * a.nsl;
     for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
     for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
     for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok && k > 0; ++s)
@@ -960,13 +964,14 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     __syncthreads();
     const int t = __builtin_amdgcn_readfirstlane(slot[0]);
     if (t >= a.ntasks) break;
-    const int ty = __builtin_amdgcn_readfirstlane(a.tasks[4 * t]);
+    const int tyg = __builtin_amdgcn_readfirstlane(a.tasks[4 * t]);
+    const int ty = tyg & 3, g = (tyg >> 2) + 1;  // (BLK: updates over g panels)
     const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
     const int r = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 2]);
     const int j = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 3]);
     if (wave == 0) {
       if (a.times) a.times[6 * t] = __builtin_amdgcn_s_memrealtime();
-      const bool ok = chain_deps(a, ty, k, r, j);
+      const bool ok = chain_deps(a, ty, k, r, j, g);
       if (a.times) {
         a.times[6 * t + 1] = __builtin_amdgcn_s_memrealtime();
         if (ty == CH_D || ty == CH_BLK) a.times[6 * t + 4] = __builtin_amdgcn_s_memtime();  // shader clock
@@ -988,7 +993,8 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     } else if (ty == CH_U32) {
       chain_u32(a.W, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
     } else {
-      blk_tile(a.W, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, a.row_end, reinterpret_cast<char*>(sm));
+      blk_tile(a.W, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, g, a.row_end,
+               reinterpret_cast<char*>(sm));
     }
     if (wave == 0 && a.times) {
       a.times[6 * t + 2] = __builtin_amdgcn_s_memrealtime();  // wave 0's body done
@@ -1007,7 +1013,7 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       } else if (ty == CH_U32) {
         st_flag(a.ucnt + (int64_t)r * a.nbc + j, k + 1);
       } else {
-        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl; ++s) st_flag(a.ucnt + (int64_t)s * a.nbc + j, k + 1);
+        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl; ++s) st_flag(a.ucnt + (int64_t)s * a.nbc + j, k + g);
       }
     }
   }

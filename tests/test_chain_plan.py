@@ -34,9 +34,15 @@ def shape(n, m):
     return n_pad, y_row, p
 
 
+def decode(task):
+    """(type, k, r, j, g): BLK tasks carry ty = 3 | (g - 1) << 2 for an update over panels k .. k + g - 1."""
+    tyg, k, r, j = (int(v) for v in task)
+    return tyg & 3, k, r, j, (tyg >> 2) + 1
+
+
 def cells(task, nsl):
     """(reads, writes) of a task as sets of (slice, block column) cells plus ('inv', k)."""
-    ty, k, r, j = (int(v) for v in task)
+    ty, k, r, j, g = decode(task)
 
     def sl(b):
         return [s for s in range(4 * b, 4 * b + 4) if s < nsl]
@@ -48,13 +54,13 @@ def cells(task, nsl):
         return {(r, k), ("inv", k)}, {(r, k)}
     if ty == U32:
         return {(r, k), (r, j)} | {(s, k) for s in sl(j)}, {(r, j)}
-    rd = {(s, k) for s in sl(r) + sl(j)} | {(s, j) for s in sl(r)}
+    rd = {(s, q) for s in sl(r) + sl(j) for q in range(k, k + g)} | {(s, j) for s in sl(r)}
     return rd, {(s, j) for s in sl(r)}
 
 
 def waits(task, nsl):
     """The kernel's waits (chain_kernel, dependency section): (counter, index, value >= )."""
-    ty, k, r, j = (int(v) for v in task)
+    ty, k, r, j, g = decode(task)
     out = []
     if ty == D:
         if k > 0:
@@ -69,22 +75,23 @@ def waits(task, nsl):
         if k > 0:
             out.append(("ucnt", (r, j), k))
     else:
-        out += [("sdone", (k, s), 1) for s in range(4 * r, 4 * r + 4) if s < nsl]
-        out += [("sdone", (k, s), 1) for s in range(4 * j, 4 * j + 4) if s < nsl]
+        q = k + g - 1
+        out += [("sdone", (q, s), 1) for s in range(4 * r, 4 * r + 4) if s < nsl]
+        out += [("sdone", (q, s), 1) for s in range(4 * j, 4 * j + 4) if s < nsl]
         if k > 0:
             out += [("ucnt", (s, j), k) for s in range(4 * r, 4 * r + 4) if s < nsl]
     return out
 
 
 def publishes(task, nsl):
-    ty, k, r, j = (int(v) for v in task)
+    ty, k, r, j, g = decode(task)
     if ty == D:
         return [("dflag", k, 1)]
     if ty == S:
         return [("sdone", (k, r), 1)]
     if ty == U32:
         return [("ucnt", (r, j), k + 1)]
-    return [("ucnt", (s, j), k + 1) for s in range(4 * r, 4 * r + 4) if s < nsl]
+    return [("ucnt", (s, j), k + g) for s in range(4 * r, 4 * r + 4) if s < nsl]
 
 
 def simulate(tasks, nsl, workers, rng):
@@ -104,7 +111,8 @@ def simulate(tasks, nsl, workers, rng):
         rd, wr = cells(task, nsl)
         for c in rd | wr:  # read-after-write / write-after-write: the last writer is done
             assert start >= last_w.get(c, 0.0), "task %d %s starts before the last writer of %s" % (t, task, c)
-        finish = start + dur[int(task[0])] * rng.uniform(0.3, 3.0)
+        ty, g = decode(task)[0], decode(task)[4]
+        finish = start + dur[ty] * g * rng.uniform(0.3, 3.0)
         for c in wr:  # write-after-read: earlier readers of the old version are done
             assert all(f <= finish for f in readers.get(c, [])), "task %d %s overwrites %s under a reader" % (
                 t, task, c)
@@ -137,7 +145,8 @@ def augmented(n, m, rng):
 
 def run_tasks(W, tasks, nblk):
     inv = {}
-    for ty, k, r, j in tasks:
+    for task in tasks:
+        ty, k, r, j, g = decode(task)
         K = slice(NB * k, NB * k + NB)
         if ty == D:
             a = np.tril(W[K, K])
@@ -151,34 +160,59 @@ def run_tasks(W, tasks, nblk):
             R, J = slice(SL * r, SL * r + SL), slice(NB * j, NB * j + NB)
             W[R, J] -= W[R, K] @ W[J, K].T
         else:
-            I, J = slice(NB * r, NB * r + NB), slice(NB * j, NB * j + NB)
-            W[I, J] -= W[I, K] @ W[J, K].T
+            I, J, KG = slice(NB * r, NB * r + NB), slice(NB * j, NB * j + NB), slice(NB * k, NB * (k + g))
+            W[I, J] -= W[I, KG] @ W[J, KG].T
     return W
 
 
-@pytest.mark.parametrize("n,m", [(1, 0), (128, 0), (300, 0), (700, 37), (1000, 200), (2048, 0)])
-def test_chain_plan_waits_cover_every_dependency(n, m):
+def plan(n_pad, y_row, grid, group):
+    old = nat.tune("chain_group", group)
+    try:
+        return nat.chain_plan(n_pad, y_row, grid)
+    finally:
+        nat.tune("chain_group", old)
+
+
+def applied_panels(tasks, nblk):
+    """Every tile update (panel q, block row i, block column j) the list applies, each exactly once."""
+    seen = []
+    for task in tasks:
+        ty, k, r, j, g = decode(task)
+        if ty == BLK:
+            seen += [(q, r, j) for q in range(k, k + g)]
+    return seen
+
+
+@pytest.mark.parametrize("n,m", [(1, 0), (128, 0), (300, 0), (700, 37), (1000, 200), (2048, 0), (3000, 0)])
+@pytest.mark.parametrize("group", [1, 4, 8])
+def test_chain_plan_waits_cover_every_dependency(n, m, group):
     _lib_or_skip()
     n_pad, y_row, p = shape(n, m)
     nsl = y_row // SL + 1
     rng = np.random.default_rng(n + m)
+    nblk, yb = n_pad // NB, y_row // NB
     for grid in (1, 3, 16, 256):
-        tasks = nat.chain_plan(n_pad, y_row, grid)
-        nblk = n_pad // NB
-        kinds = np.bincount(tasks[:, 0], minlength=4)
+        tasks = plan(n_pad, y_row, grid, group)
+        kinds = np.bincount(tasks[:, 0] & 3, minlength=4)
         assert kinds[D] == nblk
         assert len({tuple(t) for t in tasks.tolist()}) == len(tasks)
+        upd = applied_panels(tasks, nblk)
+        exp = [(q, i, j) for q in range(nblk) for j in range(q + 2, yb + 1) for i in range(j, yb + 1)]
+        assert sorted(upd) == sorted(exp)           # every (panel, tile) update exactly once
+        if group > 1 and nblk >= 2 * group + 2:
+            assert (tasks[:, 0] >> 2).max() == group - 1   # deep updates are used
         for _ in range(3):
             simulate(tasks, nsl, grid, rng)
 
 
-@pytest.mark.parametrize("n,m", [(200, 0), (600, 50), (1100, 0)])
-def test_chain_plan_reproduces_the_blocked_factorisation(n, m):
+@pytest.mark.parametrize("n,m", [(200, 0), (600, 50), (1100, 0), (2100, 40)])
+@pytest.mark.parametrize("group", [1, 4])
+def test_chain_plan_reproduces_the_blocked_factorisation(n, m, group):
     _lib_or_skip()
     rng = np.random.default_rng(7)
     n_pad, y_row, p = shape(n, m)
     W0, (xt, xs, y, noise, k) = augmented(n, m, rng)
-    tasks = nat.chain_plan(n_pad, y_row, 64)
+    tasks = plan(n_pad, y_row, 64, group)
     W = run_tasks(W0.copy(), tasks, n_pad // NB)
     Kn = k(xt, xt) + noise * np.eye(n)
     L = np.linalg.cholesky(Kn)

@@ -33,6 +33,9 @@ for _ in range(3):
 torch.cuda.synchronize()
 lay = f.layout
 tasks = nat.chain_plan(lay.n_pad, lay.y_row, grid if grid > 0 else torch.cuda.get_device_properties(0).multi_processor_count)
+gsz = (tasks[:, 0] >> 2) + 1   # BLK over g panels
+tasks = tasks.copy()
+tasks[:, 0] &= 3
 nt = len(tasks)
 buf = (ctypes.c_uint64 * (6 * nt))()
 rc = nat.load_library().gpk_chain_times(buf, nt)
@@ -51,6 +54,12 @@ for ty in range(4):
         b = T[m, 2] - T[m, 1]
         print("%-4s n %5d  wait mean %.1f  run mean %.1f  min %.1f  max %.1f us (wave 0 body %.1f, drain + barrier %.1f)" % (
             names[ty], m.sum(), w.mean(), r.mean(), r.min(), r.max(), b.mean(), (r - b).mean()), flush=True)
+        if ty == 3:
+            for gv in sorted(set(gsz[m].tolist())):
+                mm = m & (gsz == gv)
+                print("     g=%d: n %d run mean %.1f us = %.1f GF/s per CU" % (
+                    gv, mm.sum(), (T[mm, 3] - T[mm, 1]).mean(), 2 * 128 ** 3 * gv / ((T[mm, 3] - T[mm, 1]).mean() * 1e3)),
+                    flush=True)
         if ty in (1, 2):
             print("     wave 0: operands in place %.1f, MFMAs retired %.1f, body done %.1f us after ready" % (
                 np.nanmean(T[m, 4] - T[m, 1]), np.nanmean(T[m, 5] - T[m, 1]), b.mean()), flush=True)

@@ -18,6 +18,8 @@ import gaussianprocessfundamentals_amd.global_parameters as gp  # noqa: E402
 gp.init(0)
 from gaussianprocessfundamentals_amd import _native as nat  # noqa: E402
 from gaussianprocessfundamentals_amd import engine  # noqa: E402
+
+engine.CHAIN_VERIFY = os.environ.get("VERIFY", "0") == "1"  # (device span only: no info read-back per call)
 from gaussianprocessfundamentals_amd.KernelBasics import BaseKernels as bk  # noqa: E402
 
 SETS = [dict(lookahead=0, fuse_trsm=1, group=8)]
