@@ -49,9 +49,8 @@ class LogLikelihood(AbstractLogLikelihood):
         if approx and _wants_grad(hyper_parameter, noise, indices) and not (
                 self.local_approx is mht.MatrixApproximations.SKI and self.numerical_matrix_handling is H.CHOLESKY_BASED):
             # what the reference's tape sees through the approximate metric (Optimizer/Fitter.py:76-87,
-            # :124-132, :155-156): hyperparameters, noise and -- Nystroem -- the inducing inputs
-            if self.numerical_matrix_handling is H.LINEAR_CONJUGATE_GRADIENT:
-                raise NotImplementedError("gradients through LINEAR_CONJUGATE_GRADIENT are not provided")
+            # :124-132, :155-156): hyperparameters, noise and -- Nystroem -- the inducing inputs; under
+            # LINEAR_CONJUGATE_GRADIENT through the executed CG iterations on the approximate matrix
             if self.data_input.data_x_train.dim() == 3:
                 raise NotImplementedError("approximate metrics are provided for DataInput, not BatchDataInput")
             z = indices if isinstance(indices, torch.Tensor) else None
@@ -304,11 +303,16 @@ class _ApproxNegLogLikelihood(torch.autograd.Function):
     @staticmethod
     def forward(ctx, metric, z, noise, *hyper_parameter):
         A = mht.MatrixApproximations
+        H = mht.NumericalMatrixHandlingType
         hyp = [h.detach() for h in hyper_parameter]
         zd = z.detach() if isinstance(z, torch.Tensor) else z
         nys = metric.local_approx in (A.BASIC_NYSTROEM, A.SKC_LOWER_BOUND)
         ctx.fresh_det = nys and metric.nystroem_matrix.K_approx_det is None
-        nl = metric._get_metric_by_strategy(hyp, noise.detach(), zd).reshape(1, 1)
+        ctx.lcg = None
+        if metric.numerical_matrix_handling is H.LINEAR_CONJUGATE_GRADIENT:
+            nl, ctx.lcg = _approx_lcg_value(metric, hyp, noise.detach(), zd)
+        else:
+            nl = metric._get_metric_by_strategy(hyp, noise.detach(), zd).reshape(1, 1)
         ctx.metric, ctx.hyp, ctx.z, ctx.noise = metric, hyp, zd, noise.detach()
         ctx.want_z = isinstance(z, torch.Tensor) and z.requires_grad
         ctx.meta = [(h.device, h.dtype, h.shape) for h in (noise,) + hyper_parameter]
@@ -325,16 +329,34 @@ class _ApproxNegLogLikelihood(torch.autograd.Function):
         nv = float(noise)
         X = m.data_input.data_x_train
         kernel = m.covariance_matrix.kernel
+        lcg_adj = None
+        if ctx.lcg is not None:
+            # the fit's adjoint of the approximate matrix through the executed CG iterations: Q P^T
+            # (Auxiliary.LinearConjugateGradients.linear_cg_backward, seeded with 1/2 y)
+            from ..Auxiliary.LinearConjugateGradients import linear_cg_backward
+            Khat, tape, y = ctx.lcg
+            lcg_adj = linear_cg_backward(Khat, tape, 0.5 * y)
+            ctx.lcg = None
         if m.local_approx is A.SKI:
-            alpha_hat = m.get_alpha(hyp, noise, None, ctx.z)
             Ainv = m._approx_factorization(hyp, noise, ctx.z).k_inv(0).to(torch.float64).contiguous()
-            gh, gn = ag.ski_adjoint(m, hyp, noise, alpha_hat, Ainv)
+            if lcg_adj is not None:
+                # A-bar = Q P^T (fit) + 1/2 A^-1 (slogdet of the SKI matrix)
+                P, Q = lcg_adj
+                Abar = (0.5 * Ainv).contiguous()
+                if P.shape[1] > 0:
+                    engine.dgemm(Q, P, trans_b=True, beta=1.0, C=Abar)
+                gh, gn = ag.ski_adjoint_from(m, hyp, Abar)
+            else:
+                alpha_hat = m.get_alpha(hyp, noise, None, ctx.z)
+                gh, gn = ag.ski_adjoint(m, hyp, noise, alpha_hat, Ainv)
             gz = None
         else:
             Z = engine.as_device_f64(ctx.z)
             Z = Z.reshape(-1, 1) if Z.dim() == 1 else Z
             adj = ag.NystroemAdjoint(kernel, hyp, X, Z, nv)
-            if m.numerical_matrix_handling is H.CHOLESKY_BASED:
+            if lcg_adj is not None:
+                adj.lowrank_matrix_adjoint(*lcg_adj)
+            elif m.numerical_matrix_handling is H.CHOLESKY_BASED:
                 adj.exact_fit(m.covariance_matrix.get_L_alpha(hyp, noise), 0.5)
             else:
                 adj.approx_fit(m.get_alpha(hyp, noise, None, ctx.z), 0.5)
@@ -357,6 +379,26 @@ class _ApproxNegLogLikelihood(torch.autograd.Function):
         for g, (dev, dt, shp) in zip(_split_like(gh, hyp), ctx.meta[1:]):
             out.append((g * s).reshape(shp).to(device=dev, dtype=dt))
         return tuple(out)
+
+
+def _approx_lcg_value(metric, hyp, noise, z):
+    """-LML of an approximate metric under LINEAR_CONJUGATE_GRADIENT (LogLikelihood.py:36-60 with
+    Metrics.py:141-147): alpha = linear_cg(K_hat, y, 0) on the approximate matrix (its iterations recorded for
+    the reverse mode), the bound log-determinant (Nystroem determinant, or slogdet of the SKI matrix), the
+    SKC lower bound's trace correction.  Returns ([1, 1] value, (K_hat, tape, y))."""
+    from ..Auxiliary.LinearConjugateGradients import linear_cg
+    metric._require_plain()
+    Khat = metric.get_covariance_matrix(hyp, noise, z).contiguous()
+    y = metric._y(None)
+    tape = []
+    x = linear_cg(Khat, y, torch.zeros_like(y), tape=tape)
+    logdet = metric.get_log_determinant(hyp, noise, z)
+    n = float(metric.data_input.n_train)
+    ll = (-0.5 * torch.sum(y * x) + -0.5 * logdet) + (-0.5 * (n * LOG_2PI))
+    if metric.local_approx is mht.MatrixApproximations.SKC_LOWER_BOUND:
+        diff = torch.diagonal(Khat) - torch.diagonal(metric.covariance_matrix.get_K(hyp))
+        ll = ll - (1.0 / (2.0 * float(global_param.p_cov_matrix_jitter))) * torch.sum(diff)
+    return -ll.reshape(1, 1), (Khat, tape, y)
 
 
 def blockwise_hyper_parameter_offset(_gp) -> int:

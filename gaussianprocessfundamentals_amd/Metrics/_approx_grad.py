@@ -123,6 +123,24 @@ class NystroemAdjoint:
             T = T + Q + Q.T
         self._acc_t(T, w)
 
+    def lowrank_matrix_adjoint(self, P: torch.Tensor, Q: torch.Tensor):
+        """Adjoint Q P^T of the whole approximate matrix K_hat + noise I = K_nm pinv(K_mm) K_mn + noise I
+        (from the CG iterations, [n, k] each): d/d K_nm = (Kbar + Kbar^T) K_nm P_m, d/d pinv(K_mm) =
+        K_mn Kbar K_nm, d/d noise = tr Kbar -- all through the k-column factors, no n x n matrix."""
+        if P.shape[1] == 0:
+            return
+        knm, _, _, _, Pm = self.nystroem()
+        KP = engine.dgemm(knm, Pm)                              # K_nm P_m          [n, m]
+        ptk = engine.dgemm(P, KP, trans_a=True)                 # P^T K_nm P_m      [k, m]
+        qtk = engine.dgemm(Q, KP, trans_a=True)
+        M = engine.dgemm(Q, ptk)
+        engine.dgemm(P, qtk, beta=1.0, C=M)                     # Q P^T K P_m + P Q^T K P_m
+        self._acc_knm(M, 1.0)
+        a = engine.dgemm(Q, knm, trans_a=True)                  # Q^T K_nm          [k, m]
+        b = engine.dgemm(P, knm, trans_a=True)
+        self._acc_p(engine.dgemm(a, b, trans_a=True), 1.0)      # K_mn Q P^T K_nm
+        self.noise_bar.add_(torch.sum(P * Q))
+
     def approx_fit(self, alpha_hat: torch.Tensor, w: float):
         """fit = y^T (K_hat + noise I)^-1 y with K_hat = K_nm P K_mn: d/d K_nm = -2 a (P K_mn a)^T,
         d/d P = -(K_mn a)(K_mn a)^T, d/d noise = -a^T a  (a = alpha_hat)."""
@@ -169,6 +187,15 @@ def ski_adjoint(metric, hyp: List, noise, alpha_hat: torch.Tensor, Ainv: torch.T
     (Metrics/StructuredKernelInterpolation.py:10-28, Z = x_train[linspace] fixed): the adjoint of A is
     1/2 (A^-1 - a a^T), so K_zz's is W^T (.) W and the noise's its trace.  Returns (hyp adjoint, noise
     adjoint)."""
+    a = alpha_hat.reshape(-1, 1).contiguous()
+    Abar = (0.5 * Ainv).contiguous()
+    engine.dgemm(a, a, trans_b=True, alpha=-0.5, beta=1.0, C=Abar)
+    return ski_adjoint_from(metric, hyp, Abar)
+
+
+def ski_adjoint_from(metric, hyp: List, Abar: torch.Tensor):
+    """Map an adjoint Abar of the SKI matrix A = W K_zz W^T + noise I to (hyp adjoint, noise adjoint): K_zz's
+    is W^T Abar W (symmetrised for the kernel VJP), the noise's tr Abar."""
     import numpy as np
     from .StructuredKernelInterpolation import get_weight_matrix
     di = metric.data_input
@@ -176,9 +203,6 @@ def ski_adjoint(metric, hyp: List, noise, alpha_hat: torch.Tensor, Ainv: torch.T
     idx = np.linspace(start=0, stop=n, num=m, endpoint=False, dtype=int)
     z = di.get_inducting_x_train(torch.as_tensor(idx, dtype=torch.int64))
     Wm = get_weight_matrix(di)
-    a = alpha_hat.reshape(-1, 1).contiguous()
-    Abar = (0.5 * Ainv).contiguous()
-    engine.dgemm(a, a, trans_b=True, alpha=-0.5, beta=1.0, C=Abar)
-    kbar = engine.dgemm(engine.dgemm(Wm, Abar, trans_a=True), Wm)
+    kbar = engine.dgemm(engine.dgemm(Wm, Abar.contiguous(), trans_a=True), Wm)
     gh, _ = engine.kernel_vjp(metric.covariance_matrix.kernel, hyp, z, z, G=(kbar + kbar.T).contiguous())
     return 0.5 * gh, torch.trace(Abar)

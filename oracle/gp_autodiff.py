@@ -203,6 +203,8 @@ def nystroem_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.n
         alpha = pinv_or_inv(khat + nz * eye) @ Y
     elif handling == "STRICT_INVERSE":
         alpha = torch.linalg.inv(khat + nz * eye) @ Y
+    elif handling == "LINEAR_CONJUGATE_GRADIENT":
+        alpha, _ = cg_torch(khat + nz * eye, Y)
     else:
         raise ValueError(handling)
     fit = (Y.T @ alpha)[0, 0]
@@ -223,7 +225,7 @@ def nystroem_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.n
 
 def ski_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, m: int,
                       handling: str = "STRICT_INVERSE", scaled: bool = False):
-    """-LML of SKI with STRICT / PSEUDO inverse (gp_oracle.ski_nlml) and its gradient w.r.t. the
+    """-LML of SKI with STRICT / PSEUDO inverse or linear CG (gp_oracle.ski_nlml) and its gradient w.r.t. the
     hyperparameters and the noise (the inducing points x[linspace] and the weights are constants)."""
     from . import gp_oracle as o
     params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
@@ -236,7 +238,10 @@ def ski_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarra
     W = torch.as_tensor(o.ski_weight_matrix(X, X[idx]))
     kmm = kernel_matrix_t(tree, params, Zt, Zt, scaled)
     A = (W @ kmm) @ W.T + nz * torch.eye(n, dtype=F64)
-    alpha = (pinv_or_inv(A) if handling == "PSEUDO_INVERSE" else torch.linalg.inv(A)) @ Y
+    if handling == "LINEAR_CONJUGATE_GRADIENT":
+        alpha, _ = cg_torch(A, Y)
+    else:
+        alpha = (pinv_or_inv(A) if handling == "PSEUDO_INVERSE" else torch.linalg.inv(A)) @ Y
     fit = (Y.T @ alpha)[0, 0]
     logdet = torch.linalg.slogdet(A)[1]
     nl = -(-0.5 * fit - 0.5 * logdet - 0.5 * n * LOG_2PI)
@@ -260,18 +265,11 @@ def inverse_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.nd
     return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1])
 
 
-def lcg_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, scaled: bool = False):
-    """-LML with LINEAR_CONJUGATE_GRADIENT (alpha = linear_cg(K, y, 0), M/Metrics.py:141-144, the loop of
-    Auxiliary/LinearConjugateGradients.py:9-41 restated op for op -- |max r| > 1e-2 stopping rule, NaN early
-    return, the n-iteration guard) and slogdet (:146-147), with its reverse-mode gradient through the executed
-    iterations, as tf.GradientTape records them.  Returns (nlml, [grad per hyperparameter], grad noise,
-    iterations)."""
-    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
-    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
-    X = torch.as_tensor(np.asarray(x, dtype=np.float64))
-    Y = torch.as_tensor(np.asarray(y, dtype=np.float64)).reshape(-1, 1)
-    n = X.shape[0]
-    K = kernel_matrix_t(tree, params, X, X, scaled) + nz * torch.eye(n, dtype=F64)
+def cg_torch(K: torch.Tensor, Y: torch.Tensor):
+    """linear_cg(K, Y, 0) (Auxiliary/LinearConjugateGradients.py:9-41) op for op in torch, differentiable
+    through the executed iterations as tf.GradientTape records them: the |max r| > 1e-2 stopping rule, the
+    NaN early return, the n-iteration guard.  Returns (x, iterations)."""
+    n = K.shape[0]
     xk = torch.zeros((n, 1), dtype=F64)
     r = K @ xk - Y
     p = -r
@@ -291,6 +289,22 @@ def lcg_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarra
         first = False
         if k % (n / 4) == 0 and k > n:
             break
+    return xk, k
+
+
+def lcg_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, scaled: bool = False):
+    """-LML with LINEAR_CONJUGATE_GRADIENT (alpha = linear_cg(K, y, 0), M/Metrics.py:141-144, the loop of
+    Auxiliary/LinearConjugateGradients.py:9-41 restated op for op -- |max r| > 1e-2 stopping rule, NaN early
+    return, the n-iteration guard) and slogdet (:146-147), with its reverse-mode gradient through the executed
+    iterations, as tf.GradientTape records them.  Returns (nlml, [grad per hyperparameter], grad noise,
+    iterations)."""
+    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
+    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
+    X = torch.as_tensor(np.asarray(x, dtype=np.float64))
+    Y = torch.as_tensor(np.asarray(y, dtype=np.float64)).reshape(-1, 1)
+    n = X.shape[0]
+    K = kernel_matrix_t(tree, params, X, X, scaled) + nz * torch.eye(n, dtype=F64)
+    xk, k = cg_torch(K, Y)
     nl = -(-0.5 * (Y.T @ xk)[0, 0] - 0.5 * torch.linalg.slogdet(K)[1] - 0.5 * n * LOG_2PI)
     grads = torch.autograd.grad(nl, params + [nz])
     return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1]), k
@@ -322,3 +336,40 @@ def batch_nlml_and_grad(tree, hyp: List, noise: float, xb: np.ndarray, yb: np.nd
     nl = -red(ll)
     grads = torch.autograd.grad(nl, params + [nz])
     return float(nl.detach()), [g.numpy() for g in grads[:-1]], float(grads[-1])
+
+
+def skc_upper_nlml_and_grad(tree, hyp: List, noise: float, x: np.ndarray, y: np.ndarray, z: np.ndarray,
+                            k_fresh: bool = True, det_fresh: bool = True, scaled: bool = False):
+    """LogLikelihoodUpperBound.get_metric (gp_oracle.skc_upper_bound, Metrics/SkcLogLikelihood.py:26-69) and
+    the gradient tf.GradientTape takes of it (Optimizer/Fitter.py:76-87): the VariationalSGD step writes
+    alpha by a variable assignment, which the tape does not differentiate, so alpha is a constant for it
+    and the value 1/2 alpha^T K alpha - alpha^T y - 1/2 det - n/2 log 2 pi is differentiated at the stepped
+    alpha.  K (the metric's last_covariance_matrix) and the Nystroem determinant are cached across calls
+    (the metric never resets): a cached one is a constant for the tape -- k_fresh / det_fresh say whether
+    this call computed them.  Returns (value, [d/d h], d/d noise, d/d z or None)."""
+    from . import gp_oracle as o
+    params = [torch.tensor(np.asarray(h, dtype=np.float64), dtype=F64, requires_grad=True) for h in hyp]
+    nz = torch.tensor(float(noise), dtype=F64, requires_grad=True)
+    Z = torch.tensor(np.asarray(z, dtype=np.float64), dtype=F64, requires_grad=True)
+    X = torch.as_tensor(np.asarray(x, dtype=np.float64))
+    Y = torch.as_tensor(np.asarray(y, dtype=np.float64)).reshape(-1, 1)
+    n, m = X.shape[0], Z.shape[0]
+    K = kernel_matrix_t(tree, params, X, X, scaled) + nz * torch.eye(n, dtype=F64)
+    Kd = K.detach()
+    one = torch.ones((n, 1), dtype=F64)
+    g = (Kd @ one - Y) + Kd @ one
+    a = torch.as_tensor(o.vsgd_step(one.numpy(), g.numpy()))
+    Ku = K if k_fresh else Kd
+    fit = 0.5 * (a.T @ Ku @ a)[0, 0] - (a.T @ Y)[0, 0]
+    knm = kernel_matrix_t(tree, params, X, Z, scaled)
+    kmm = kernel_matrix_t(tree, params, Z, Z, scaled)
+    P = tf_pinv(kmm)
+    to_det = torch.eye(m, dtype=F64) * nz + knm.T @ (knm @ P)
+    det = (n - m) * torch.log(nz) + torch.linalg.slogdet(to_det)[1]
+    if not det_fresh:
+        det = det.detach()
+    val = fit - 0.5 * det - 0.5 * n * LOG_2PI
+    grads = torch.autograd.grad(val, params + [nz, Z], allow_unused=True)
+    gz = grads[-1]
+    return (float(val.detach()), [gg.numpy() if gg is not None else np.zeros(np.shape(h)) for gg, h in zip(grads[:-2], hyp)],
+            float(grads[-2]) if grads[-2] is not None else 0.0, gz.numpy() if gz is not None else None)

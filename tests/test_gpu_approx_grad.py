@@ -176,3 +176,56 @@ def test_ski_gradient_matches_oracle(handling):
     nl, gh, gn = ad.ski_nlml_and_grad(("SE", {}), [0.08], 0.05, x, y, m, handling.name)
     assert abs(float(out) - nl) <= 1e-9 * abs(nl)
     _close([float(h[0].grad), float(nz.grad)], [float(gh[0]), gn], 1e-7)
+
+
+@pytest.mark.parametrize("approx", [A.BASIC_NYSTROEM, A.SKC_LOWER_BOUND, A.SKI])
+def test_approximation_lcg_gradient_matches_oracle(approx):
+    """LINEAR_CONJUGATE_GRADIENT on the approximate matrix (M/Metrics.py:141-147 with :95-105): the tape
+    gradient through the executed CG iterations (linear_cg_backward) mapped through the Nystroem / SKI
+    structure, against oracle/gp_autodiff (torch's tape of the same loop).  Noise 0.4 keeps the CG iterate
+    insensitive to the device GEMV's rounding: value rel 1e-9, gradients 1e-6 max|g|."""
+    g, x, y = _gp(("SE", {}), n=256, seed=6)
+    m = 24
+    noise = 0.4
+    h = [torch.tensor(0.05, dtype=F64, requires_grad=True)]
+    nz = torch.tensor(noise, dtype=F64, requires_grad=True)
+    if approx is A.SKI:
+        met = get_metric_by_type(MetricType.LL, g, A.SKI, H.LINEAR_CONJUGATE_GRADIENT, subset_size=m)
+        out = met.get_metric(h, nz)
+        out.sum().backward()
+        nl, gh, gn = ad.ski_nlml_and_grad(("SE", {}), [0.05], noise, x, y, m, "LINEAR_CONJUGATE_GRADIENT")
+    else:
+        lower = approx is A.SKC_LOWER_BOUND
+        z = np.sort(np.random.default_rng(2).uniform(0, 1, (m, 1)), axis=0)
+        zt = torch.tensor(z, dtype=F64, requires_grad=True)
+        met = get_metric_by_type(MetricType.LL, g, approx, H.LINEAR_CONJUGATE_GRADIENT, subset_size=m)
+        out = met.get_metric(h, nz, zt)
+        out.sum().backward()
+        nl, gh, gn, gz = ad.nystroem_nlml_and_grad(("SE", {}), [0.05], noise, x, y, z, "LINEAR_CONJUGATE_GRADIENT",
+                                                   lower, float(gpar.p_cov_matrix_jitter))
+        _close(zt.grad.numpy(), gz, 1e-5 if lower else 1e-6)
+    assert abs(float(out) - nl) <= 1e-9 * abs(nl)
+    _close([float(h[0].grad), float(nz.grad)], [float(gh[0]), gn], 1e-5 if approx is A.SKC_LOWER_BOUND else 1e-6)
+
+
+def test_skc_upper_bound_gradient_matches_oracle():
+    """SKC_UPPER_BOUND (M/SkcLogLikelihood.py:53-69) differentiated as the fitter's tape does: alpha from
+    the VariationalSGD step is a constant; the first call computes K and the Nystroem determinant (both
+    differentiated), a second call reuses the metric's caches (constants: no gradient at all)."""
+    g, x, y = _gp(("SE", {}), n=200, seed=7)
+    m = 20
+    z = np.sort(np.random.default_rng(4).uniform(0, 1, (m, 1)), axis=0)
+    met = get_metric_by_type(MetricType.LL, g, A.SKC_UPPER_BOUND, subset_size=m)
+    h = [torch.tensor(0.06, dtype=F64, requires_grad=True)]
+    nz = torch.tensor(0.05, dtype=F64, requires_grad=True)
+    zt = torch.tensor(z, dtype=F64, requires_grad=True)
+    out = met.get_metric(h, nz, zt)
+    out.sum().backward()
+    val, gh, gn, gz = ad.skc_upper_nlml_and_grad(("SE", {}), [0.06], 0.05, x, y, z)
+    assert abs(float(out) - val) <= 1e-9 * abs(val)
+    _close([float(h[0].grad), float(nz.grad)], [float(gh[0]), gn], 1e-7)
+    _close(zt.grad.numpy(), gz, 1e-6)
+    h2 = [torch.tensor(0.07, dtype=F64, requires_grad=True)]
+    nz2 = torch.tensor(0.05, dtype=F64, requires_grad=True)
+    met.get_metric(h2, nz2, torch.tensor(z, dtype=F64)).sum().backward()
+    assert float(h2[0].grad) == 0.0 and float(nz2.grad) == 0.0

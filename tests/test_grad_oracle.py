@@ -137,3 +137,54 @@ def test_lcg_gradient_oracle_matches_finite_differences(n, ls, noise):
     fd, fdn = ad.finite_difference(f, [ls], noise, h=h)
     np.testing.assert_allclose(g[0], fd[0], rtol=1e-6)
     assert abs(gn - fdn) < 1e-6 * max(1.0, abs(fdn))
+
+
+@pytest.mark.parametrize("approx", ["NYSTROEM", "SKC_LOWER", "SKI"])
+def test_approximation_lcg_gradient_oracle_matches_finite_differences(approx):
+    """LINEAR_CONJUGATE_GRADIENT under BASIC_NYSTROEM / SKC_LOWER_BOUND / SKI (M/Metrics.py:141-147 on the
+    approximate matrix): the value equals gp_oracle's, the tape gradient through the executed CG iterations
+    equals central differences (same iteration count at the perturbed points)."""
+    x, y = o.make_inputs("C1", n=80, seed=6)
+    tree, hyp, noise = ("SE", {}), [0.05], 0.4
+    if approx == "SKI":
+        f = lambda h, nz: o.ski_nlml(tree, h, nz, x, y, 20, "LINEAR_CONJUGATE_GRADIENT")
+        nl, g, gn = ad.ski_nlml_and_grad(tree, hyp, noise, x, y, 20, "LINEAR_CONJUGATE_GRADIENT")
+        gz = None
+    else:
+        lower = approx == "SKC_LOWER"
+        z = np.sort(np.random.default_rng(2).uniform(0, 1, (10, 1)), axis=0)
+        f = lambda h, nz: o.nystroem_nlml(tree, h, nz, x, y, z, "LINEAR_CONJUGATE_GRADIENT", lower, 1e-3)
+        nl, g, gn, gz = ad.nystroem_nlml_and_grad(tree, hyp, noise, x, y, z, "LINEAR_CONJUGATE_GRADIENT", lower, 1e-3)
+        assert gz is not None
+    assert abs(nl - f(hyp, noise)) < 1e-9 * abs(nl)
+    fd, fdn = ad.finite_difference(f, hyp, noise, h=1e-6)
+    np.testing.assert_allclose(g[0], fd[0], rtol=1e-5, atol=1e-6)
+    assert abs(gn - fdn) < 1e-5 * max(1.0, abs(fdn))
+
+
+@pytest.mark.parametrize("k_fresh,det_fresh", [(True, True), (True, False), (False, True)])
+def test_skc_upper_bound_gradient_oracle(k_fresh, det_fresh):
+    """The SKC upper bound's tape gradient: alpha (one VariationalSGD step, a variable assignment) is a
+    constant, so the gradient is the partial derivative of 1/2 a^T K a - a^T y - 1/2 det at the stepped a --
+    checked by central differences of that expression with a held fixed; cached K / determinant contribute
+    nothing."""
+    x, y = o.make_inputs("C1", n=90, seed=5)
+    z = np.sort(np.random.default_rng(3).uniform(0, 1, (12, 1)), axis=0)
+    tree, hyp, noise = ("SE", {}), [0.04], 0.05
+    val, g, gn, gz = ad.skc_upper_nlml_and_grad(tree, hyp, noise, x, y, z, k_fresh, det_fresh)
+    assert abs(val - o.skc_upper_bound(tree, hyp, noise, x, y, z)) < 1e-9 * abs(val)
+    yv = y.reshape(-1, 1)
+    n = len(y)
+    K0 = o.k_noised(tree, hyp, noise, x)
+    a = o.vsgd_step(np.ones((n, 1)), (K0 @ np.ones((n, 1)) - yv) + K0 @ np.ones((n, 1)))
+    det0 = o.nystroem_det(tree, hyp, noise, x, z)
+
+    def f(h, nz):
+        K = o.k_noised(tree, h, nz, x) if k_fresh else K0
+        det = o.nystroem_det(tree, h, nz, x, z) if det_fresh else det0
+        return 0.5 * float((a.T @ K @ a)[0, 0]) - float((a.T @ yv)[0, 0]) - 0.5 * det
+    fd, fdn = ad.finite_difference(f, hyp, noise, h=1e-6)
+    np.testing.assert_allclose(g[0], fd[0], rtol=1e-5, atol=1e-6)
+    assert abs(gn - fdn) < 1e-5 * max(1.0, abs(fdn))
+    if not det_fresh:
+        assert gz is None or np.all(gz == 0)
