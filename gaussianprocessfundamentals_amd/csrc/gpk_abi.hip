@@ -1587,7 +1587,7 @@ int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
 // ------------------------------------------------------------------- tridiagonal eigensolver (gpk_eig.hip)
 namespace {
 constexpr int kEigNb = 32;  // reflectors per compact-WY block of the back-transformation
-#define GPK_SYEVD_MAX_M 4096   // dc_deflate_kernel sorts a merged block in LDS (4096 keys + indices + z)
+#define GPK_SYEVD_MAX_M 16384  // dc_gather_kernel holds a row of a merged block in LDS (128 KB)
 
 struct EigWs {  // carving of the gpk_syevd workspace
   double *W, *Qg, *U, *d, *e, *tau, *Y, *T1, *T2, *Gs, *S, *PV, *vg, *yg, *Sall;
@@ -1638,6 +1638,7 @@ EigWs eig_carve(int64_t m, void* base) {
   L.kcnt = itake(hp);
   L.rcnt = itake(hp);
   L.flip = itake(hp);
+  L.gscr = take((size_t)5 * m);
   ws.bytes = off;
   return ws;
 }
@@ -1657,7 +1658,7 @@ size_t gpk_syevd_workspace_bytes(int64_t m) {
 
 int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
               void* work, size_t work_bytes, void* stream) {
-  if (m < 0 || m > GPK_SYEVD_MAX_M) return fail_arg(1, "m (gpk_syevd: m <= 4096)");
+  if (m < 0 || m > GPK_SYEVD_MAX_M) return fail_arg(1, "m (gpk_syevd: m <= 16384)");
   if (batch < 0) return fail_arg(2, "batch");
   if (m == 0 || batch == 0) return 0;
   if (!A) return fail_arg(3, "A");

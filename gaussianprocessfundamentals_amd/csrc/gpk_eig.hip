@@ -333,20 +333,36 @@ __global__ __launch_bounds__(256) void dc_init_kernel(const double* d, const dou
   if (t < (int64_t)m * m) Q[t] = (t / m == t % m) ? 1.0 : 0.0;
 }
 
-// One workgroup per pair.  LDS: D[P2] z[k] idx[P2] kept[k] defl[k] red[32]
+// One workgroup per pair.  Merged blocks of up to DC_LDS_MAX_K rows sort and deflate in LDS: D[P2] z[k] idx[P2]
+// kept[k] defl[k]; larger ones (m > 4096, the non-positive-definite fallbacks of the metrics at large n) use the
+// same arrays in the level's HBM scratch L.gscr (pair p at offset 2a / a: the pairs' regions never overlap),
+// ordered by the same workgroup barriers (one workgroup, one CU: its stores and loads meet in that CU's L1 / L2).
+constexpr int DC_LDS_MAX_K = 4096;
+constexpr int DC_MAX_M = 16384;  // gpk_syevd's cap: dc_gather_kernel holds a row of the merged block in LDS
 __global__ __launch_bounds__(256) void dc_deflate_kernel(const double* __restrict__ e, const double* __restrict__ Q,
                                                          int m, int w, DcLevel L) {
   extern __shared__ __attribute__((aligned(16))) double sh[];
+  __shared__ double red[32];
   const int p = blockIdx.x, tid = threadIdx.x;
   const int a = 2 * w * p, b = a + w, c = min(a + 2 * w, m), k = c - a;
   int P2 = 1;
   while (P2 < k) P2 <<= 1;
-  double* D = sh;
-  double* z = D + P2;
-  double* red = z + k;
-  int* idx = reinterpret_cast<int*>(red + 32);
-  int* kept = idx + P2;
-  int* defl = kept + k;
+  double *D, *z;
+  int *idx, *kept, *defl;
+  if (k <= DC_LDS_MAX_K) {
+    D = sh;
+    z = D + P2;
+    idx = reinterpret_cast<int*>(z + k);
+    kept = idx + P2;
+    defl = kept + k;
+  } else {
+    D = L.gscr + 2 * (int64_t)a;
+    z = L.gscr + 2 * (int64_t)m + a;
+    int* gi = reinterpret_cast<int*>(L.gscr + 3 * (int64_t)m);
+    idx = gi + 2 * (int64_t)a;
+    kept = gi + 2 * (int64_t)m + a;
+    defl = gi + 3 * (int64_t)m + a;
+  }
   const double rho = e[b - 1];
   const bool flip = rho < 0.0;
   auto zorig = [&](int s) -> double { return s < w ? Q[(int64_t)(b - 1) * m + a + s] : Q[(int64_t)b * m + a + s]; };
@@ -801,16 +817,18 @@ hipError_t launch_eig_tridiag(double* W, int m, double* d, double* e, double* ta
 }
 
 static size_t dc_deflate_lds(int k) {
+  if (k > DC_LDS_MAX_K) return 16;  // (the arrays live in L.gscr)
   int P2 = 1;
   while (P2 < k) P2 <<= 1;
-  return sizeof(double) * ((size_t)P2 + k + 32) + sizeof(int) * ((size_t)P2 + 2 * (size_t)k);
+  return sizeof(double) * ((size_t)P2 + k) + sizeof(int) * ((size_t)P2 + 2 * (size_t)k);
 }
 
 hipError_t launch_eig_dc(const double* d, const double* e, int m, const DcLevel& L, double* Q, double* Qg, double* U,
                          hipStream_t s) {
   {
-    hipError_t err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_deflate_kernel), dc_deflate_lds(4096));
-    if (err == hipSuccess) err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_gather_kernel), 4096 * 8);
+    hipError_t err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_deflate_kernel), dc_deflate_lds(DC_LDS_MAX_K));
+    if (err == hipSuccess)  // (a pair's row of up to DC_MAX_M doubles)
+      err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_gather_kernel), (size_t)DC_MAX_M * 8);
     if (err != hipSuccess) return err;
   }
   const int64_t mm = (int64_t)m * m;

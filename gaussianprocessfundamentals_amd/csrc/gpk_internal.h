@@ -271,6 +271,7 @@ hipError_t launch_eig_tridiag(double* W, int m, double* d, double* e, double* ta
                               double* yg, int split_m, hipStream_t s);
 struct DcLevel {  // divide-and-conquer scratch, every array [m] (pair arrays [m / 2 + 1])
   double *lam, *dK, *zK, *rc, *rs, *root_t, *zhat, *rho;
+  double* gscr;  // [5 m]: the deflation's sort arrays of merged blocks too large for LDS
   int32_t *idx, *ord, *rp, *rn, *root_o, *kcnt, *rcnt, *flip;
 };
 hipError_t launch_eig_dc(const double* d, const double* e, int m, const DcLevel& L, double* Q, double* Qg, double* U,

@@ -608,12 +608,12 @@ def syevd(A: torch.Tensor):
     """Eigendecomposition of a symmetric [m, m] (or [B, m, m]) device matrix by the tridiagonal route
     (gpk_syevd: blocked Householder tridiagonalisation, divide and conquer on the tridiagonal matrix,
     compact-WY back-transformation): returns (lam, V with the eigenvectors in its columns), eigenvalues in no
-    particular order.  m > 4096 goes to the Jacobi solver (gpk_syevj)."""
+    particular order.  m > 16384 goes to the Jacobi solver (gpk_syevj)."""
     A3, lda, abs_ = _mat_args(A, "A")
     batch, m = A3.shape[0], A3.shape[1]
     if A3.shape[2] != m:
         raise ValueError("A must be square")
-    if m > 4096:
+    if m > 16384:
         lam, V, _ = syevj(A)
         return lam, V
     L = nat.lib()

@@ -304,7 +304,7 @@ int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
  * tridiagonalisation, divide and conquer on the tridiagonal matrix (deflation, Gu-Eisenstat eigenvectors,
  * MFMA GEMM merges), compact-WY back-transformation on the f64 MFMA GEMM.  Same outputs as gpk_syevj
  * (V [m, m] row-major, eigenvectors in its columns; lam in no particular order); A's lower triangle is read.
- * m <= 4096.  Asynchronous on the stream.
+ * m <= 16384 (merged blocks above 4096 rows sort in the workspace instead of LDS).  Asynchronous on the stream.
  * work: gpk_syevd_workspace_bytes(m) (reused across the batch). */
 size_t gpk_syevd_workspace_bytes(int64_t m);
 int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,

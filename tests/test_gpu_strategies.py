@@ -115,12 +115,12 @@ def test_handlings_of_an_indefinite_covariance(handling):
     assert rel(got, ref) <= 1e-8, (got, ref)
 
 
-@pytest.mark.parametrize("handling", [H.STRICT_INVERSE, H.PSEUDO_INVERSE])
-def test_handlings_of_an_indefinite_covariance_n4096(handling):
-    """The same at n = 4096 (the eigendecomposition fallback's cap, gpk_syevd): K - 0.3 I of 4096 SE inputs.
-    Reference alpha / log|det| from numpy's eigh (no eigenvalue near tf.linalg.pinv's cutoff here, so pinv =
-    inv); NLL rel <= 1e-8."""
-    g, x, y, _, _ = setup(n=4096)
+@pytest.mark.parametrize("handling,n", [(H.STRICT_INVERSE, 4096), (H.PSEUDO_INVERSE, 4096), (H.PSEUDO_INVERSE, 6144)])
+def test_handlings_of_an_indefinite_covariance_large(handling, n):
+    """The same at n = 4096 and 6144 (the eigendecomposition fallback, gpk_syevd, whose top merges sort in HBM
+    above 4096): K - 0.3 I of n SE inputs.  Reference alpha / log|det| from numpy's eigh (no eigenvalue near
+    tf.linalg.pinv's cutoff here, so pinv = inv); NLL rel <= 1e-8."""
+    g, x, y, _, _ = setup(n=n)
     noise = -0.3
     K = o.k_noised(SE, [0.1], noise, x)
     lam, V = np.linalg.eigh(K)
@@ -128,7 +128,7 @@ def test_handlings_of_an_indefinite_covariance_n4096(handling):
     met = get_metric_by_type(MetricType.LL, g, numerical_matrix_handling=handling)
     got = float(met.get_metric(hyp_list([0.1]), T(noise)).reshape(-1)[0])
     alpha = V @ ((V.T @ y) / lam)
-    ref = o.nlml_with_alpha(alpha, y, float(np.sum(np.log(np.abs(lam)))), 4096)
+    ref = o.nlml_with_alpha(alpha, y, float(np.sum(np.log(np.abs(lam)))), n)
     assert rel(got, ref) <= 1e-8, (got, ref)
 
 
