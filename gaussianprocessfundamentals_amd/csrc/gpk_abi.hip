@@ -172,6 +172,8 @@ struct Tune {
   int64_t chain_grid;     //   workgroups of that launch (0: one per CU)
   int64_t chain_timeout_ms;  // bound of every wait inside it (then info = -1)
   int64_t chain_group;    //   panels per deferred tile update (1: every tile update one panel deep)
+  int64_t chain_max_batch;   // batches of up to this many members run as one persistent launch too ...
+  int64_t chain_batch_max_p; //   ... while the augmented matrix has at most this many rows
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -190,8 +192,9 @@ Tune& tune() {
                          env_i64("GPK_RL_MAX_TILES", 256), env_i64("GPK_BAND_SKIP", 1),
                          env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0),
                          env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024),
-                         env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 7424), env_i64("GPK_CHAIN_GRID", 0),
-                         env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 4)};
+                         env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 12416), env_i64("GPK_CHAIN_GRID", 0),
+                         env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 4),
+                         env_i64("GPK_CHAIN_MAX_BATCH", 1), env_i64("GPK_CHAIN_BATCH_MAX_P", 4224)};
   return t;
 }
 
@@ -214,7 +217,8 @@ const Knob kKnobs[] = {
     {"fuse_trsm_max", &Tune::fuse_trsm_max}, {"trd_split_m", &Tune::trd_split_m},
     {"chain", &Tune::chain},                 {"chain_max_p", &Tune::chain_max_p},
     {"chain_grid", &Tune::chain_grid},       {"chain_timeout_ms", &Tune::chain_timeout_ms},
-    {"chain_group", &Tune::chain_group},
+    {"chain_group", &Tune::chain_group},     {"chain_max_batch", &Tune::chain_max_batch},
+    {"chain_batch_max_p", &Tune::chain_batch_max_p},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -346,7 +350,7 @@ struct ChainPlan {
   int32_t nblk = 0, nsl = 0, nbc = 0;
 };
 std::mutex g_chain_mu;
-std::map<std::tuple<int, int64_t, int64_t, int, int>, ChainPlan> g_chain_plans;
+std::map<std::tuple<int, int64_t, int64_t, int, int, int>, ChainPlan> g_chain_plans;
 // Counter scratch of the persistent launch, per (host thread, device, stream): the counters are zeroed
 // by a memset enqueued before each launch, so two threads enqueueing on one stream (torch's null stream
 // is shared by every thread) must never share them -- memset A, memset B, launch A, launch B would hand
@@ -398,7 +402,7 @@ int64_t g_chain_times_n = 0;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
-std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group) {
+std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group, int nmem) {
   const int nblk = (int)(n_pad / NB), yb = (int)(y_row / NB), rlast = (int)(y_row / 32);
   struct Task {
     int ty, k, r, j;
@@ -468,6 +472,20 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
       }
     }
   }
+  // independent members (a small batch): one copy of the graph per member, tagged in the type word's bits
+  // 8.. (task fields: ty | (g - 1) << 2 | member << 8), scheduled together so that every member's diagonal
+  // chain runs beside the others' tile updates
+  if (nmem > 1) {
+    const int n1 = (int)T.size();
+    T.reserve((size_t)n1 * nmem);
+    for (int m = 1; m < nmem; ++m)
+      for (int t = 0; t < n1; ++t) {
+        Task c = T[t];
+        c.ty |= m << 8;
+        for (int& dd : c.deps) dd += m * n1;
+        T.push_back(std::move(c));
+      }
+  }
   const int n = (int)T.size();
   std::vector<std::vector<int>> succ(n);
   std::vector<int> indeg(n, 0);
@@ -514,8 +532,11 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
 // captured (the first call of a shape uploads its task list), up to chain_max_p rows
 bool chain_applies(const gpk_layout* lay, bool eye, const int64_t* n_dev, const int64_t* m_dev, const Tune& tn,
                    hipStream_t s) {
-  if (!tn.chain || lay->dtype != GPK_F64 || lay->batch != 1 || eye || n_dev || m_dev) return false;
-  if (lay->p > tn.chain_max_p || tn.diag_dbg != 0 || tn.diag_version == 1) return false;
+  if (!tn.chain || lay->dtype != GPK_F64 || eye || n_dev || m_dev) return false;
+  if (lay->batch == 1 ? lay->p > tn.chain_max_p
+                      : (lay->batch > tn.chain_max_batch || lay->p > tn.chain_batch_max_p))
+    return false;
+  if (tn.diag_dbg != 0 || tn.diag_version == 1) return false;
   if (!plain_stream(s)) return false;
   if (tn.chain == 1 && other_stream_busy(s)) {
     ++g_chain_declined;
@@ -534,11 +555,11 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   size_t ctl_ints = 0;
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
-    const int group = (int)tn.chain_group;
-    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group);
+    const int group = (int)tn.chain_group, nmem = lay->batch;
+    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group, nmem);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
-      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, group);
+      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, group, nmem);
       ChainPlan p;
       p.ntasks = (int32_t)(ord.size() / 4);
       p.nblk = (int32_t)(lay->n_pad / NB);
@@ -549,7 +570,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
       it = g_chain_plans.emplace(key, p).first;  // owned for the life of the process
     }
     plan = it->second;
-    ctl_ints = 4 + (size_t)plan.nblk + (size_t)plan.nblk * plan.nsl + (size_t)plan.nsl * plan.nbc;
+    ctl_ints = 4 + (size_t)lay->batch * ((size_t)plan.nblk + (size_t)plan.nblk * plan.nsl + (size_t)plan.nsl * plan.nbc);
     ctl_ints = (ctl_ints + 3) / 4 * 4;
   }
   {
@@ -580,6 +601,10 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.ucnt = a.sdone + (size_t)plan.nblk * plan.nsl;
   a.nsl = plan.nsl;
   a.nbc = plan.nbc;
+  a.nmem = lay->batch;
+  a.w_bs = lay->w_batch_stride;
+  a.inv_bs = lay->inv_batch_stride;
+  a.ctl_stride = (int64_t)plan.nblk + (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
   a.row_end = lay->y_row + 1;
   a.timeout = std::max<int64_t>(1, tn.chain_timeout_ms) * 100000;  // 100 MHz ticks
   for (int64_t f = g_chain_force_timeout.load(); f > 0;)
@@ -603,7 +628,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     a.trace = grid <= 4096 ? g_chain_trace : nullptr;
   }
   const double n3 = (double)lay->n_pad;
-  GPK_HIP(timed(3, n3 * n3 * n3 / 3.0, 0.0, s, [&] { return launch_chain(a, grid, s); }), "chain");
+  GPK_HIP(timed(3, lay->batch * n3 * n3 * n3 / 3.0, 0.0, s, [&] { return launch_chain(a, grid, s); }), "chain");
   ++g_chain_launches;
   t_chain_last = true;
   return 0;
@@ -1835,7 +1860,7 @@ int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_ou
   if (y_row < n_pad) return fail_arg(2, "y_row (>= n_pad)");
   if (grid <= 0) return fail_arg(3, "grid");
   if (!ntasks) return fail_arg(6, "ntasks");
-  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, (int)tune_now().chain_group);
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, (int)tune_now().chain_group, 1);
   *ntasks = (int64_t)(ord.size() / 4);
   if (tasks_out) {
     if (cap < *ntasks) return fail_arg(5, "cap (fewer than ntasks)");

@@ -44,9 +44,12 @@ __device__ __forceinline__ int classify(const AsmArgs& a, int64_t g, int64_t n, 
 __device__ __forceinline__ int64_t member_n(const AsmArgs& a, int b) { return a.nb ? a.nb[b] : a.n; }
 __device__ __forceinline__ int64_t member_m(const AsmArgs& a, int b) { return a.mb ? a.mb[b] : a.m; }
 
-// Stage 64 points (raw + per-ARD-node rescaled copies) of one tile edge into LDS.
+// Stage 64 points (raw + per-ARD-node rescaled copies) of one tile edge into LDS.  sc_slot > 0: also
+// sin(pi f) and cos(pi f) of u = x / p (f = u - rint(u)) for the periodic node sc_node(kd) into slots
+// sc_slot and sc_slot + 1, clearing *sc_flag if any |u| exceeds SC_MAX_U.
 __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs& a, const double* hyp,
-                                             double* dst, int64_t g0, int b, bool rows, int slot_stride) {
+                                             double* dst, int64_t g0, int b, bool rows, int slot_stride,
+                                             int sc_slot = 0, double sc_iper = 0.0, int* sc_flag = nullptr) {
   const int tid = threadIdx.x;
   for (int e = tid; e < ATILE * a.d; e += 256) {
     const int pt = e / a.d, k = e - pt * a.d;
@@ -62,6 +65,14 @@ __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs&
       else if (c == CLS_TEST && a.E == nullptr && !a.eye) v = a.Xs[(int64_t)b * a.xs_bs + (g - a.n_pad) * a.d + k];
     }
     dst[pt * a.dp + k] = v;
+    if (sc_slot > 0) {
+      const double u = v * sc_iper;
+      if (!(fabs(u) <= SC_MAX_U)) atomicAnd(sc_flag, 0);
+      double sv, cv;
+      sincospi(u - rint(u), &sv, &cv);
+      dst[sc_slot * slot_stride + pt * a.dp + k] = sv;
+      dst[(sc_slot + 1) * slot_stride + pt * a.dp + k] = cv;
+    }
     // ARD copies: u = x / ls (the reference kernel with l = 1 on rescaled inputs)
     for (int q = 0; q < kd.n_nodes; ++q) {
       const gpk_node nd = kd.nodes[q];
@@ -84,6 +95,28 @@ __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs&
 // broadcast, and the D loops unroll; one loop per base-kernel op, the op test hoisted out of it.  Same
 // formulas, operation order and contraction (gpk_kernels.h) as the generic path and the fused build,
 // so every path writes the same bits.
+template <typename TOut, int D>
+__device__ __forceinline__ void interior_single_sc(FastNode fn, const double* prow, const double* pcol, int dp, int c,
+                                                   int r0, int64_t gi0, int64_t gj, double noise, TOut* W, int64_t ld) {
+  double sb[D], cb[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    sb[k] = pcol[fn.sc_sin + c * dp + k];
+    cb[k] = pcol[fn.sc_cos + c * dp + k];
+  }
+  fn.d = D;
+  for (int rr = r0; rr < ATILE; rr += 4) {
+    const double* ps = prow + fn.sc_sin + rr * dp;
+    const double* pc = prow + fn.sc_cos + rr * dp;
+    double v = GPK_ASM_ABLATE ? 0.0
+                              : per_sc_value(fn, [ps](int k) { return ps[k]; }, [pc](int k) { return pc[k]; },
+                                             [&sb](int k) { return sb[k]; }, [&cb](int k) { return cb[k]; });
+    const int64_t gi = gi0 + rr;
+    if (gi == gj) v += noise;
+    W[gi * ld + gj] = (TOut)v;
+  }
+}
+
 template <typename TOut, int D, int OP>
 __device__ __forceinline__ void interior_single(FastNode fn, const double* prow, const double* pcol, int dp, int c,
                                                 int r0, int64_t gi0, int64_t gj, double noise, TOut* W, int64_t ld) {
@@ -105,12 +138,15 @@ __device__ __forceinline__ void interior_single(FastNode fn, const double* prow,
 template <typename TOut, int D>
 __device__ __forceinline__ void interior_tree(const gpk_kdesc& kd, const FastNode* fns, const double* prow,
                                               const double* pcol, int off1, int dp, int c, int r0, int64_t gi0,
-                                              int64_t gj, double noise, TOut* W, int64_t ld) {
-  double cb0[D], cb1[D];
+                                              int64_t gj, double noise, TOut* W, int64_t ld, int sc_sin, int sc_cos,
+                                              bool sc_on) {
+  double cb0[D], cb1[D], csb[D], ccb[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     cb0[k] = pcol[c * dp + k];
     cb1[k] = pcol[off1 + c * dp + k];
+    csb[k] = sc_on ? pcol[sc_sin + c * dp + k] : 0.0;
+    ccb[k] = sc_on ? pcol[sc_cos + c * dp + k] : 0.0;
   }
   for (int rr = r0; rr < ATILE; rr += 4) {
     Stack st;
@@ -126,10 +162,17 @@ __device__ __forceinline__ void interior_tree(const gpk_kdesc& kd, const FastNod
       } else {
         FastNode f = fns[q];
         f.d = D;
-        const bool s1 = f.off != 0;
-        const double* pa = prow + f.off + rr * dp;
-        st.set(sp, fast_value_at(f, [pa](int k) { return pa[k]; },
-                                 [&cb0, &cb1, s1](int k) { return s1 ? cb1[k] : cb0[k]; }));
+        if (sc_on && f.sc && f.op == GPK_OP_PER) {
+          const double* ps = prow + sc_sin + rr * dp;
+          const double* pc = prow + sc_cos + rr * dp;
+          st.set(sp, per_sc_value(f, [ps](int k) { return ps[k]; }, [pc](int k) { return pc[k]; },
+                                  [&csb](int k) { return csb[k]; }, [&ccb](int k) { return ccb[k]; }));
+        } else {
+          const bool s1 = f.off != 0;
+          const double* pa = prow + f.off + rr * dp;
+          st.set(sp, fast_value_at(f, [pa](int k) { return pa[k]; },
+                                   [&cb0, &cb1, s1](int k) { return s1 ? cb1[k] : cb0[k]; }));
+        }
         sp += 1;
       }
     }
@@ -143,8 +186,13 @@ __device__ __forceinline__ void interior_tree(const gpk_kdesc& kd, const FastNod
 template <typename TOut, int D, bool TREE>
 __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& fn, const FastNode* fns, bool fast,
                                            const double* prow, const double* pcol, int slot_stride, int dp, int c,
-                                           int r0, int64_t gi0, int64_t gj, double noise, TOut* W, int64_t ld) {
+                                           int r0, int64_t gi0, int64_t gj, double noise, TOut* W, int64_t ld,
+                                           int sc_sin, int sc_cos, bool sc_on) {
   if (fast) {
+    if (sc_on && fn.sc && fn.op == GPK_OP_PER) {
+      interior_single_sc<TOut, D>(fn, prow, pcol, dp, c, r0, gi0, gj, noise, W, ld);
+      return true;
+    }
     switch (fn.op) {
       case GPK_OP_SE: interior_single<TOut, D, GPK_OP_SE>(fn, prow, pcol, dp, c, r0, gi0, gj, noise, W, ld); return true;
       case GPK_OP_PER: interior_single<TOut, D, GPK_OP_PER>(fn, prow, pcol, dp, c, r0, gi0, gj, noise, W, ld); return true;
@@ -154,7 +202,7 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
     }
   }
   if (!TREE || GPK_ASM_INTERIOR_TREE == 0 || kd.n_ard > 1 || kd.n_nodes > 8) return false;
-  interior_tree<TOut, D>(kd, fns, prow, pcol, slot_stride, dp, c, r0, gi0, gj, noise, W, ld);
+  interior_tree<TOut, D>(kd, fns, prow, pcol, slot_stride, dp, c, r0, gi0, gj, noise, W, ld, sc_sin, sc_cos, sc_on);
   return true;
 }
 
@@ -164,10 +212,15 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
 template <typename TOut, bool TREE>
 __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int sc_flag;
   const int slot_stride = ATILE * a.dp;
+  // slots per tile edge: raw points, one per ARD node, and (periodic node through sin / cos) sin, cos
+  const int scq = a.A == nullptr ? sc_node(kd) : -1;
+  const int sc_slot = 1 + kd.n_ard;
+  const int nslot = sc_slot + (scq >= 0 ? 2 : 0);
   double* hyp_s = smem;                                  // GPK_MAX_HYP
-  double* prow = smem + GPK_MAX_HYP;                     // (1 + n_ard) * slot_stride
-  double* pcol = prow + (1 + kd.n_ard) * slot_stride;
+  double* prow = smem + GPK_MAX_HYP;                     // nslot * slot_stride
+  double* pcol = prow + nslot * slot_stride;
 
   const int b = blockIdx.y;
   int64_t ti, tj;
@@ -195,24 +248,34 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   const int tid = threadIdx.x;
   const double* hyp_g = a.hyp + (int64_t)b * a.hyp_stride;
   for (int e = tid; e < kd.n_hyp; e += 256) hyp_s[e] = hyp_g[e];
+  if (tid == 0) sc_flag = 1;
   __syncthreads();
   // per-node constants of a tree (reciprocals of the hyperparameters; single nodes keep theirs in
   // registers below)
-  FastNode* fns = reinterpret_cast<FastNode*>(pcol + (1 + kd.n_ard) * slot_stride);
+  FastNode* fns = reinterpret_cast<FastNode*>(pcol + nslot * slot_stride);
+  const int sc_sin = sc_slot * slot_stride, sc_cos = (sc_slot + 1) * slot_stride;
   if (kd.n_nodes > 1 && tid < kd.n_nodes) {
     const gpk_node nd = kd.nodes[tid];
     if (nd.op != GPK_OP_ADD && nd.op != GPK_OP_MUL) {
       FastNode f = make_fast_node(nd, hyp_s, a.d);
       f.off = (nd.flags & GPK_NODE_ARD) ? (nd.ard_slot + 1) * slot_stride : 0;
+      if (tid == scq) {
+        f.sc = 1;
+        f.sc_sin = sc_sin;
+        f.sc_cos = sc_cos;
+      }
       fns[tid] = f;
     }
   }
   const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
   if (a.A == nullptr) {
-    stage_points(kd, a, hyp_s, prow, gi0, b, true, slot_stride);
-    stage_points(kd, a, hyp_s, pcol, gj0, b, false, slot_stride);
+    const double sc_iper = scq >= 0 ? 1.0 / hyp_s[kd.nodes[scq].hyp_offset + 1] : 0.0;
+    stage_points(kd, a, hyp_s, prow, gi0, b, true, slot_stride, scq >= 0 ? sc_slot : 0, sc_iper, &sc_flag);
+    stage_points(kd, a, hyp_s, pcol, gj0, b, false, slot_stride, scq >= 0 ? sc_slot : 0, sc_iper, &sc_flag);
   }
   __syncthreads();
+  // the sin / cos form for this tile: every staged point within |x / p| <= SC_MAX_U (workgroup-uniform)
+  const bool sc_on = scq >= 0 && sc_flag != 0;
 
   const int c = tid & 63;
   const int r0 = tid >> 6;
@@ -223,10 +286,17 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
       const int64_t gi = gi0 + rr;
       if (gi >= a.n || gj >= a.m) continue;
       if (a.uplo && gj > gi) continue;
-      double v = (kd.n_nodes == 1)
-                     ? fast_value(make_fast_node(kd.nodes[0], hyp_s, a.d), prow + rr * a.dp + fast_off(kd, slot_stride),
-                                  pcol + c * a.dp + fast_off(kd, slot_stride))
-                     : eval_tree_fast(kd, fns, prow + rr * a.dp, pcol + c * a.dp);
+      double v;
+      if (kd.n_nodes == 1) {
+        FastNode f1 = make_fast_node(kd.nodes[0], hyp_s, a.d);
+        f1.sc = scq == 0 ? 1 : 0;
+        f1.sc_sin = sc_sin;
+        f1.sc_cos = sc_cos;
+        v = fast_value(f1, prow + rr * a.dp + fast_off(kd, slot_stride), pcol + c * a.dp + fast_off(kd, slot_stride),
+                       sc_on);
+      } else {
+        v = eval_tree_fast(kd, fns, prow + rr * a.dp, pcol + c * a.dp, sc_on);
+      }
       if (gi == gj) v += a.diag_add;
       W[gi * a.ld + gj] = (TOut)v;
     }
@@ -240,14 +310,17 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   const bool fast = kd.n_nodes == 1;
   FastNode fn = make_fast_node(kd.nodes[0], hyp_s, a.d);
   fn.off = fast_off(kd, slot_stride);
+  fn.sc = scq == 0 ? 1 : 0;
+  fn.sc_sin = sc_sin;
+  fn.sc_cos = sc_cos;
   if (GPK_ASM_INTERIOR && !a.generic && a.A == nullptr && gi0 + ATILE <= nm) {  // lower tiles: gj0 <= gi0
     bool done = false;
     switch (a.d) {
-      case 1: done = interior_d<TOut, 1, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
-      case 2: done = interior_d<TOut, 2, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
-      case 3: done = interior_d<TOut, 3, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
-      case 4: done = interior_d<TOut, 4, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
-      case 8: done = interior_d<TOut, 8, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld); break;
+      case 1: done = interior_d<TOut, 1, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld, sc_sin, sc_cos, sc_on); break;
+      case 2: done = interior_d<TOut, 2, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld, sc_sin, sc_cos, sc_on); break;
+      case 3: done = interior_d<TOut, 3, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld, sc_sin, sc_cos, sc_on); break;
+      case 4: done = interior_d<TOut, 4, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld, sc_sin, sc_cos, sc_on); break;
+      case 8: done = interior_d<TOut, 8, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld, sc_sin, sc_cos, sc_on); break;
       default: break;
     }
     if (done) return;
@@ -273,8 +346,8 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
       if (gi == gj) v += noise;
     } else if ((rcls == CLS_TRAIN || rcls == CLS_TEST) && col_kernel) {
       if (!GPK_ASM_ABLATE)
-        v = fast ? fast_value(fn, prow + fn.off + rr * a.dp, pcol + fn.off + c * a.dp)
-                 : eval_tree_fast(kd, fns, prow + rr * a.dp, pcol + c * a.dp);
+        v = fast ? fast_value(fn, prow + fn.off + rr * a.dp, pcol + fn.off + c * a.dp, sc_on)
+                 : eval_tree_fast(kd, fns, prow + rr * a.dp, pcol + c * a.dp, sc_on);
       if (rcls == CLS_TRAIN && ccls == CLS_TRAIN && gi == gj) v += noise;
     } else if (rcls == CLS_Y && ccls == CLS_TRAIN) {
       v = yv;
@@ -828,7 +901,8 @@ hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_
 
 hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
                            hipStream_t s) {
-  const size_t lds = sizeof(double) * (GPK_MAX_HYP + 2 * (size_t)(1 + kd.n_ard) * ATILE * a.dp) +
+  const int nslot = 1 + kd.n_ard + ((a.A == nullptr && sc_node(kd) >= 0) ? 2 : 0);
+  const size_t lds = sizeof(double) * (GPK_MAX_HYP + 2 * (size_t)nslot * ATILE * a.dp) +
                      sizeof(FastNode) * GPK_MAX_NODES;
   dim3 grid;
   if (a.plain) {

@@ -153,6 +153,8 @@ struct ChainArgs {
   int32_t* sdone;        // [nblk][nsl]: S(k, r) done
   int32_t* ucnt;         // [nsl][nbc]: panels applied to slice r of block column j
   int32_t nsl, nbc;      // live 32-row slices (the last one holds the y row), live block columns
+  int32_t nmem;          // members (task word bits 8..): W + m w_bs, Winv + m inv_bs, info + m, counters + m ctl_stride
+  int64_t w_bs, inv_bs, ctl_stride;
   int64_t row_end;       // y_row + 1: rows below are zero
   int64_t timeout;       // per wait, in s_memrealtime ticks (100 MHz)
   int32_t* trace;        // debugging (GPK_CHAIN_TRACE=1, else NULL): host-visible [grid][32] progress words

@@ -162,7 +162,20 @@ struct Stack {
 struct FastNode {
   int op, flags, d, off;
   double il, il2, i3l2, iper, sg;
+  // periodic node through the staged sin / cos of its points (sc_node): sin(pi u), cos(pi u) per point and
+  // dimension at offsets sc_sin / sc_cos from the point (tiles whose points all have |u| = |x / p| <= 4)
+  int sc, sc_sin, sc_cos;
 };
+
+// The periodic node whose sin^2(pi (x_k - y_k) / p) terms the K build takes from per-point sin / cos
+// (sin(a - b) = sin a cos b - cos a sin b; separable per dimension: the standard form, or D = 1 where the
+// reference's L1 form is the same): the first such node of the program, -1 if none.
+__host__ __device__ inline int sc_node(const gpk_kdesc& kd) {
+  for (int q = 0; q < kd.n_nodes; ++q)
+    if (kd.nodes[q].op == GPK_OP_PER && ((kd.nodes[q].flags & GPK_NODE_STANDARD) || kd.dim == 1)) return q;
+  return -1;
+}
+constexpr double SC_MAX_U = 4.0;  // |x / p| bound of a tile for the sin / cos form (phase error <= 8 pi eps)
 
 __device__ __forceinline__ int fast_off(const gpk_kdesc& kd, int slot_stride) {
   return (kd.nodes[0].flags & GPK_NODE_ARD) ? (kd.nodes[0].ard_slot + 1) * slot_stride : 0;
@@ -191,7 +204,25 @@ __device__ __forceinline__ FastNode make_fast_node(const gpk_node& nd, const dou
   f.il2 = 1.0 / (l * l);
   f.i3l2 = 1.0 / (3.0 * (l * l));
   f.sg = (nd.flags & GPK_NODE_SCALED) ? h[sg_at] : 1.0;
+  f.sc = 0;
+  f.sc_sin = f.sc_cos = 0;
   return f;
+}
+
+// sin^2 over the dimensions from per-point sin(pi u) / cos(pi u) (u = x / p, reduced by the nearest integer
+// before the sincospi: the sign (-1)^n cancels in the square): sin(pi (u_a - u_b)) = s_a c_b - c_a s_b.
+// Same contraction everywhere it is used (interior, generic and plain paths write the same bits).  Against the
+// reference's sin(pi |x_a - x_b| / p) the phase error is eps (|u_a| + |u_b|) pi <= 8 pi eps on a tile that
+// qualifies (SC_MAX_U): 3 VALU operations per dimension instead of the reduced Taylor series' ~25.
+template <typename SA, typename CA, typename SB, typename CB>
+__device__ __forceinline__ double per_sc_value(const FastNode& f, SA sa, CA ca, SB sb, CB cb) {
+#pragma clang fp contract(on)  // fuse within an expression only: every caller rounds alike
+  double sn = 0.0;
+  for (int k = 0; k < f.d; ++k) {
+    const double t = sa(k) * cb(k) - ca(k) * sb(k);
+    sn += t * t;
+  }
+  return f.sg * exp((-2.0 * sn) * f.il2);
 }
 
 // sin^2(pi t), t >= 0 (the periodic kernel's sin^2(pi d / p) with t = d / p).  sin^2 has period 1 in
@@ -274,7 +305,12 @@ __device__ __forceinline__ double fast_value_at(const FastNode& f, PA a, PB b) {
   return f.sg * r;
 }
 
-__device__ __forceinline__ double fast_value(const FastNode& f, const double* a, const double* b) {
+__device__ __forceinline__ double fast_value(const FastNode& f, const double* a, const double* b, bool sc_on = false) {
+  if (sc_on && f.sc && f.op == GPK_OP_PER) {
+    const int so = f.sc_sin, co = f.sc_cos;
+    return per_sc_value(f, [a, so](int k) { return a[so + k]; }, [a, co](int k) { return a[co + k]; },
+                        [b, so](int k) { return b[so + k]; }, [b, co](int k) { return b[co + k]; });
+  }
   return fast_value_at(f, [a](int k) { return a[k]; }, [b](int k) { return b[k]; });
 }
 
@@ -282,7 +318,7 @@ __device__ __forceinline__ double fast_value(const FastNode& f, const double* a,
 // node q, fns[q].off its ARD slot offset): the tree form of the single-node fast path -- no division
 // by a hyperparameter per element, the periodic nodes through sin2_pi.
 __device__ __forceinline__ double eval_tree_fast(const gpk_kdesc& kd, const FastNode* fns, const double* pa,
-                                                 const double* pb) {
+                                                 const double* pb, bool sc_on = false) {
   Stack st;
   st.s0 = 0.0;
   int sp = 0;
@@ -295,7 +331,7 @@ __device__ __forceinline__ double eval_tree_fast(const gpk_kdesc& kd, const Fast
       sp -= 1;
     } else {
       const FastNode f = fns[q];
-      st.set(sp, fast_value(f, pa + f.off, pb + f.off));
+      st.set(sp, fast_value(f, pa + f.off, pb + f.off, sc_on));
       sp += 1;
     }
   }

@@ -668,9 +668,12 @@ __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p,
     if (__builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) return false;
     if (a.force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout) {
       st_flag(a.ctl + 1, 1);
-      int32_t zero = 0;
-      __hip_atomic_compare_exchange_strong((gi32*)a.info, &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+      // every member may be incomplete now: info = -1 wherever no non-positive pivot was found first
+      for (int m = 0; m < a.nmem; ++m) {
+        int32_t zero = 0;
+        __hip_atomic_compare_exchange_strong((gi32*)(a.info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      }
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -922,29 +925,32 @@ __device__ __forceinline__ int claim_ticket(int32_t* p) {
 
 // Wave 0 (all its lanes poll the same words: no lane-divergent branch) waits until the task's inputs are
 // published; false on timeout (reported) or after another task's timeout.
-__device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, int r, int j, int g) {
+__device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, int r, int j, int g, int64_t co) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   bool ok = true;
+  const int32_t* dflag = a.dflag + co;
+  const int32_t* sdone = a.sdone + co;
+  const int32_t* ucnt = a.ucnt + co;
   if (ty == CH_D) {
     if (k > 0)
-      for (int s = 4 * k; s <= 4 * k + 3 && ok; ++s) ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + k, k, t0);
+      for (int s = 4 * k; s <= 4 * k + 3 && ok; ++s) ok = chain_wait(a, ucnt + (int64_t)s * a.nbc + k, k, t0);
   } else if (ty == CH_S) {
-    ok = chain_wait(a, a.dflag + k, 1, t0);
-    if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + k, k, t0);
+    ok = chain_wait(a, dflag + k, 1, t0);
+    if (ok && k > 0) ok = chain_wait(a, ucnt + (int64_t)r * a.nbc + k, k, t0);
   } else if (ty == CH_U32) {
-    const int32_t* sd = a.sdone + (int64_t)k * a.nsl;
+    const int32_t* sd = sdone + (int64_t)k * a.nsl;
     ok = chain_wait(a, sd + r, 1, t0);
     for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
-    if (ok && k > 0) ok = chain_wait(a, a.ucnt + (int64_t)r * a.nbc + j, k, t0);
+    if (ok && k > 0) ok = chain_wait(a, ucnt + (int64_t)r * a.nbc + j, k, t0);
   } else {
     // BLK over the g panels k .. k + g - 1: the last panel's solves of both blocks' slices (S(q, r) done
     // implies S(q', r) done for q' < q: S(q, r) waited for the update of panel q - 1, which waited for
     // S(q - 1, r)), and the tile's previous update
-    const int32_t* sd = a.sdone + (int64_t)(k + g - 1) * a.nsl;
+    const int32_t* sd = sdone + (int64_t)(k + g - 1) * a.nsl;
     for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
     for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
     for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok && k > 0; ++s)
-      ok = chain_wait(a, a.ucnt + (int64_t)s * a.nbc + j, k, t0);
+      ok = chain_wait(a, ucnt + (int64_t)s * a.nbc + j, k, t0);
   }
   return ok;
 }
@@ -965,13 +971,15 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     const int t = __builtin_amdgcn_readfirstlane(slot[0]);
     if (t >= a.ntasks) break;
     const int tyg = __builtin_amdgcn_readfirstlane(a.tasks[4 * t]);
-    const int ty = tyg & 3, g = (tyg >> 2) + 1;  // (BLK: updates over g panels)
+    const int ty = tyg & 3, g = ((tyg >> 2) & 63) + 1, mem = tyg >> 8;  // (BLK: updates over g panels; member)
+    double* const Wm = a.W + (int64_t)mem * a.w_bs;
+    const int64_t co = (int64_t)mem * a.ctl_stride;
     const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
     const int r = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 2]);
     const int j = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 3]);
     if (wave == 0) {
       if (a.times) a.times[6 * t] = __builtin_amdgcn_s_memrealtime();
-      const bool ok = chain_deps(a, ty, k, r, j, g);
+      const bool ok = chain_deps(a, ty, k, r, j, g, co);
       if (a.times) {
         a.times[6 * t + 1] = __builtin_amdgcn_s_memrealtime();
         if (ty == CH_D || ty == CH_BLK) a.times[6 * t + 4] = __builtin_amdgcn_s_memtime();  // shader clock
@@ -987,13 +995,14 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
     if (ty == CH_D) {
-      chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, k, sm);
+      chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, sm);
     } else if (ty == CH_S) {
-      chain_s(a.W, a.ld, a.Winv, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      chain_s(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
+              reinterpret_cast<char*>(sm));
     } else if (ty == CH_U32) {
-      chain_u32(a.W, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      chain_u32(Wm, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
     } else {
-      blk_tile(a.W, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, g, a.row_end,
+      blk_tile(Wm, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, g, a.row_end,
                reinterpret_cast<char*>(sm));
     }
     if (wave == 0 && a.times) {
@@ -1007,13 +1016,13 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       chain_trace(a, 1, 4);
       if (a.times) a.times[6 * t + 3] = __builtin_amdgcn_s_memrealtime();
       if (ty == CH_D) {
-        st_flag(a.dflag + k, 1);
+        st_flag(a.dflag + co + k, 1);
       } else if (ty == CH_S) {
-        st_flag(a.sdone + (int64_t)k * a.nsl + r, 1);
+        st_flag(a.sdone + co + (int64_t)k * a.nsl + r, 1);
       } else if (ty == CH_U32) {
-        st_flag(a.ucnt + (int64_t)r * a.nbc + j, k + 1);
+        st_flag(a.ucnt + co + (int64_t)r * a.nbc + j, k + 1);
       } else {
-        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl; ++s) st_flag(a.ucnt + (int64_t)s * a.nbc + j, k + g);
+        for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl; ++s) st_flag(a.ucnt + co + (int64_t)s * a.nbc + j, k + g);
       }
     }
   }

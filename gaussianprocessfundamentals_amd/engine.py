@@ -191,7 +191,7 @@ class AugmentedFactorization:
         global CHAIN_FALLBACKS
         if not CHAIN_VERIFY or not nat.last_factorisation_was_chain():
             return
-        if int(self.info[0]) != -1:   # (synchronises the stream)
+        if not bool((self.info == -1).any()):   # (synchronises the stream)
             return
         CHAIN_FALLBACKS += 1
         logging.warning("persistent factorisation timed out (gpk_tune chain_timeout_ms): re-running it on the "

@@ -3,9 +3,10 @@ DESIGN §4) against the launch-per-panel schedule and the oracle (needs the MI35
 
 One f64 member without identity / ragged rows runs as ONE launch whose workgroups claim the tasks of
 gpk_chain_plan (tests/test_chain_plan.py checks that list on the host).  Contract with the launch path:
-agreement to 1e-12 relative in L, z, -LML, mu and Sigma at every size up to the chain_max_p edge (N = 7296:
-7424 augmented rows), at the reference's 1e-8 jitter as well; test_chain_bitwise_vs_launch_path records
-whether the two are also bit-identical.  Between runs of the chain itself the arithmetic order is fixed
+agreement to 1e-12 relative in L, z, -LML, mu and Sigma at every size (N up to 7296 here), at the reference's
+1e-8 jitter as well; and bit-identical results (test_chain_bitwise_vs_launch_path, N up to 12288, the
+chain_max_p edge): every tile update and panel solve keeps the launch path's MFMA k-order, the deferred tile
+updates over g panels included, and an f64 accumulator stored and reloaded between panels rounds nothing.  Between runs of the chain itself the arithmetic order is fixed
 (every tile's updates are serialised by its counter), so repeated runs are bitwise equal.  A wait that
 times out is recovered in the same call on the launch path (engine.AugmentedFactorization._verify_chain).
 """
@@ -57,7 +58,7 @@ def _lower(f):
 def test_chain_matches_the_launch_path(n, m, noise):
     fc, _ = _run(n, m, 1, noise=noise)
     fl, _ = _run(n, m, 0, noise=noise)
-    assert fc.layout.p <= 7424  # (inside chain_max_p: the persistent launch ran)
+    assert fc.layout.p <= 12416  # (inside chain_max_p: the persistent launch ran)
     assert int(fc.info.cpu()[0]) == 0 and int(fl.info.cpu()[0]) == 0
     a, b = _lower(fc), _lower(fl)
     scale = np.abs(b).max()
@@ -69,7 +70,7 @@ def test_chain_matches_the_launch_path(n, m, noise):
         np.testing.assert_allclose(fc.var.cpu().numpy(), fl.var.cpu().numpy(), rtol=0, atol=1e-10)
 
 
-@pytest.mark.parametrize("n,m", [(257, 0), (3000, 300), (4096, 0), (7296, 0)])
+@pytest.mark.parametrize("n,m", [(257, 0), (3000, 300), (4096, 0), (7296, 0), (8192, 0), (12288, 0)])
 def test_chain_bitwise_vs_launch_path(n, m):
     """Same MFMA k-order in every tile update and panel solve, and an f64 accumulator stored and reloaded
     between panels rounds nothing: the persistent launch reproduces the launch path bit for bit."""
@@ -242,3 +243,66 @@ def test_auto_mode_declines_while_another_stream_is_busy():
     assert s1["declined_busy"] > s0["declined_busy"] and s1["launches"] == s0["launches"]
     assert s2["launches"] == s1["launches"] + 1 and s2["last_was_chain"]
     assert float(one.nlml().cpu()[0]) == pytest.approx(o.nlml(SE, [0.1], 1e-2, x, y), rel=1e-9)
+
+
+@pytest.mark.parametrize("n,batch", [(1000, 2), (2048, 3), (700, 5)])
+def test_chain_batched_members_bitwise_vs_launch_path(n, batch):
+    """A small batch as ONE persistent launch (gpk_tune chain_max_batch): every member's task graph in one
+    list, member index in the task word.  Each member -- different hyperparameters, one of them not positive
+    definite (negative noise) -- is bitwise the launch path's, info included."""
+    x, y = o.make_inputs("C1", n=n, seed=11)
+    dev = engine.device()
+    kd = engine.kernel_descriptor(make_kernel(SE, 1), 1)
+    H = torch.linspace(0.06, 0.14, batch, dtype=torch.float64, device=dev).reshape(batch, 1).contiguous()
+    NZ = torch.full((batch,), 1e-2, dtype=torch.float64, device=dev)
+    NZ[1] = -0.5
+    X = torch.tensor(x, dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+    Y = torch.tensor(y, dtype=torch.float64, device=dev).reshape(1, -1).contiguous()
+    res = []
+    for mode in (2, 0):
+        before = engine.nat.chain_stats()["launches"]
+        with engine.nat.thread_tune(chain=mode, chain_max_batch=8):
+            f = engine.AugmentedFactorization(n, 1, 0, batch)
+            f.W.zero_()
+            f.run(kd, H, 1, NZ, 1, X, 0, Y, 0)
+            torch.cuda.synchronize()
+        assert (engine.nat.chain_stats()["launches"] > before) == (mode == 2)
+        res.append((f.info.cpu().clone(), f.out.cpu().clone(), [_lower_b(f, b) for b in range(batch)]))
+    (ic, oc, lc), (il, ol, ll) = res
+    assert torch.equal(ic, il) and int(ic[1]) > 0 and int(ic[0]) == 0
+    for b in range(batch):
+        if b == 1:
+            continue
+        assert np.array_equal(lc[b].view(np.uint64), ll[b].view(np.uint64)), b
+        assert oc[4 * b].item() == ol[4 * b].item()
+        assert float(oc[4 * b]) == pytest.approx(o.nlml(SE, [float(H[b, 0])], 1e-2, x, y), rel=1e-9)
+
+
+def _lower_b(f, b):
+    lay = f.layout
+    w = f.w(b).cpu().numpy()
+    return np.tril(w[: lay.y_row + 1, : lay.y_row + 1])
+
+
+def test_chain_batched_timeout_falls_back():
+    """A forced timeout in a batched persistent launch marks every unfinished member -1 and the whole batch
+    is re-run on the launch path in the same call."""
+    x, y = o.make_inputs("C1", n=1500, seed=12)
+    dev = engine.device()
+    kd = engine.kernel_descriptor(make_kernel(SE, 1), 1)
+    H = torch.tensor([[0.08], [0.1], [0.12]], dtype=torch.float64, device=dev)
+    NZ = torch.tensor([1e-2], dtype=torch.float64, device=dev)
+    X = torch.tensor(x, dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+    Y = torch.tensor(y, dtype=torch.float64, device=dev).reshape(1, -1).contiguous()
+    before = engine.CHAIN_FALLBACKS
+    engine.nat.tune("chain_force_timeout", 1)
+    try:
+        with engine.nat.thread_tune(chain=2, chain_max_batch=8):
+            f = engine.AugmentedFactorization(1500, 1, 0, 3)
+            f.run(kd, H, 1, NZ, 0, X, 0, Y, 0)
+    finally:
+        engine.nat.tune("chain_force_timeout", 0)
+    assert engine.CHAIN_FALLBACKS == before + 1
+    got = f.nlml().cpu().numpy()
+    for b, l in enumerate((0.08, 0.1, 0.12)):
+        assert got[b] == pytest.approx(o.nlml(SE, [l], 1e-2, x, y), rel=1e-9)
