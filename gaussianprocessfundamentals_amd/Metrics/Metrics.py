@@ -7,11 +7,11 @@ The reference binds ``get_alpha`` / ``get_log_determinant`` per numerical handli
   STRICT_INVERSE             alpha = inv(K) y: K^-1 from the identity-augmented factorisation,
                              one device GEMV; logdet = slogdet(K)                (:132-133, :148-149)
   PSEUDO_INVERSE             alpha = pinv(K) y: inv(K) y for a positive-definite K; otherwise the
-                             Jacobi eigendecomposition with tf.linalg.pinv's cutoff (:135-136)
+                             eigendecomposition (gpk_syevd) with tf.linalg.pinv's cutoff (:135-136)
   LINEAR_CONJUGATE_GRADIENT  alpha = linear_cg(K, y, 0) (device GEMV per iteration) (:141-144)
 
 slogdet(K)[1] is log|det K| = 2 sum log diag L for a positive-definite K (the device Cholesky) and
-sum log|lam_i| from the Jacobi eigenvalues otherwise; STRICT_INVERSE of an indefinite nonsingular K
+sum log|lam_i| from the eigenvalues (gpk_syevd) otherwise; STRICT_INVERSE of an indefinite nonsingular K
 (LU in the reference) is V diag(1/lam) V^T.  The eigendecomposition fallback is limited to n <= 16384.
 Subset-of-data approximations (SOD_GRID, SOD_RANDOM) evaluate the exact path on the subset
 (:60-68).  Matrix approximations (:77-126) swap get_covariance_matrix / get_log_determinant:
@@ -206,7 +206,7 @@ class Metric(AbstractMetric):
 
     def get_alpha_pseudo_inverse(self, hyper_parameter: List, noise, y=None, indices=None):
         """pinv(K) y (Metrics.py:135-136): inv(K) y for a positive-definite K; otherwise the
-        eigendecomposition route of tf.linalg.pinv (Jacobi, cutoff 10 n eps max|lam|)."""
+        eigendecomposition route of tf.linalg.pinv (gpk_syevd, cutoff 10 n eps max|lam|)."""
         from .. import engine
         self._require_plain()
         if self._positive_definite(hyper_parameter, noise, indices):

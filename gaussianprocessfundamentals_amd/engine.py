@@ -653,8 +653,8 @@ def pinv_factor(lam: torch.Tensor, V: torch.Tensor, mode: int, rcond: float = -1
 
 
 def pinv_sym(A: torch.Tensor, rcond: float = -1.0) -> torch.Tensor:
-    """tf.linalg.pinv of a symmetric matrix (gpbasics/Statistics/Nystroem_K.py:53): Jacobi
-    eigendecomposition, the reference's cutoff 10 m eps max|lam|, then V diag(1/lam) V^T on MFMA."""
+    """tf.linalg.pinv of a symmetric matrix (gpbasics/Statistics/Nystroem_K.py:53): the eigendecomposition
+    (:func:`eigh`, gpk_syevd), the reference's cutoff 10 m eps max|lam|, then V diag(1/lam) V^T on MFMA."""
     lam, V, _ = eigh(A)
     U, _ = pinv_factor(lam, V, 0, rcond)
     return dgemm(U, V, trans_b=True)
@@ -664,7 +664,7 @@ def pinv_backward(lam: torch.Tensor, V: torch.Tensor, mu: torch.Tensor, Pbar: Op
                   T: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Adjoint of a symmetric A from the adjoint Pbar of pinv(A) (tf.linalg.pinv's reverse mode,
     gpbasics/Statistics/Nystroem_K.py:53): V (F o sym(V^T Pbar V)) V^T with the Daleckii-Krein quotients of
-    f = 1/lam over the kept eigenvalues (gpk_pinv_backward_scale); lam, V from :func:`syevj`, mu the mode-0
+    f = 1/lam over the kept eigenvalues (gpk_pinv_backward_scale); lam, V from :func:`eigh`, mu the mode-0
     factors of :func:`pinv_factor`.  T: the adjoint already in the eigenbasis (V^T Pbar V) instead."""
     m = int(V.shape[-1])
     if T is None:

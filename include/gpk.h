@@ -317,7 +317,7 @@ int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam
                     double* mu, double* U, int32_t* rank_dev, void* stream);
 
 /* Reverse mode of pinv for symmetric matrices (tf.linalg.pinv, Nystroem_K.py:53, as TensorFlow's tape
- * differentiates it): with lam, V the eigendecomposition (gpk_syevj) and mu the mode-0 factors of
+ * differentiates it): with lam, V the eigendecomposition (gpk_syevd or gpk_syevj) and mu the mode-0 factors of
  * gpk_pinv_factor, and T = V^T Pbar V for the adjoint Pbar of pinv(A), replaces T (in place, [batch, m, m])
  * by F o (T + T^T)/2 with F_ij = (mu_i - mu_j) / (lam_i - lam_j) (-mu_i mu_j for two kept values, 0 for two
  * dropped ones); the adjoint of A is then V T V^T. */
