@@ -173,7 +173,10 @@ struct Tune {
   int64_t chain_timeout_ms;  // bound of every wait inside it (then info = -1)
   int64_t chain_group;    //   panels per deferred tile update (1: every tile update one panel deep)
   int64_t chain_max_batch;   // batches of up to this many members run as one persistent launch too ...
-  int64_t chain_batch_max_p; //   ... while the augmented matrix has at most this many rows
+  int64_t chain_batch_max_rows;  // ... while batch x (rows of the augmented matrix) stays within this
+                                 // (batch x span, persistent vs launch path: N = 2048 x 8 1.15 vs 1.38 ms,
+                                 // 4096 x 2 1.87 vs 2.53, 4096 x 4 2.83 vs 3.51; 4096 x 8 5.32 vs 5.07,
+                                 // 2048 x 16 2.02 vs 1.94 -- profiles/r04_chain_batch.jsonl)
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -194,7 +197,7 @@ Tune& tune() {
                          env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024),
                          env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 12416), env_i64("GPK_CHAIN_GRID", 0),
                          env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 4),
-                         env_i64("GPK_CHAIN_MAX_BATCH", 1), env_i64("GPK_CHAIN_BATCH_MAX_P", 4224)};
+                         env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500)};
   return t;
 }
 
@@ -218,7 +221,7 @@ const Knob kKnobs[] = {
     {"chain", &Tune::chain},                 {"chain_max_p", &Tune::chain_max_p},
     {"chain_grid", &Tune::chain_grid},       {"chain_timeout_ms", &Tune::chain_timeout_ms},
     {"chain_group", &Tune::chain_group},     {"chain_max_batch", &Tune::chain_max_batch},
-    {"chain_batch_max_p", &Tune::chain_batch_max_p},
+    {"chain_batch_max_rows", &Tune::chain_batch_max_rows},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -534,7 +537,7 @@ bool chain_applies(const gpk_layout* lay, bool eye, const int64_t* n_dev, const 
                    hipStream_t s) {
   if (!tn.chain || lay->dtype != GPK_F64 || eye || n_dev || m_dev) return false;
   if (lay->batch == 1 ? lay->p > tn.chain_max_p
-                      : (lay->batch > tn.chain_max_batch || lay->p > tn.chain_batch_max_p))
+                      : (lay->batch > tn.chain_max_batch || lay->batch * lay->p > tn.chain_batch_max_rows))
     return false;
   if (tn.diag_dbg != 0 || tn.diag_version == 1) return false;
   if (!plain_stream(s)) return false;

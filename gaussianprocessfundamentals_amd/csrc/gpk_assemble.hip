@@ -17,6 +17,7 @@
 //   Auxiliary/Distances.py:4-7 (GPK_NODE_SE_EXPANDED) or the direct sum of squares.
 //   noise on the training diagonal only: Statistics/CovarianceMatrix.py:197-206; K_ss has none
 //   (:218-225); K_s = k(X, X_test) (:277-286).
+#include <stdlib.h>
 #include <string.h>
 
 #include "gpk_internal.h"
@@ -183,7 +184,79 @@ __device__ __forceinline__ void interior_tree(const gpk_kdesc& kd, const FastNod
   }
 }
 
-template <typename TOut, int D, bool TREE>
+// Trees of exactly two base nodes under one ADD / MUL (postfix [leaf, leaf, op]; SURVEY C5's SE-ARD + PER):
+// leaf by leaf over the lane's 16 rows -- each leaf's op is tile-uniform, so one specialised loop per leaf
+// (its column point, raw / ARD slot / the periodic leaf's sin and cos, in registers) instead of the program
+// loop, value stack and op dispatch per element; the 16 row values stay in registers between the leaves.
+// Same leaf functions and the same combination (below op top) as eval_tree_fast: the same bits.
+template <int D, int OP>
+__device__ __forceinline__ void leaf_rows(FastNode f, const double* prow, const double* pcol, int dp, int c, int r0,
+                                          int mode, double (&acc)[ATILE / 4]) {
+  f.op = OP;  // compile-time op: only its branch of fast_value_at is generated
+  f.d = D;
+  double cb[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) cb[k] = pcol[f.off + c * dp + k];
+#pragma unroll
+  for (int i = 0; i < ATILE / 4; ++i) {
+    const double* pa = prow + f.off + (r0 + 4 * i) * dp;
+    const double v = GPK_ASM_ABLATE ? 0.0 : fast_value_at(f, [pa](int k) { return pa[k]; }, [&cb](int k) { return cb[k]; });
+    acc[i] = mode == 0 ? v : (mode == 1 ? acc[i] + v : acc[i] * v);
+  }
+}
+template <int D>
+__device__ __forceinline__ void leaf_rows_sc(FastNode f, const double* prow, const double* pcol, int dp, int c, int r0,
+                                             int mode, double (&acc)[ATILE / 4]) {
+  f.d = D;
+  double sb[D], cb[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    sb[k] = pcol[f.sc_sin + c * dp + k];
+    cb[k] = pcol[f.sc_cos + c * dp + k];
+  }
+#pragma unroll
+  for (int i = 0; i < ATILE / 4; ++i) {
+    const double* ps = prow + f.sc_sin + (r0 + 4 * i) * dp;
+    const double* pc = prow + f.sc_cos + (r0 + 4 * i) * dp;
+    const double v = GPK_ASM_ABLATE ? 0.0
+                                    : per_sc_value(f, [ps](int k) { return ps[k]; }, [pc](int k) { return pc[k]; },
+                                                   [&sb](int k) { return sb[k]; }, [&cb](int k) { return cb[k]; });
+    acc[i] = mode == 0 ? v : (mode == 1 ? acc[i] + v : acc[i] * v);
+  }
+}
+template <int D>
+__device__ __forceinline__ void leaf_dispatch(const FastNode& f, bool sc_on, const double* prow, const double* pcol,
+                                              int dp, int c, int r0, int mode, double (&acc)[ATILE / 4]) {
+  if (sc_on && f.sc && f.op == GPK_OP_PER) {
+    leaf_rows_sc<D>(f, prow, pcol, dp, c, r0, mode, acc);
+    return;
+  }
+  switch (f.op) {
+    case GPK_OP_SE: leaf_rows<D, GPK_OP_SE>(f, prow, pcol, dp, c, r0, mode, acc); break;
+    case GPK_OP_PER: leaf_rows<D, GPK_OP_PER>(f, prow, pcol, dp, c, r0, mode, acc); break;
+    case GPK_OP_MAT32: leaf_rows<D, GPK_OP_MAT32>(f, prow, pcol, dp, c, r0, mode, acc); break;
+    default: leaf_rows<D, GPK_OP_MAT52>(f, prow, pcol, dp, c, r0, mode, acc); break;
+  }
+}
+template <typename TOut, int D>
+__device__ __forceinline__ void interior_pair(const gpk_kdesc& kd, const FastNode* fns, const double* prow,
+                                              const double* pcol, int dp, int c, int r0, int64_t gi0, int64_t gj,
+                                              double noise, TOut* W, int64_t ld, bool sc_on) {
+  double acc[ATILE / 4];
+  const FastNode f0 = fns[0], f1 = fns[1];
+  leaf_dispatch<D>(f0, sc_on, prow, pcol, dp, c, r0, 0, acc);
+  leaf_dispatch<D>(f1, sc_on, prow, pcol, dp, c, r0, kd.nodes[2].op == GPK_OP_MUL ? 2 : 1, acc);
+#pragma unroll
+  for (int i = 0; i < ATILE / 4; ++i) {
+    double v = acc[i];
+    const int64_t gi = gi0 + r0 + 4 * i;
+    if (gi == gj) v += noise;
+    W[gi * ld + gj] = (TOut)v;
+  }
+}
+
+// TREE: 0 single base node, 1 general tree, 2 two-leaf tree (interior_pair)
+template <typename TOut, int D, int TREE>
 __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& fn, const FastNode* fns, bool fast,
                                            const double* prow, const double* pcol, int slot_stride, int dp, int c,
                                            int r0, int64_t gi0, int64_t gj, double noise, TOut* W, int64_t ld,
@@ -201,6 +274,10 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
       default: return false;
     }
   }
+  if (TREE == 2) {
+    interior_pair<TOut, D>(kd, fns, prow, pcol, dp, c, r0, gi0, gj, noise, W, ld, sc_on);
+    return true;
+  }
   if (!TREE || GPK_ASM_INTERIOR_TREE == 0 || kd.n_ard > 1 || kd.n_nodes > 8) return false;
   interior_tree<TOut, D>(kd, fns, prow, pcol, slot_stride, dp, c, r0, gi0, gj, noise, W, ld, sc_sin, sc_cos, sc_on);
   return true;
@@ -209,7 +286,7 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
 
 // TREE: the instantiation for kernel trees (its interior loop holds two column points in registers;
 // single-node kernels get the lighter instantiation and keep four waves per SIMD)
-template <typename TOut, bool TREE>
+template <typename TOut, int TREE>
 __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int sc_flag;
@@ -899,6 +976,14 @@ hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_
   return hipGetLastError();
 }
 
+static bool tune_pair_off() {  // GPK_ASM_PAIR=0: two-leaf trees through the general tree instantiation (A/B)
+  static const bool off = [] {
+    const char* v = getenv("GPK_ASM_PAIR");
+    return v && *v == '0';
+  }();
+  return off;
+}
+
 hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
                            hipStream_t s) {
   const int nslot = 1 + kd.n_ard + ((a.A == nullptr && sc_node(kd) >= 0) ? 2 : 0);
@@ -914,17 +999,23 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
   } else {
     grid = dim3((unsigned)(a.ntile * (a.ntile + 1) / 2), (unsigned)batch, 1);
   }
-  const bool tree = kd.n_nodes > 1;
+  // instantiation: 0 single base node, 2 two leaves under one ADD / MUL, 1 any other tree
+  const bool pair = kd.n_nodes == 3 && (kd.nodes[2].op == GPK_OP_ADD || kd.nodes[2].op == GPK_OP_MUL);
+  const int tree = kd.n_nodes == 1 ? 0 : (pair && !tune_pair_off() ? 2 : 1);
   if (dtype == GPK_F64) {
-    if (tree)
-      hipLaunchKernelGGL((assemble_kernel<double, true>), grid, dim3(256), lds, s, kd, a);
+    if (tree == 2)
+      hipLaunchKernelGGL((assemble_kernel<double, 2>), grid, dim3(256), lds, s, kd, a);
+    else if (tree == 1)
+      hipLaunchKernelGGL((assemble_kernel<double, 1>), grid, dim3(256), lds, s, kd, a);
     else
-      hipLaunchKernelGGL((assemble_kernel<double, false>), grid, dim3(256), lds, s, kd, a);
+      hipLaunchKernelGGL((assemble_kernel<double, 0>), grid, dim3(256), lds, s, kd, a);
   } else {
-    if (tree)
-      hipLaunchKernelGGL((assemble_kernel<float, true>), grid, dim3(256), lds, s, kd, a);
+    if (tree == 2)
+      hipLaunchKernelGGL((assemble_kernel<float, 2>), grid, dim3(256), lds, s, kd, a);
+    else if (tree == 1)
+      hipLaunchKernelGGL((assemble_kernel<float, 1>), grid, dim3(256), lds, s, kd, a);
     else
-      hipLaunchKernelGGL((assemble_kernel<float, false>), grid, dim3(256), lds, s, kd, a);
+      hipLaunchKernelGGL((assemble_kernel<float, 0>), grid, dim3(256), lds, s, kd, a);
   }
   return hipGetLastError();
 }

@@ -394,7 +394,9 @@ int gpk_timing_reset(void);
  * "chain_max_p" (7424) rows that is not being captured runs as ONE persistent launch -- "chain_grid"
  * workgroups (0: one per CU), every wait bounded by "chain_timeout_ms": 1, the default, auto: unless a
  * factorisation this library enqueued on another stream of the device is still in flight (each
- * persistent launch claims every CU); 2 always; 0 never).  A persistent launch whose wait timed out
+ * persistent launch claims every CU); 2 always; 0 never), with "chain_group" panels per deferred tile update
+ * (4) and, for batches, "chain_max_batch" members (8) while batch x p <= "chain_batch_max_rows" (17500).
+ * A persistent launch whose wait timed out
  * sets info = -1 -- an infrastructure failure, not a non-positive pivot: the factorisation is
  * incomplete and W undefined; re-assemble and re-run it with "chain" 0 (the Python layer does,
  * engine.AugmentedFactorization).  "chain_force_timeout" (testing) makes the next `value` persistent

@@ -27,7 +27,7 @@ for n in [int(a) for a in sys.argv[1:]] or [2048, 4096]:
         H = torch.linspace(0.08, 0.12, batch, dtype=torch.float64, device=dev).reshape(batch, 1).contiguous()
         f = engine.AugmentedFactorization(n, 1, 0, batch)
         for mode in (0, 2):
-            with nat.thread_tune(chain=mode, chain_max_batch=64, chain_batch_max_p=100000):
+            with nat.thread_tune(chain=mode, chain_max_batch=64, chain_batch_max_rows=100000):
                 ts = []
                 for i in range(23):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

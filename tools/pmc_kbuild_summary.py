@@ -1,0 +1,49 @@
+"""Summary of tools/r4d_kbuild_pmc.sh (rocprofv3 PMC passes over tools/bench_kbuild.py C5): per assemble_kernel
+dispatch, the VALU / SALU / LDS instruction counts per matrix element, the VALU issue utilisation, and HBM bytes
+(2 x FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction) against the algorithmic bytes and 8 TB/s.
+
+usage: python tools/pmc_kbuild_summary.py [dir] [n] [d]"""
+import collections
+import csv
+import glob
+import sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/kb"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
+d = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+p = -(-(n + 1) // 128) * 128          # augmented rows (m = 0)
+ntile = p // 64
+elements = ntile * (ntile + 1) // 2 * 64 * 64
+alg_bytes = 8 * p * (p + 64) / 2 + 8 * n * d
+tot = collections.defaultdict(float)
+cnt = collections.Counter()
+dur = []
+for f in sorted(glob.glob(root + "/p*/run_counter_collection.csv")):
+    per = collections.defaultdict(dict)
+    for r in csv.DictReader(open(f)):
+        if "assemble" in r["Kernel_Name"]:
+            per[r["Dispatch_Id"]][r["Counter_Name"]] = per[r["Dispatch_Id"]].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    for dd in per.values():
+        for k, v in dd.items():
+            tot[k] += v
+            cnt[k] += 1
+for f in sorted(glob.glob(root + "/p*/run_kernel_trace.csv"))[:1]:
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(open(f)) if "assemble" in r["Kernel_Name"]]
+avg = {k: tot[k] / cnt[k] for k in tot}
+us = sorted(dur)[len(dur) // 2] if dur else float("nan")
+we = elements / 64.0   # wave-elements (one element per lane)
+print("assemble_kernel, N = %d, D = %d: %d dispatches, median %.1f us, %.3g elements" % (n, d, len(dur), us, elements))
+for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+    if k in avg:
+        print("  %-14s %.4g per dispatch = %.1f per element (per lane)" % (k, avg[k], avg[k] / we))
+if "GRBM_GUI_ACTIVE" in avg:
+    clk = avg["GRBM_GUI_ACTIVE"] / 8 / (us * 1e-6) / 1e9
+    print("  effective clock %.2f GHz (GRBM_GUI_ACTIVE / 8 XCDs / duration)" % clk)
+    if "SQ_INSTS_VALU" in avg:
+        per_simd = avg["SQ_INSTS_VALU"] / 1024
+        cyc = avg["GRBM_GUI_ACTIVE"] / 8
+        print("  VALU wave-instructions per SIMD per cycle %.3f (f64 VALU: 4 cycles each -> at most 0.25)" % (per_simd / cyc))
+if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+    hbm = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+    print("  HBM bytes (2 FETCH + WRITE) %.4g vs algorithmic %.4g (%.2fx); %.0f GB/s = %.1f %% of 8 TB/s" % (
+        hbm, alg_bytes, hbm / alg_bytes, hbm / (us * 1e-6) / 1e9, 100 * hbm / (us * 1e-6) / 8e12))
