@@ -177,6 +177,8 @@ struct Tune {
                                  // (batch x span, persistent vs launch path: N = 2048 x 8 1.15 vs 1.38 ms,
                                  // 4096 x 2 1.87 vs 2.53, 4096 x 4 2.83 vs 3.51; 4096 x 8 5.32 vs 5.07,
                                  // 2048 x 16 2.02 vs 1.94 -- profiles/r04_chain_batch.jsonl)
+  int64_t chain_uq;       //   the next diagonal block's update split by 32-column quarter (0: one task per slice)
+  // (new fields go last: tune() initialises the struct positionally)
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -197,7 +199,8 @@ Tune& tune() {
                          env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024),
                          env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 12416), env_i64("GPK_CHAIN_GRID", 0),
                          env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 4),
-                         env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500)};
+                         env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500),
+                         env_i64("GPK_CHAIN_UQ", 1)};
   return t;
 }
 
@@ -221,7 +224,7 @@ const Knob kKnobs[] = {
     {"chain", &Tune::chain},                 {"chain_max_p", &Tune::chain_max_p},
     {"chain_grid", &Tune::chain_grid},       {"chain_timeout_ms", &Tune::chain_timeout_ms},
     {"chain_group", &Tune::chain_group},     {"chain_max_batch", &Tune::chain_max_batch},
-    {"chain_batch_max_rows", &Tune::chain_batch_max_rows},
+    {"chain_batch_max_rows", &Tune::chain_batch_max_rows}, {"chain_uq", &Tune::chain_uq},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -353,7 +356,7 @@ struct ChainPlan {
   int32_t nblk = 0, nsl = 0, nbc = 0;
 };
 std::mutex g_chain_mu;
-std::map<std::tuple<int, int64_t, int64_t, int, int, int>, ChainPlan> g_chain_plans;
+std::map<std::tuple<int, int64_t, int64_t, int, int, int, int>, ChainPlan> g_chain_plans;
 // Counter scratch of the persistent launch, per (host thread, device, stream): the counters are zeroed
 // by a memset enqueued before each launch, so two threads enqueueing on one stream (torch's null stream
 // is shared by every thread) must never share them -- memset A, memset B, launch A, launch B would hand
@@ -405,7 +408,7 @@ int64_t g_chain_times_n = 0;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
-std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group, int nmem) {
+std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group, int nmem, int chain_uq) {
   const int nblk = (int)(n_pad / NB), yb = (int)(y_row / NB), rlast = (int)(y_row / 32);
   struct Task {
     int ty, k, r, j;
@@ -445,10 +448,20 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
     if (it != last_upd.end()) t.deps.push_back(it->second);
     last_upd[{i, jj}] = add(t);
   };
+  // the next diagonal block's update by panel k, split by 32-column quarter (UQ: U32 with the quarter + 1 in
+  // the type word's bits 2..7): 10 tasks of 32 x 32 x 128 on the chain to D(k + 1) instead of 4 of 32 x 128 x
+  // 128, each loading 64 KB of panel instead of 160 (chain_uq; 0: one U32 per slice)
+  const bool uq = chain_uq != 0;
+  std::map<int, std::vector<int>> uq_of;  // slice s of diagonal block k + 1 -> its UQ tasks (panel k)
   for (int k = 0; k < nblk; ++k) {
     Task d{CHT_D, k, 0, k, dur[0], {}};
     if (k > 0)
-      for (int s = 4 * k; s <= std::min(4 * k + 3, rlast); ++s) d.deps.push_back(u_of(k - 1, s));
+      for (int s = 4 * k; s <= std::min(4 * k + 3, rlast); ++s) {
+        if (uq)
+          for (int t : uq_of[s]) d.deps.push_back(t);
+        else
+          d.deps.push_back(u_of(k - 1, s));
+      }
     D[k] = add(d);
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
       Task t{CHT_S, k, r, 0, dur[1], {D[k]}};
@@ -456,10 +469,21 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
       S[(size_t)k * nr + r] = add(t);
     }
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
+      auto it = last_upd.find({r / 4, k + 1});
+      if (uq && k + 1 < nblk && r < 4 * (k + 2)) {
+        const int rl = r - 4 * (k + 1);
+        for (int q = 0; q <= rl; ++q) {  // lower quarters of the diagonal block's slice r
+          Task t{CHT_U32 | ((q + 1) << 2), k, r, k + 1, dur[2] * 0.5f, {s_of(k, r)}};
+          if (q != rl) t.deps.push_back(s_of(k, 4 * (k + 1) + q));
+          if (it != last_upd.end()) t.deps.push_back(it->second);
+          uq_of[r].push_back(add(t));
+        }
+        U[(size_t)k * nr + r] = uq_of[r].back();  // (not read: D(k + 1) waits for every quarter)
+        continue;
+      }
       Task t{CHT_U32, k, r, k + 1, dur[2], {s_of(k, r)}};
       for (int s = 4 * (k + 1); s <= std::min(4 * (k + 1) + 3, rlast); ++s)
         if (s != r) t.deps.push_back(s_of(k, s));
-      auto it = last_upd.find({r / 4, k + 1});
       if (it != last_upd.end()) t.deps.push_back(it->second);
       U[(size_t)k * nr + r] = add(t);
     }
@@ -559,10 +583,10 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
     const int group = (int)tn.chain_group, nmem = lay->batch;
-    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group, nmem);
+    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
-      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, group, nmem);
+      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq);
       ChainPlan p;
       p.ntasks = (int32_t)(ord.size() / 4);
       p.nblk = (int32_t)(lay->n_pad / NB);
@@ -573,7 +597,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
       it = g_chain_plans.emplace(key, p).first;  // owned for the life of the process
     }
     plan = it->second;
-    ctl_ints = 4 + (size_t)lay->batch * ((size_t)plan.nblk + (size_t)plan.nblk * plan.nsl + (size_t)plan.nsl * plan.nbc);
+    ctl_ints = 4 + (size_t)lay->batch * ((size_t)plan.nblk + 2 * (size_t)plan.nblk * plan.nsl + (size_t)plan.nsl * plan.nbc);
     ctl_ints = (ctl_ints + 3) / 4 * 4;
   }
   {
@@ -602,12 +626,14 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.dflag = ctl + 4;
   a.sdone = a.dflag + plan.nblk;
   a.ucnt = a.sdone + (size_t)plan.nblk * plan.nsl;
+  a.qdone = a.ucnt + (size_t)plan.nsl * plan.nbc;
   a.nsl = plan.nsl;
   a.nbc = plan.nbc;
   a.nmem = lay->batch;
   a.w_bs = lay->w_batch_stride;
   a.inv_bs = lay->inv_batch_stride;
-  a.ctl_stride = (int64_t)plan.nblk + (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
+  a.ctl_stride = (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
+  a.uq = tn.chain_uq != 0 ? 1 : 0;
   a.row_end = lay->y_row + 1;
   a.timeout = std::max<int64_t>(1, tn.chain_timeout_ms) * 100000;  // 100 MHz ticks
   for (int64_t f = g_chain_force_timeout.load(); f > 0;)
@@ -1863,7 +1889,7 @@ int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_ou
   if (y_row < n_pad) return fail_arg(2, "y_row (>= n_pad)");
   if (grid <= 0) return fail_arg(3, "grid");
   if (!ntasks) return fail_arg(6, "ntasks");
-  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, (int)tune_now().chain_group, 1);
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, (int)tune_now().chain_group, 1, (int)tune_now().chain_uq);
   *ntasks = (int64_t)(ord.size() / 4);
   if (tasks_out) {
     if (cap < *ntasks) return fail_arg(5, "cap (fewer than ntasks)");

@@ -152,6 +152,8 @@ struct ChainArgs {
   int32_t* dflag;        // [nblk]: D(k) done
   int32_t* sdone;        // [nblk][nsl]: S(k, r) done
   int32_t* ucnt;         // [nsl][nbc]: panels applied to slice r of block column j
+  int32_t* qdone;        // [nblk][nsl]: quarter updates (UQ) of panel k done on slice r of diagonal block k + 1
+  int32_t uq;            // D(k) waits for the UQ tasks of panel k - 1 (else for ucnt)
   int32_t nsl, nbc;      // live 32-row slices (the last one holds the y row), live block columns
   int32_t nmem;          // members (task word bits 8..): W + m w_bs, Winv + m inv_bs, info + m, counters + m ctl_stride
   int64_t w_bs, inv_bs, ctl_stride;

@@ -639,6 +639,8 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 //                 left it; L_kk to W, L_kk^-1 to Winv; dflag[k]
 //   S(k, r)       slice r below block k: X = A(r, k) L_kk^-T, in place; sdone[k][r]
 //   U32(q, r, j)  slice r of block column j = q + 1: C -= X(r, q) X(j, q)^T; ucnt[r][j] = q + 1
+//   UQ(q, r, j, c) the same on the 32-column quarter c only, for the slices r of diagonal block j (round 4);
+//                 qdone[q][r] += 1 -- D(j) waits for all of them
 //   BLK(q, i, j)  128 x 128 tile (i, j), j >= q + 2: C -= X(i, q..) X(j, q..)^T over g panels q .. q + g - 1
 //                 (g = 1 for the columns the diagonal chain needs soon, g = the planner's group for the deferred
 //                 ones: the launch path's deep group update); ucnt[r][j] = q + g for the slices r of block i
@@ -755,6 +757,61 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
   for (int i = 0; i < 4; ++i) {
     if (live0) sts<true>(Cr + 4 * i * ld, acc0[i]);
     if (live1) sts<true>(Cr + (16 + 4 * i) * ld, acc1[i]);
+  }
+}
+
+// UQ: the 32 x 32 quarter q of slice r in the next diagonal block, C -= A B^T with A = X(r) [32 x 128] and
+// B = X(slice q of that block) [32 x 128] (K = 128, panel k): one 16 x 16 block per wave for waves 0..3 (wave w:
+// rows 16 (w & 1), columns 16 (w >> 1)), the A rows staged in LDS by all 8 waves as in slab_gemm, the wave's B
+// rows straight to registers.  Every accumulator runs slab_gemm's k-steps in its order (the same bits as the
+// per-slice U32 and the launch path); on the diagonal quarter the block right of the diagonal is skipped.
+// 64 KB of operands per task instead of U32's 160 KB: the update that gates the next diagonal block.
+__device__ __forceinline__ void slab_q(const double* A, const double* B, int64_t ld, double* C, bool diag, uint64_t* st,
+                                       char* smem) {
+  typedef double dbl2 __attribute__((ext_vector_type(2)));
+  const int tid = opaque_tid();
+  const int lane = tid & 63;
+  const int w = wave_uniform(tid >> 6);
+  const int lr = lane & 15, q = lane >> 4;
+  const int rb = w & 1, cbl = (w >> 1) & 1;
+  const bool active = w < 4 && (!diag || cbl <= rb);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 4 * w + i;
+    glds16a<kLdAux>(A + (int64_t)row * ld + 2 * lane, smem + row * SLAB_LDS_ROW);
+  }
+  const __amdgpu_buffer_rsrc_t brs = uniform_rsrc(B), crs = uniform_rsrc(C);
+  const int bvo = (int)(((int64_t)(cbl * 16 + lr) * ld + 2 * q) * 8);
+  const int cvo = (int)(((int64_t)(rb * 16 + q) * ld + cbl * 16 + lr) * 8);  // C/D layout: row q + 4 i, column lr
+  const int ldc4 = __builtin_amdgcn_readfirstlane((int)(4 * ld * 8));
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = ld8_buf(crs, cvo, i * ldc4);
+  }
+  dbl2 bv[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) bv[j] = ld16_buf(brs, active ? bvo + j * 64 : kRsrcBytes, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA writes are not tracked by hipcc)
+  __syncthreads();
+  if (st && w == 0) st[4] = __builtin_amdgcn_s_memrealtime();  // (profiling: operands in place)
+  if (active) {
+    const char* a0 = smem + (rb * 16 + lr) * SLAB_LDS_ROW + q * 16;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const dbl2 x = *reinterpret_cast<const dbl2*>(a0 + j * 64);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x[e], bv[j][e], acc, 0, 0, 1);
+    }
+  }
+  if (st && w == 0) {
+    const int dep = __builtin_amdgcn_readfirstlane((int)acc[3]);
+    st[5] = __builtin_amdgcn_s_memrealtime() + (dep == 0x7fffffff ? 1 : 0);
+  }
+  if (active) {
+    double* Cr = C + (int64_t)(rb * 16 + q) * ld + cbl * 16 + lr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sts<true>(Cr + 4 * i * ld, acc[i]);
   }
 }
 
@@ -890,6 +947,12 @@ GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int 
   double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
   slab_gemm<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem);
 }
+GPK_CHAIN_FN void chain_uq(double* W, int64_t ld, int k, int r, int j, int qq, uint64_t* st, char* smem) {
+  const int64_t R = (int64_t)r * 32;
+  const int64_t J = (int64_t)j * NB;
+  const int64_t Bq = J + 32 * qq;  // rows of slice qq of block j = its quarter qq of columns
+  slab_q(W + R * ld + (int64_t)k * NB, W + Bq * ld + (int64_t)k * NB, ld, W + R * ld + Bq, R == Bq, st, smem);
+}
 GPK_CHAIN_FN void chain_u32(double* W, int64_t ld, int q, int r, int j, uint64_t* st, char* smem) {
   const int64_t R = (int64_t)r * 32;
   const int64_t J = (int64_t)j * NB;
@@ -932,15 +995,24 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, in
   const int32_t* sdone = a.sdone + co;
   const int32_t* ucnt = a.ucnt + co;
   if (ty == CH_D) {
-    if (k > 0)
+    if (k > 0 && a.uq) {
+      // every quarter update of panel k - 1 on the block's slices (slice s has s - 4 k + 1 of them)
+      const int32_t* qd = a.qdone + co + (int64_t)(k - 1) * a.nsl;
+      for (int s = 4 * k; s <= 4 * k + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, qd + s, s - 4 * k + 1, t0);
+    } else if (k > 0) {
       for (int s = 4 * k; s <= 4 * k + 3 && ok; ++s) ok = chain_wait(a, ucnt + (int64_t)s * a.nbc + k, k, t0);
+    }
   } else if (ty == CH_S) {
     ok = chain_wait(a, dflag + k, 1, t0);
     if (ok && k > 0) ok = chain_wait(a, ucnt + (int64_t)r * a.nbc + k, k, t0);
   } else if (ty == CH_U32) {
     const int32_t* sd = sdone + (int64_t)k * a.nsl;
     ok = chain_wait(a, sd + r, 1, t0);
-    for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+    if (g > 1) {  // UQ, quarter g - 2: slice 4 j + quarter of the panel
+      if (ok) ok = chain_wait(a, sd + 4 * j + (g - 2), 1, t0);
+    } else {
+      for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+    }
     if (ok && k > 0) ok = chain_wait(a, ucnt + (int64_t)r * a.nbc + j, k, t0);
   } else {
     // BLK over the g panels k .. k + g - 1: the last panel's solves of both blocks' slices (S(q, r) done
@@ -971,7 +1043,8 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     const int t = __builtin_amdgcn_readfirstlane(slot[0]);
     if (t >= a.ntasks) break;
     const int tyg = __builtin_amdgcn_readfirstlane(a.tasks[4 * t]);
-    const int ty = tyg & 3, g = ((tyg >> 2) & 63) + 1, mem = tyg >> 8;  // (BLK: updates over g panels; member)
+    // BLK: updates over g panels; U32 with g > 1: the quarter g - 2 task (UQ); member
+    const int ty = tyg & 3, g = ((tyg >> 2) & 63) + 1, mem = tyg >> 8;
     double* const Wm = a.W + (int64_t)mem * a.w_bs;
     const int64_t co = (int64_t)mem * a.ctl_stride;
     const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
@@ -999,6 +1072,8 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     } else if (ty == CH_S) {
       chain_s(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
               reinterpret_cast<char*>(sm));
+    } else if (ty == CH_U32 && g > 1) {
+      chain_uq(Wm, a.ld, k, r, j, g - 2, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
     } else if (ty == CH_U32) {
       chain_u32(Wm, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
     } else {
@@ -1019,6 +1094,11 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
         st_flag(a.dflag + co + k, 1);
       } else if (ty == CH_S) {
         st_flag(a.sdone + co + (int64_t)k * a.nsl + r, 1);
+      } else if (ty == CH_U32 && g > 1) {
+        // +1 from lane 0 only (every lane of wave 0 executes this: an add of 1 would count 64; the compiler
+        // reduces the lanes' values and issues one atomic)
+        __hip_atomic_fetch_add((gi32*)(a.qdone + co + (int64_t)k * a.nsl + r), (threadIdx.x & 63) == 0 ? 1 : 0,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else if (ty == CH_U32) {
         st_flag(a.ucnt + co + (int64_t)r * a.nbc + j, k + 1);
       } else {

@@ -125,3 +125,17 @@ def test_thread_tune_is_per_thread(lib):
     with pytest.raises(Exception):
         with _native.thread_tune(no_such_knob=1):
             pass
+
+
+def test_knob_defaults_land_in_their_fields(lib):
+    """tune() initialises its struct positionally: every knob reads back its documented default (a field
+    inserted out of order shifts the values of the ones after it)."""
+    import os
+    expect = {"chain": 1, "chain_max_p": 12416, "chain_grid": 0, "chain_timeout_ms": 1000, "chain_group": 4,
+              "chain_max_batch": 8, "chain_batch_max_rows": 17500, "chain_uq": 1, "group": 8, "lookahead": 2,
+              "fuse_kbuild": 1, "diag_version": 2}
+    for k, v in expect.items():
+        if os.environ.get("GPK_" + k.upper()):
+            continue
+        old = _native.tune(k, v)
+        assert old == v, (k, old)

@@ -35,13 +35,15 @@ def shape(n, m):
 
 
 def decode(task):
-    """(type, k, r, j, g): BLK tasks carry ty = 3 | (g - 1) << 2 for an update over panels k .. k + g - 1."""
+    """(type, k, r, j, g): BLK tasks carry ty = 3 | (g - 1) << 2 for an update over panels k .. k + g - 1; a U32
+    task with g > 1 is the quarter g - 2 (UQ) of slice r in diagonal block j; bits 8.. hold the member."""
     tyg, k, r, j = (int(v) for v in task)
-    return tyg & 3, k, r, j, (tyg >> 2) + 1
+    return tyg & 3, k, r, j, ((tyg >> 2) & 63) + 1
 
 
-def cells(task, nsl):
-    """(reads, writes) of a task as sets of (slice, block column) cells plus ('inv', k)."""
+def cells(task, nsl, uq=False):
+    """(reads, writes) of a task as sets of (slice, block column) cells plus ('inv', k) and, for the quarter
+    updates (UQ), ('q', slice, block column, quarter)."""
     ty, k, r, j, g = decode(task)
 
     def sl(b):
@@ -49,21 +51,27 @@ def cells(task, nsl):
 
     if ty == D:
         c = {(s, k) for s in sl(k)}
-        return c, c | {("inv", k)}
+        qc = {("q", s, k, q) for s in sl(k) for q in range(s - 4 * k + 1)} if (uq and k > 0) else set()
+        return c | qc, c | {("inv", k)}
     if ty == S:
         return {(r, k), ("inv", k)}, {(r, k)}
+    if ty == U32 and g > 1:
+        q = g - 2
+        return {(r, k), (4 * j + q, k), (r, j)}, {("q", r, j, q)}
     if ty == U32:
         return {(r, k), (r, j)} | {(s, k) for s in sl(j)}, {(r, j)}
     rd = {(s, q) for s in sl(r) + sl(j) for q in range(k, k + g)} | {(s, j) for s in sl(r)}
     return rd, {(s, j) for s in sl(r)}
 
 
-def waits(task, nsl):
+def waits(task, nsl, uq=False):
     """The kernel's waits (chain_kernel, dependency section): (counter, index, value >= )."""
     ty, k, r, j, g = decode(task)
     out = []
     if ty == D:
-        if k > 0:
+        if k > 0 and uq:
+            out += [("qdone", (k - 1, s), s - 4 * k + 1) for s in range(4 * k, 4 * k + 4) if s < nsl]
+        elif k > 0:
             out += [("ucnt", (s, k), k) for s in range(4 * k, 4 * k + 4)]
     elif ty == S:
         out.append(("dflag", k, 1))
@@ -71,7 +79,10 @@ def waits(task, nsl):
             out.append(("ucnt", (r, k), k))
     elif ty == U32:
         out.append(("sdone", (k, r), 1))
-        out += [("sdone", (k, s), 1) for s in range(4 * j, 4 * j + 4) if s < nsl]
+        if g > 1:
+            out.append(("sdone", (k, 4 * j + g - 2), 1))
+        else:
+            out += [("sdone", (k, s), 1) for s in range(4 * j, 4 * j + 4) if s < nsl]
         if k > 0:
             out.append(("ucnt", (r, j), k))
     else:
@@ -89,6 +100,8 @@ def publishes(task, nsl):
         return [("dflag", k, 1)]
     if ty == S:
         return [("sdone", (k, r), 1)]
+    if ty == U32 and g > 1:
+        return [("qdone", (k, r), "+1")]
     if ty == U32:
         return [("ucnt", (r, j), k + 1)]
     return [("ucnt", (s, j), k + g) for s in range(4 * r, 4 * r + 4) if s < nsl]
@@ -96,7 +109,8 @@ def publishes(task, nsl):
 
 def simulate(tasks, nsl, workers, rng):
     """Claim in list order; start = max(worker free, every wait's publish time); check cell versions."""
-    pub = {}           # (counter, index) -> list of (value, time)
+    uq = any(decode(t)[0] == U32 and decode(t)[4] > 1 for t in tasks)
+    pub = {}           # (counter, index) -> list of (value, time); counters added to: value = "+1"
     last_w = {}        # cell -> finish time of the last earlier-claimed writer
     readers = {}       # cell -> finish times of earlier-claimed readers since that writer
     free = [0.0] * workers
@@ -104,11 +118,18 @@ def simulate(tasks, nsl, workers, rng):
     for t, task in enumerate(tasks):
         w = int(np.argmin(free))
         start = free[w]
-        for cnt, idx, v in waits(task, nsl):
-            hits = [tm for (val, tm) in pub.get((cnt, idx), []) if val >= v]
+        for cnt, idx, v in waits(task, nsl, uq):
+            got = pub.get((cnt, idx), [])
+            if got and got[0][0] == "+1":   # a counter of increments: the v-th finished add
+                times = sorted(tm for _, tm in got)
+                assert len(times) >= v, "task %d %s waits on %s%s >= %d, added to %d times earlier" % (
+                    t, task, cnt, idx, v, len(times))
+                start = max(start, times[v - 1])
+                continue
+            hits = [tm for (val, tm) in got if val >= v]
             assert hits, "task %d %s waits on %s%s >= %d, set by no earlier task" % (t, task, cnt, idx, v)
             start = max(start, min(hits))
-        rd, wr = cells(task, nsl)
+        rd, wr = cells(task, nsl, uq)
         for c in rd | wr:  # read-after-write / write-after-write: the last writer is done
             assert start >= last_w.get(c, 0.0), "task %d %s starts before the last writer of %s" % (t, task, c)
         ty, g = decode(task)[0], decode(task)[4]
@@ -156,6 +177,10 @@ def run_tasks(W, tasks, nblk):
         elif ty == S:
             R = slice(SL * r, SL * r + SL)
             W[R, K] = W[R, K] @ inv[k].T
+        elif ty == U32 and g > 1:
+            q = g - 2
+            R, Q = slice(SL * r, SL * r + SL), slice(NB * j + SL * q, NB * j + SL * q + SL)
+            W[R, Q] -= W[R, K] @ W[Q, K].T
         elif ty == U32:
             R, J = slice(SL * r, SL * r + SL), slice(NB * j, NB * j + NB)
             W[R, J] -= W[R, K] @ W[J, K].T
@@ -165,12 +190,9 @@ def run_tasks(W, tasks, nblk):
     return W
 
 
-def plan(n_pad, y_row, grid, group):
-    old = nat.tune("chain_group", group)
-    try:
+def plan(n_pad, y_row, grid, group, uq=1):
+    with nat.thread_tune(chain_group=group, chain_uq=uq):
         return nat.chain_plan(n_pad, y_row, grid)
-    finally:
-        nat.tune("chain_group", old)
 
 
 def applied_panels(tasks, nblk):
@@ -184,35 +206,37 @@ def applied_panels(tasks, nblk):
 
 
 @pytest.mark.parametrize("n,m", [(1, 0), (128, 0), (300, 0), (700, 37), (1000, 200), (2048, 0), (3000, 0)])
-@pytest.mark.parametrize("group", [1, 4, 8])
-def test_chain_plan_waits_cover_every_dependency(n, m, group):
+@pytest.mark.parametrize("group,uq", [(1, 1), (4, 1), (8, 1), (4, 0)])
+def test_chain_plan_waits_cover_every_dependency(n, m, group, uq):
     _lib_or_skip()
     n_pad, y_row, p = shape(n, m)
     nsl = y_row // SL + 1
     rng = np.random.default_rng(n + m)
     nblk, yb = n_pad // NB, y_row // NB
     for grid in (1, 3, 16, 256):
-        tasks = plan(n_pad, y_row, grid, group)
+        tasks = plan(n_pad, y_row, grid, group, uq)
         kinds = np.bincount(tasks[:, 0] & 3, minlength=4)
+        nq = int(np.sum(((tasks[:, 0] & 3) == U32) & (((tasks[:, 0] >> 2) & 63) > 0)))
+        assert nq == (10 * (nblk - 1) if uq else 0)   # 1 + 2 + 3 + 4 quarters per next diagonal block
         assert kinds[D] == nblk
         assert len({tuple(t) for t in tasks.tolist()}) == len(tasks)
         upd = applied_panels(tasks, nblk)
         exp = [(q, i, j) for q in range(nblk) for j in range(q + 2, yb + 1) for i in range(j, yb + 1)]
         assert sorted(upd) == sorted(exp)           # every (panel, tile) update exactly once
         if group > 1 and nblk >= 2 * group + 2:
-            assert (tasks[:, 0] >> 2).max() == group - 1   # deep updates are used
+            assert (tasks[(tasks[:, 0] & 3) == BLK, 0] >> 2).max() == group - 1   # deep updates are used
         for _ in range(3):
             simulate(tasks, nsl, grid, rng)
 
 
 @pytest.mark.parametrize("n,m", [(200, 0), (600, 50), (1100, 0), (2100, 40)])
-@pytest.mark.parametrize("group", [1, 4])
-def test_chain_plan_reproduces_the_blocked_factorisation(n, m, group):
+@pytest.mark.parametrize("group,uq", [(1, 0), (4, 1)])
+def test_chain_plan_reproduces_the_blocked_factorisation(n, m, group, uq):
     _lib_or_skip()
     rng = np.random.default_rng(7)
     n_pad, y_row, p = shape(n, m)
     W0, (xt, xs, y, noise, k) = augmented(n, m, rng)
-    tasks = plan(n_pad, y_row, 64, group)
+    tasks = plan(n_pad, y_row, 64, group, uq)
     W = run_tasks(W0.copy(), tasks, n_pad // NB)
     Kn = k(xt, xt) + noise * np.eye(n)
     L = np.linalg.cholesky(Kn)
