@@ -391,11 +391,13 @@ int gpk_timing_reset(void);
  * same bits, slower -- for A/B checks), "trd_split_m" (gpk_syevd: above this m, at most 1024, the
  * tridiagonalisation's A22 v runs over the chip, three launches per column, instead of one workgroup per
  * panel; default 1024), "chain" (every f64, batch-1, non-ragged factorisation with at most
- * "chain_max_p" (7424) rows that is not being captured runs as ONE persistent launch -- "chain_grid"
+ * "chain_max_p" (12416) rows that is not being captured runs as ONE persistent launch -- "chain_grid"
  * workgroups (0: one per CU), every wait bounded by "chain_timeout_ms": 1, the default, auto: unless a
  * factorisation this library enqueued on another stream of the device is still in flight (each
  * persistent launch claims every CU); 2 always; 0 never), with "chain_group" panels per deferred tile update
- * (4) and, for batches, "chain_max_batch" members (8) while batch x p <= "chain_batch_max_rows" (17500).
+ * (4), "chain_uq" (1: the next diagonal block's update by each panel as 32-column quarter tasks; 0: one task
+ * per 32-row slice) and, for batches, "chain_max_batch" members (8) while batch x p <= "chain_batch_max_rows"
+ * (17500).
  * A persistent launch whose wait timed out
  * sets info = -1 -- an infrastructure failure, not a non-positive pivot: the factorisation is
  * incomplete and W undefined; re-assemble and re-run it with "chain" 0 (the Python layer does,
