@@ -643,12 +643,19 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     }
   if (env_i64("GPK_CHAIN_TIMES", 0)) {
     std::lock_guard<std::mutex> lk(g_chain_mu);
-    if (g_chain_times_n < a.ntasks) {
+#ifndef GPK_DIAG_PROF
+#define GPK_DIAG_PROF 0
+#endif
+    // (GPK_DIAG_PROF builds: the D tasks' phase stamps follow the task stamps, 8 steps x 8 waves x 6 per block,
+    // read back as extra "tasks" of gpk_chain_times)
+    const int64_t extra = GPK_DIAG_PROF ? (int64_t)plan.nblk * 8 * 8 : 0;
+    if (g_chain_times_n < a.ntasks + extra) {
       if (g_chain_times) hipFree(g_chain_times);
-      GPK_HIP(hipMalloc(&g_chain_times, (size_t)a.ntasks * 6 * sizeof(uint64_t)), "chain times");
-      g_chain_times_n = a.ntasks;
+      GPK_HIP(hipMalloc(&g_chain_times, (size_t)(a.ntasks + extra) * 6 * sizeof(uint64_t)), "chain times");
+      g_chain_times_n = a.ntasks + extra;
     }
     a.times = g_chain_times;
+    if (extra) a.dprof = g_chain_times + (size_t)a.ntasks * 6;
   }
   if (env_i64("GPK_CHAIN_TRACE", 0)) {
     std::lock_guard<std::mutex> lk(g_chain_mu);

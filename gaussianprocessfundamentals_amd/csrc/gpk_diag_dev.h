@@ -53,6 +53,189 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+#ifndef GPK_DIAG_PROF
+#define GPK_DIAG_PROF 0
+#endif
+#ifndef GPK_POTF2_MODE
+#define GPK_POTF2_MODE 2  // pivot column broadcast: 2 DPP row_newbcast, 1 v_readlane, 0 LDS (rounds 1-4; A/B builds)
+#endif
+#define GPK_POTF2_READLANE (GPK_POTF2_MODE == 1)
+#ifndef GPK_POTF2_PIPE
+#define GPK_POTF2_PIPE 1  // mode 2: the software-pipelined issue order (potf2_pipelined)
+#endif
+// lane l's value of v, wave-uniform (two v_readlane_b32 into SGPRs; l a compile-time lane)
+__device__ __forceinline__ double bcast_lane(double v, int l) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// Lane C of each 16-lane row of the wave, as a 64-bit DPP move (row_newbcast), and w += (lane C's u) * ng as
+// one DPP-sourced f64 FMA.  (s_nop 1: a VALU write of a VGPR needs two wait states before a DPP read of it --
+// the compiler's hazard recognizer does not see into inline asm.  Wave 0 runs these with every lane active.)
+#ifndef GPK_DPP_VOLATILE
+#define GPK_DPP_VOLATILE 0  // 1: the DPP statements in program order (asm volatile); 0: the scheduler interleaves them
+#endif
+#if GPK_DPP_VOLATILE
+#define GPK_DPP_VOL volatile
+#else
+#define GPK_DPP_VOL
+#endif
+template <int C>
+__device__ __forceinline__ double row_bcast(double v) {
+  double r;
+  asm GPK_DPP_VOL("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "n"(C));
+  return r;
+}
+template <int C>
+__device__ __forceinline__ void fmac_row_bcast(double& w, double u, double ng) {
+  asm GPK_DPP_VOL("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(w) : "v"(u), "v"(ng),
+      "n"(C));
+}
+// potf2 pivot J (mode 2): every 16-lane row holds the whole problem -- lane r the tile row r (w) and column r of
+// the inverse (v) -- so column J of the tile, entry (c, J) in lane c's w[J], reaches every lane of the row by DPP
+// inside the FMAs; the same arithmetic as the other modes: a = x[J] / L[J][J]; x[J] = a; x[c] -= (a / L[J][J]) u[c]
+template <int J, int C>
+struct Potf2Upd {
+  static __device__ __forceinline__ void run(double* w, double* v, double u, double ngw, double ngv) {
+    fmac_row_bcast<C>(w[C], u, ngw);
+    fmac_row_bcast<C>(v[C], u, ngv);
+    Potf2Upd<J, C + 1>::run(w, v, u, ngw, ngv);
+  }
+};
+template <int J>
+struct Potf2Upd<J, 16> {
+  static __device__ __forceinline__ void run(double*, double*, double, double, double) {}
+};
+template <int J>
+struct Potf2Step {
+  static __device__ __forceinline__ void run(double* w, double* v, int& bad) {
+    const double u = w[J];
+    const double piv = row_bcast<J>(u);
+    bad = (bad == 0 && !(piv > 0.0)) ? J + 1 : bad;
+    const double ri = rsqrt_refined(piv);  // 1 / L[J][J]
+    const double aw = u * ri, av = v[J] * ri;
+    const double ngw = -(aw * ri), ngv = -(av * ri);
+    w[J] = aw;
+    v[J] = av;
+    Potf2Upd<J, J + 1>::run(w, v, u, ngw, ngv);
+    Potf2Step<J + 1>::run(w, v, bad);
+  }
+};
+template <>
+struct Potf2Step<16> {
+  static __device__ __forceinline__ void run(double*, double*, int&) {}
+};
+
+template <int C>
+__device__ __forceinline__ void fmac_bcast_v(double& w, double u, double ng) {
+  // (no wait states: u was written many instructions earlier -- tools/isa_dpp_hazard.py checks the binary)
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(w) : "v"(u), "v"(ng),
+               "n"(C));
+}
+template <int C>
+__device__ __forceinline__ double bcast_v(double v) {
+  double r;
+  asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "n"(C));
+  return r;
+}
+__device__ __forceinline__ double vmul(double a, double b) {
+  double r;
+  asm volatile("v_mul_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmul_mhalf(double a) {  // a * -0.5
+  double r;
+  asm volatile("v_mul_f64 %0, %1, -0.5" : "=v"(r) : "v"(a));
+  return r;
+}
+__device__ __forceinline__ double vmul_neg(double a, double b) {  // a * (-b)
+  double r;
+  asm volatile("v_mul_f64 %0, %1, -%2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vfma(double a, double b, double c) {
+  double r;
+  asm volatile("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ double vrsq(double a) {
+  double r;
+  asm volatile("v_rsq_f64 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+// deferred FMA number D of pivot J - 1 (issued during pivot J): v[J] first (this pivot's a reads it), then
+// w[c], v[c] for c = J + 1 .. 15 (w[J] was the previous pivot's critical FMA)
+template <int J, int D>
+struct DeferOp {
+  static __device__ __forceinline__ void run(double* w, double* v, double up, double ngw, double ngv) {
+    constexpr int ND = (J == 0) ? 0 : 1 + 2 * (DB - 1 - J);
+    if constexpr (D < ND) {
+      // (entry c takes column entry (c, J - 1), i.e. lane c's u)
+      if constexpr (D == 0) {
+        fmac_bcast_v<J>(v[J], up, ngv);
+      } else {
+        constexpr int C = J + 1 + (D - 1) / 2;
+        if constexpr (((D - 1) & 1) != 0)
+          fmac_bcast_v<C>(v[C], up, ngv);
+        else
+          fmac_bcast_v<C>(w[C], up, ngw);
+      }
+    }
+  }
+};
+template <int J, int D0, int D1>
+struct DeferRange {
+  static __device__ __forceinline__ void run(double* w, double* v, double up, double ngw, double ngv) {
+    if constexpr (D0 < D1 && D0 < 2 * DB) {
+      DeferOp<J, D0>::run(w, v, up, ngw, ngv);
+      DeferRange<J, D0 + 1, D1>::run(w, v, up, ngw, ngv);
+    }
+  }
+};
+template <int J>
+struct PipeStep {
+  static __device__ __forceinline__ void run(double* w, double* v, int& bad, double up, double ngwp, double ngvp,
+                                             double c15) {
+    if constexpr (J < DB) {
+      const double u = w[J];
+      const double piv = bcast_v<J>(u);
+      bad = (bad == 0 && !(piv > 0.0)) ? J + 1 : bad;
+      const double r0 = vrsq(piv);
+      const double hn = vmul_mhalf(piv);
+      DeferRange<J, 0, 3>::run(w, v, up, ngwp, ngvp);
+      double t = vmul(hn, r0);
+      DeferRange<J, 3, 4>::run(w, v, up, ngwp, ngvp);
+      t = vfma(t, r0, c15);
+      DeferRange<J, 4, 5>::run(w, v, up, ngwp, ngvp);
+      const double r1 = vmul(r0, t);
+      DeferRange<J, 5, 6>::run(w, v, up, ngwp, ngvp);
+      t = vmul(hn, r1);
+      DeferRange<J, 6, 7>::run(w, v, up, ngwp, ngvp);
+      t = vfma(t, r1, c15);
+      DeferRange<J, 7, 8>::run(w, v, up, ngwp, ngvp);
+      const double ri = vmul(r1, t);  // 1 / L[J][J]
+      DeferRange<J, 8, 9>::run(w, v, up, ngwp, ngvp);
+      const double aw = vmul(u, ri), av = vmul(v[J], ri);
+      const double ngw = vmul_neg(aw, ri), ngv = vmul_neg(av, ri);
+      if constexpr (J + 1 < DB) fmac_bcast_v<J + 1>(w[J + 1], u, ngw);  // the next pivot's input
+      DeferRange<J, 9, 2 * DB>::run(w, v, up, ngwp, ngvp);       // the rest of the previous pivot's FMAs
+      w[J] = aw;
+      v[J] = av;
+      PipeStep<J + 1>::run(w, v, bad, u, ngw, ngv, c15);
+    }
+  }
+};
+// pivot j's chain: bcast -> rsq -> 2 Newton steps -> a -> -a / L[j][j] -> the FMA of entry j + 1 (the next
+// pivot's input), ~110 cycles; its other 2 (15 - j) FMAs go into the latency gaps of pivot j + 1's chain instead
+// of in front of it.  Every instruction pinned in that order (asm volatile).  Measured per wave (tools/probe):
+// dependent f64 FMA 8 cycles, rsq 20, 64-bit DPP move 16 (with its two wait states), independent f64 FMA issue
+// 5, mode 0's LDS round trip 112.  The same operations on the same values as the other modes: the same bits.
+__device__ __forceinline__ void potf2_pipelined(double* w, double* v, int& bad) {
+  PipeStep<0>::run(w, v, bad, 0.0, 0.0, 0.0, 1.5);
+}
+
 // potf2 + inverse of tile (kb, kb), one wave.  Lanes 0..15 hold row r = lane of the tile and
 // factor it (right-looking); lanes 16..31 hold column r = lane - 16 of the identity and turn it
 // into column r of L^-1 (column-oriented forward substitution).  Both run the SAME update per
@@ -67,6 +250,38 @@ __device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf
   const int r = lane & 15;
   const bool inv = (lane & 16) != 0;
   const int c0 = kb * DB;
+#if GPK_POTF2_MODE == 2
+  {
+    (void)inv;
+    (void)colbuf;
+    double w[DB], v[DB];
+#pragma unroll
+    for (int c = 0; c < DB; c += 2) {
+      const dbl2 t = *reinterpret_cast<const dbl2*>(A + aidx(c0 + r, c0 + c));
+      w[c] = t.x;
+      w[c + 1] = t.y;
+      v[c] = (c == r) ? 1.0 : 0.0;
+      v[c + 1] = (c + 1 == r) ? 1.0 : 0.0;
+    }
+    int bad = 0;
+#if GPK_POTF2_PIPE
+    potf2_pipelined(w, v, bad);
+#else
+    Potf2Step<0>::run(w, v, bad);
+#endif
+#pragma unroll
+    for (int c = 0; c < DB; ++c) asm volatile("" : "+v"(w[c]), "+v"(v[c]));  // (computed here, every lane active)
+    if (bad != 0 && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + bad);
+    if (lane < DB) {
+#pragma unroll
+      for (int c = 0; c < DB; ++c) A[aidx(c0 + r, c0 + c)] = (c <= r) ? w[c] : 0.0;
+    } else if (lane < 2 * DB) {
+#pragma unroll
+      for (int rr = 0; rr < DB; ++rr) Dk[rr * DBS + r] = v[rr];  // Dinv[rr][r]
+    }
+    return;
+  }
+#endif
   // rows: entries above the diagonal are never used (only c <= r is stored, and column j is
   // read from rows c >= j only), so the tile row is loaded whole
   double w[DB];
@@ -79,6 +294,14 @@ __device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf
   int bad = 0;  // first non-positive pivot of this tile (1-based in the tile), wave-uniform
 #pragma unroll
   for (int j = 0; j < DB; ++j) {
+    double u[DB];
+#if GPK_POTF2_READLANE
+    // column j, entry (c, j) from lane c (which holds row c), straight into SGPRs: the same values as the
+    // LDS form below without its store -> wait -> load round trip on the pivot chain (D task 33 -> ? us)
+#pragma unroll
+    for (int c = j; c < DB; ++c) u[c] = bcast_lane(w[j], c);
+    (void)colbuf;
+#else
     double* cb = colbuf + (j & 1) * DB;
     if (lane < DB) cb[lane] = w[j];            // column j: entry (r, j) of row r
     // Other lanes' stores are invisible to the per-thread memory model: without a fence hipcc
@@ -87,13 +310,13 @@ __device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double u[DB];
 #pragma unroll
     for (int c = j & ~1; c < DB; c += 2) {
       const dbl2 t = *reinterpret_cast<const dbl2*>(cb + c);
       u[c] = t.x;
       u[c + 1] = t.y;
     }
+#endif
     const double piv = u[j];
     bad = (bad == 0 && !(piv > 0.0)) ? j + 1 : bad;
     const double ri = rsqrt_refined(piv);      // 1 / L[j][j]
@@ -340,6 +563,13 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
   T* Ib = reinterpret_cast<T*>(a.Winv) + (int64_t)b * a.inv_bs + a.kblk * NB * NB;
   typedef double dbl2 __attribute__((ext_vector_type(2)));
   dbl2 pa[FUSE ? NTL : 1][2];  // A operands: chunk kc, pieces lk and lk + 4 (k-steps 0, 1 and 2, 3)
+  // (GPK_DIAG_PROF builds: lane 0 of every wave stamps the shader clock at the phase boundaries of each step --
+  // 0 P_s start, 1 P_s work done, 2 QR_s start, 3 QR_s work done; step 0 / 5: block loaded, step 7 / 4: end)
+  auto stamp = [&](int s, int ph) {
+    if constexpr (GPK_DIAG_PROF != 0) {
+      if (a.prof && lane == 0) a.prof[((a.kblk * NTL + s) * 8 + wave) * 6 + ph] = __builtin_amdgcn_s_memtime();
+    }
+  };
   {
     // the lower 16-tiles of the block, 16 B per load, every load of a thread in flight at once
     constexpr int EPC = 16 / (int)sizeof(T);
@@ -368,6 +598,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
     }
   }
   if (tid == 0) *flag = 0;
+  stamp(0, 5);
   wg_sync<SC1>();
   if (FUSE) {
     // the whole block is in LDS (every load retired into the LDS stores above): draw the ticket
@@ -400,6 +631,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
   d4 xs = {0.0, 0.0, 0.0, 0.0};  // wave 0: X_{s+1} (operand layout) from QR_s, stored in P_{s+1}
   auto step = [&](int s, auto last) {
     // ---------------------------------------------------------------- P_s
+    stamp(s, 0);
     if (decltype(last)::value && wave != 0) prefetch();
     if (wave == 0) {
       if (s > 0) {
@@ -438,8 +670,10 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
         store_inv_diag<T, SC1>(Dinv, Ib, I, tid - 64, DT - 64);
       }
     }
+    stamp(s, 1);
     wg_sync<SC1>();
     // ---------------------------------------------------------------- QR_s
+    stamp(s, 2);
     xs = d4{0.0, 0.0, 0.0, 0.0};  // (the old value is dead: nothing keeps it alive across potf2)
     if (s < NTL - 1 && wave < NTL - 1 - s && !(a.dbg & 4)) {
       const int i = s + 1 + wave;
@@ -466,6 +700,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
         for (int q = 0; q < 4; ++q) A[aidx(i * DB + lr, s * DB + lk + 4 * q)] = xi[q];
       }
     }
+    stamp(s, 3);
     wg_sync<SC1>();
     };
   const int nsteps = (a.dbg & 16) ? 0 : NTL;
@@ -484,6 +719,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
     store_l_rows<T, SC1>(A, Wb, a.ld, NTL - 1, tid, DT);
     if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
   }
+  stamp(NTL - 1, 4);
   if (!FUSE) return;
   wg_sync<SC1>();  // block row 7 of L^-1 in LDS
   if (!live) return;

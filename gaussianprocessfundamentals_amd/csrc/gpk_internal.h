@@ -138,6 +138,7 @@ struct DiagArgs {
   const int64_t* nb;
   const int64_t* mb;
   int32_t* ctr;
+  uint64_t* prof;  // (GPK_DIAG_PROF builds) per step and wave: s_memtime stamps of the phases, else NULL
 };
 
 // persistent factorisation (gpk_potrf.hip chain_kernel): one f64 member, tasks in host-computed order
@@ -162,6 +163,7 @@ struct ChainArgs {
   int32_t* trace;        // debugging (GPK_CHAIN_TRACE=1, else NULL): host-visible [grid][32] progress words
   int32_t dbg;           // debugging (GPK_CHAIN_DBG): 4 = one diagonal task alone (chain_d_only_kernel)
   int32_t force_abort;   // testing (gpk_tune "chain_force_timeout"): the first wait reports a timeout
+  uint64_t* dprof;       // (GPK_DIAG_PROF builds) the D tasks' phase stamps, else NULL
   uint64_t* times;       // profiling (GPK_CHAIN_TIMES=1, else NULL): per task [claimed, inputs ready, wave 0's body done, published, S / U32: loads returned, MFMAs retired] (100 MHz)
 };
 

@@ -930,7 +930,7 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
 // per-lane scratch and every field read becomes a VGPR load -- divergent for the compiler, which then
 // turned the claim loop's exit into an exec-mask-controlled loop whose barriers the waves no longer
 // executed the same number of times (the deadlock of the first versions).
-GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, int dbg, int k,
+GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, int dbg, int k, uint64_t* dprof,
                                     double* sm) {
   DiagArgs da{};
   da.W = W;
@@ -940,7 +940,8 @@ GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, in
   da.kblk = k;
   da.info = info;
   da.version = 2;
-  (void)dbg;
+  da.dbg = dbg;  // (GPK_CHAIN_DBG: diag2_body's timing ablations -- wrong results)
+  da.prof = dprof;
   diag2_body<double, false, true>(da, 0, sm);
 }
 GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
@@ -1068,7 +1069,7 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
     if (ty == CH_D) {
-      chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, sm);
+      chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, a.dprof, sm);
     } else if (ty == CH_S) {
       chain_s(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
               reinterpret_cast<char*>(sm));
@@ -1183,7 +1184,7 @@ hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipSt
 
 __global__ __launch_bounds__(DT) void chain_d_only_kernel(ChainArgs a) {  // (debugging: GPK_CHAIN_DBG=4)
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, 0, sm);
+  chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, 0, a.dprof, sm);
 }
 
 hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {

@@ -95,3 +95,25 @@ for ty in (0, 3):
     us = (Traw[m, 2] - Traw[m, 1]) / 100.0
     ok = (cyc > 0) & (us > 0)
     print("%s body: shader clock %.2f GHz (median over %d tasks)" % (names[ty], np.median(cyc[ok] / us[ok]) / 1e3, ok.sum()), flush=True)
+
+# every step: the hand-off gaps of the chain and how much of each is a late claim (the task's ticket was drawn
+# only after its inputs were published: its workgroup was still busy with an earlier task)
+rows = []
+for k in range(1, len(d) - 1):
+    i_d, i_d1 = d[k], d[k + 1]
+    sl = [i for i in range(nt) if tasks[i, 0] == 1 and tasks[i, 1] == k and tasks[i, 2] // 4 == k + 1]
+    ul = [i for i in range(nt) if tasks[i, 0] == 2 and tasks[i, 1] == k and tasks[i, 2] // 4 == k + 1]
+    if not sl or not ul:
+        continue
+    d_done = T[i_d, 3]
+    s_rdy, s_done = max(T[sl, 1]), max(T[sl, 3])
+    u_rdy, u_done = max(T[ul, 1]), max(T[ul, 3])
+    late_s = max(0.0, max(T[sl, 0]) - d_done)
+    late_u = max(0.0, max(T[ul, 0]) - s_done)
+    late_d = max(0.0, T[i_d1, 0] - u_done)
+    rows.append((T[i_d, 3] - T[i_d, 1], s_rdy - d_done, late_s, s_done - s_rdy, u_rdy - s_done, late_u,
+                 u_done - u_rdy, T[i_d1, 1] - u_done, late_d, T[i_d1, 1] - T[i_d, 1]))
+if rows:
+    r = np.array(rows).mean(axis=0)
+    print("mean over %d steps: D %.1f | ->S %.1f (late claim %.1f) | S %.1f | ->U %.1f (late %.1f) | U %.1f | "
+          "->D %.1f (late %.1f) | step %.1f us" % ((len(rows),) + tuple(r)), flush=True)

@@ -1,0 +1,6 @@
+# potf2 pivot column through v_readlane instead of LDS: correctness, then spans and per-task profile
+set -o pipefail
+O=gpurun_out/r4h; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_chain.py tests/test_gpu_parity.py tests/test_gpu_diag_versions.py -m gpu > $O/tests.log 2>&1 || { echo "tests failed" >> $O/tests.log; exit 1; }
+SETS='{"chain":1};{"chain":0,"lookahead":2}' timeout -k 10 300 python tools/single_sched.py 1024 2048 4096 8192 > $O/ab.jsonl 2>&1 || exit 1
+timeout -k 10 120 python tools/chain_prof.py 4096 > $O/prof.txt 2>&1 || exit 1
