@@ -43,6 +43,12 @@ if "GRBM_GUI_ACTIVE" in avg:
         per_simd = avg["SQ_INSTS_VALU"] / 1024
         cyc = avg["GRBM_GUI_ACTIVE"] / 8
         print("  VALU wave-instructions per SIMD per cycle %.3f (f64 VALU: 4 cycles each -> at most 0.25)" % (per_simd / cyc))
+    if "SQ_ACTIVE_INST_VALU" in avg:
+        # SQ_ACTIVE_INST_VALU counts quad-cycles (one per wave64 VALU instruction issued: 3.26e8 against
+        # SQ_INSTS_VALU 3.22e8 on C5); VALU busy = its cycles over the SIMD-cycles of the dispatch (256 CUs x 4 SIMDs)
+        busy = avg["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * avg["GRBM_GUI_ACTIVE"] / 8)
+        print("  VALU busy %.1f %% of the SIMD cycles (SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x cycles)): the kernel's "
+              "roofline is the VALU issue rate" % (100 * busy))
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     hbm = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
     print("  HBM bytes (2 FETCH + WRITE) %.4g vs algorithmic %.4g (%.2fx); %.0f GB/s = %.1f %% of 8 TB/s" % (
