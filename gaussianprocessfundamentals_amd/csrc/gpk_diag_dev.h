@@ -733,11 +733,12 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
       if (!(a.dbg & 2)) potf2_tile(A, Dinv + s * DTS, colbuf, s, lane, flag, a.j0);  // timing ablation
       if (decltype(last)::value) prefetch();
     } else if (s == 0) {
-      if (!(a.dbg & 8) && wr) store_inv_zeros<T, SC1>(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
+      if (!(a.dbg & 8) && wr && !a.no_inv_zeros) store_inv_zeros<T, SC1>(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
     } else {
       const int w = wave - 1;
       const int I = s - 1;
       if (w < I && !(a.dbg & 1)) inverse_tile<T, SC1>(A, Dinv, Ib, I, w, lr, lk, wr);
+      if (s < NTL - 1) stamp(s, 5);  // (profiling: inverse tile done)
       // trailing update of step s - 1 for tile columns j >= s + 1 (column s was done in QR_{s-1});
       // the last waves take the first tiles (waves 1..I hold an inverse tile)
       const int m = NTL - 1 - s;
@@ -757,6 +758,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
 #pragma unroll
         for (int q = 0; q < 4; ++q) A[aidx(i * DB + lk + 4 * q, j * DB + lr)] = acc[q];
       }
+      if (s < NTL - 1) stamp(s, 4);  // (profiling: trailing tiles done)
       if (!(a.dbg & 8) && wr) {
         store_l_rows<T, SC1>(A, Wb, a.ld, I, tid - 64, DT - 64);
         store_inv_diag<T, SC1>(Dinv, Ib, I, tid - 64, DT - 64);

@@ -139,6 +139,8 @@ struct DiagArgs {
   const int64_t* mb;
   int32_t* ctr;
   uint64_t* prof;  // (GPK_DIAG_PROF builds) per step and wave: s_memtime stamps of the phases, else NULL
+  int32_t no_inv_zeros;  // 1: leave the tiles of Winv above the diagonal tiles unwritten (the persistent
+                         // factorisation's panel solves never read them; the launch path's TRSM does)
 };
 
 // persistent factorisation (gpk_potrf.hip chain_kernel): one f64 member, tasks in host-computed order

@@ -653,6 +653,9 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 // plain loads behind one agent acquire per task.  Every wait is bounded: on timeout
 // the task sets ctl[1] and info = -1 and every workgroup drains the list without work.
 enum { CH_D = 0, CH_S = 1, CH_U32 = 2, CH_BLK = 3 };
+#ifndef GPK_CHAIN_SPREF
+#define GPK_CHAIN_SPREF 0  // 1: S stages its slice before waiting for D (0: one wait for both inputs)
+#endif
 constexpr int CHAIN_SLOT_OFF = (int)((DIAG_LDS_BYTES + 15) / 16 * 16);
 constexpr size_t CHAIN_LDS_BYTES = CHAIN_SLOT_OFF + 16;
 
@@ -696,7 +699,18 @@ __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p,
 // acquire, sc1 stores.  (The first form -- 2 x 4 waves of 16 x 32, A and B loaded per wave from HBM / L2 --
 // moved 384 KB per task: 16 us against 11-12 us for the same work with the zero pieces skipped.)
 constexpr int SLAB_LDS_ROW = 1040;
-template <bool SUB>
+// A rows 4 w .. 4 w + 3 into LDS, one 1-KB row per instruction (the slab's first operand)
+__device__ __forceinline__ void slab_stage_a(const double* A, int64_t ld, char* smem) {
+  const int tid = opaque_tid();
+  const int lane = tid & 63;
+  const int w = wave_uniform(tid >> 6);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 4 * w + i;
+    glds16a<kLdAux>(A + (int64_t)row * ld + 2 * lane, smem + row * SLAB_LDS_ROW);
+  }
+}
+template <bool SUB, bool STAGED = false>
 __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int64_t ldb, double* C, int64_t ld,
                                           int diag_off, uint64_t* st, char* smem) {
   typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -709,12 +723,8 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
   const int cb = w < 4 ? w : 11 - w;
   // live row blocks of this wave's column block (U32 on the diagonal block: columns <= the rows' block)
   const bool live0 = diag_off < 0 || cb <= (diag_off >> 4), live1 = diag_off < 0 || cb <= (diag_off >> 4) + 1;
-  // A rows 4 w .. 4 w + 3 into LDS, one 1-KB row per instruction
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = 4 * w + i;
-    glds16a<kLdAux>(A + (int64_t)row * ld + 2 * lane, smem + row * SLAB_LDS_ROW);
-  }
+  // (STAGED: the caller issued them already -- the panel solve prefetches its slice before L^-1 is ready)
+  if (!STAGED) slab_stage_a(A, ld, smem);
   const __amdgpu_buffer_rsrc_t brs = uniform_rsrc(B), crs = uniform_rsrc(C);
   const int bvo = (int)(((int64_t)(cb * 16 + lr) * ldb + 2 * q) * 8);
   const int cvo = (int)(((int64_t)q * ld + cb * 16 + lr) * 8);  // C/D layout: row q + 4 i, column lr
@@ -942,11 +952,19 @@ GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, in
   da.version = 2;
   da.dbg = dbg;  // (GPK_CHAIN_DBG: diag2_body's timing ablations -- wrong results)
   da.prof = dprof;
+  da.no_inv_zeros = 1;  // (S reads only the lower 16-tiles of L^-1: slab_gemm's skipped pieces; gpk_trsv likewise)
   diag2_body<double, false, true>(da, 0, sm);
 }
 GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
   double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
   slab_gemm<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem);
+}
+GPK_CHAIN_FN void chain_s_staged(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
+  double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
+  slab_gemm<false, true>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem);
+}
+GPK_CHAIN_FN void chain_s_stage(double* W, int64_t ld, int k, int r, char* smem) {
+  slab_stage_a(W + (int64_t)r * 32 * ld + (int64_t)k * NB, ld, smem);
 }
 GPK_CHAIN_FN void chain_uq(double* W, int64_t ld, int k, int r, int j, int qq, uint64_t* st, char* smem) {
   const int64_t R = (int64_t)r * 32;
@@ -1051,9 +1069,15 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
     const int r = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 2]);
     const int j = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 3]);
+    // S (GPK_CHAIN_SPREF): its slice of the panel is final once the slice's last update is published, before
+    // L_kk^-1 is: wait for that first, start the slice's LDS-DMA, then wait for D(k) -- the slice's load leaves
+    // the critical chain D(k) -> S
+    const bool spref = GPK_CHAIN_SPREF && ty == CH_S;
     if (wave == 0) {
       if (a.times) a.times[6 * t] = __builtin_amdgcn_s_memrealtime();
-      const bool ok = chain_deps(a, ty, k, r, j, g, co);
+      const bool ok = spref ? (k == 0 || chain_wait(a, a.ucnt + co + (int64_t)r * a.nbc + k, k,
+                                                    __builtin_amdgcn_s_memrealtime()))
+                            : chain_deps(a, ty, k, r, j, g, co);
       if (a.times) {
         a.times[6 * t + 1] = __builtin_amdgcn_s_memrealtime();
         if (ty == CH_D || ty == CH_BLK) a.times[6 * t + 4] = __builtin_amdgcn_s_memtime();  // shader clock
@@ -1068,8 +1092,28 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     }
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
+    if (spref) {
+      chain_s_stage(Wm, a.ld, k, r, reinterpret_cast<char*>(sm));
+      if (wave == 0) {
+        const bool ok = chain_wait(a, a.dflag + co + k, 1, __builtin_amdgcn_s_memrealtime());
+        if (a.times) a.times[6 * t + 1] = __builtin_amdgcn_s_memrealtime();
+        if (ok && !kChainSc1Ld) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        slot[1] = ok ? 1 : 0;
+      }
+      __syncthreads();
+      if (!__builtin_amdgcn_readfirstlane(slot[1])) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the staged slice lands before anything else)
+        continue;
+      }
+    }
     if (ty == CH_D) {
       chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, a.dprof, sm);
+    } else if (spref) {
+      chain_s_staged(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
+                     reinterpret_cast<char*>(sm));
     } else if (ty == CH_S) {
       chain_s(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
               reinterpret_cast<char*>(sm));

@@ -54,3 +54,10 @@ for s in range(8):
     step = np.mean([(P[k, s + 1, 0, 0] if s < 7 else P[k, 7, 0, 4]) - P[k, s, 0, 0] for k in ks])
     print("s %d step %5.0f | P work w0 %5.0f  w1-7 %s | P bar w0 %4.0f | QR work %s | QR bar+ w0 %4.0f" % (
         s, step, pw[0], " ".join("%4.0f" % v for v in pw[1:]), pb[0], " ".join("%4.0f" % v for v in qw), qb[0]))
+print("waves 1-7, P work split (cycles, steps 1..6): inverse tile | trailing tiles | HBM stores of L / L^-1 rows")
+for s in range(1, 7):
+    inv = np.mean([P[k, s, 1:, 5] - P[k, s, 1:, 0] for k in ks], axis=0)
+    trl = np.mean([P[k, s, 1:, 4] - P[k, s, 1:, 5] for k in ks], axis=0)
+    sto = np.mean([P[k, s, 1:, 1] - P[k, s, 1:, 4] for k in ks], axis=0)
+    print("s %d inv %s | trail %s | store %s" % (s, " ".join("%4.0f" % v for v in inv), " ".join("%4.0f" % v for v in trl),
+                                                " ".join("%4.0f" % v for v in sto)))
