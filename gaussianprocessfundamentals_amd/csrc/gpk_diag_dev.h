@@ -60,9 +60,6 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
 #define GPK_POTF2_MODE 2  // pivot column broadcast: 2 DPP row_newbcast, 1 v_readlane, 0 LDS (rounds 1-4; A/B builds)
 #endif
 #define GPK_POTF2_READLANE (GPK_POTF2_MODE == 1)
-#ifndef GPK_POTF2_PACK
-#define GPK_POTF2_PACK 0  // mode 2: factor rows and inverse columns in the two halves of the wave (PkStep)
-#endif
 #ifndef GPK_POTF2_PIPE
 #define GPK_POTF2_PIPE 1  // mode 2: the software-pipelined issue order (potf2_pipelined)
 #endif
@@ -239,68 +236,6 @@ __device__ __forceinline__ void potf2_pipelined(double* w, double* v, int& bad) 
   PipeStep<0>::run(w, v, bad, 0.0, 0.0, 0.0, 1.5);
 }
 
-// Packed form (GPK_POTF2_PACK): lanes 0..31 hold the tile rows, lanes 32..63 the identity columns, in the SAME
-// registers R[16] -- one FMA per entry serves the factor and the inverse (half of the unpacked form's FMAs).  The
-// broadcast source of pivot J is its column copied into the upper half (v_permlane32_swap: lanes 32..63 of the
-// first operand <- lanes 0..31 of the second), so both halves see the factor column; the per-lane multiplier
-// -a / L[J][J] is the factor's in the lower half and the inverse's in the upper half -- the same values as above.
-__device__ __forceinline__ double up_copy(double u) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, u);
-  uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32), lo2 = lo, hi2 = hi;
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %2, %3"
-               : "+v"(lo), "+v"(lo2), "+v"(hi), "+v"(hi2));
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-template <int J, int D>
-struct PkDeferOp {  // deferred FMA number D of pivot J - 1 (issued during pivot J): entry J + 1 + D
-  static __device__ __forceinline__ void run(double* R, double xp, double ngp) {
-    constexpr int C = J + 1 + D;
-    if constexpr (J > 0 && C < DB) fmac_bcast_v<C>(R[C], xp, ngp);
-  }
-};
-template <int J, int D0, int D1>
-struct PkDefer {
-  static __device__ __forceinline__ void run(double* R, double xp, double ngp) {
-    if constexpr (D0 < D1 && D0 < DB) {
-      PkDeferOp<J, D0>::run(R, xp, ngp);
-      PkDefer<J, D0 + 1, D1>::run(R, xp, ngp);
-    }
-  }
-};
-template <int J>
-struct PkStep {
-  static __device__ __forceinline__ void run(double* R, int& bad, double xp, double ngp, double c15) {
-    if constexpr (J < DB) {
-      const double u = R[J];
-      const double x = up_copy(u);
-      const double piv = bcast_v<J>(x);
-      bad = (bad == 0 && !(piv > 0.0)) ? J + 1 : bad;
-      const double r0 = vrsq(piv);
-      const double hn = vmul_mhalf(piv);
-      PkDefer<J, 0, 3>::run(R, xp, ngp);
-      double t = vmul(hn, r0);
-      PkDefer<J, 3, 4>::run(R, xp, ngp);
-      t = vfma(t, r0, c15);
-      PkDefer<J, 4, 5>::run(R, xp, ngp);
-      double ri = vmul(r0, t);
-      if constexpr (GPK_RSQ_NEWTON >= 2) {
-        PkDefer<J, 5, 6>::run(R, xp, ngp);
-        t = vmul(hn, ri);
-        PkDefer<J, 6, 7>::run(R, xp, ngp);
-        t = vfma(t, ri, c15);
-        PkDefer<J, 7, 8>::run(R, xp, ngp);
-        ri = vmul(ri, t);  // 1 / L[J][J]
-      }
-      const double a = vmul(u, ri);
-      const double ng = vmul_neg(a, ri);
-      if constexpr (J + 1 < DB) fmac_bcast_v<J + 1>(R[J + 1], x, ng);  // the next pivot's input
-      PkDefer<J, (GPK_RSQ_NEWTON >= 2 ? 8 : 5), DB>::run(R, xp, ngp);  // the rest of the previous pivot's FMAs
-      R[J] = a;
-      PkStep<J + 1>::run(R, bad, x, ng, c15);
-    }
-  }
-};
-
 // potf2 + inverse of tile (kb, kb), one wave.  Lanes 0..15 hold row r = lane of the tile and
 // factor it (right-looking); lanes 16..31 hold column r = lane - 16 of the identity and turn it
 // into column r of L^-1 (column-oriented forward substitution).  Both run the SAME update per
@@ -315,33 +250,6 @@ __device__ __forceinline__ void potf2_tile(double* A, double* Dk, double* colbuf
   const int r = lane & 15;
   const bool inv = (lane & 16) != 0;
   const int c0 = kb * DB;
-#if GPK_POTF2_MODE == 2 && GPK_POTF2_PACK
-  {
-    (void)inv;
-    (void)colbuf;
-    const bool upper = lane >= 32;
-    double R[DB];
-#pragma unroll
-    for (int c = 0; c < DB; c += 2) {
-      const dbl2 t = *reinterpret_cast<const dbl2*>(A + aidx(c0 + r, c0 + c));
-      R[c] = upper ? ((c == r) ? 1.0 : 0.0) : t.x;
-      R[c + 1] = upper ? ((c + 1 == r) ? 1.0 : 0.0) : t.y;
-    }
-    int bad = 0;
-    PkStep<0>::run(R, bad, 0.0, 0.0, 1.5);
-#pragma unroll
-    for (int c = 0; c < DB; ++c) asm volatile("" : "+v"(R[c]));  // (computed here, every lane active)
-    if (bad != 0 && lane == 0 && *flag == 0) *flag = (int)(col_base + c0 + bad);
-    if (lane < DB) {
-#pragma unroll
-      for (int c = 0; c < DB; ++c) A[aidx(c0 + r, c0 + c)] = (c <= r) ? R[c] : 0.0;
-    } else if (lane >= 32 && lane < 32 + DB) {
-#pragma unroll
-      for (int rr = 0; rr < DB; ++rr) Dk[rr * DBS + r] = R[rr];  // Dinv[rr][r]
-    }
-    return;
-  }
-#endif
 #if GPK_POTF2_MODE == 2
   {
     (void)inv;
@@ -743,11 +651,17 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
       // the last waves take the first tiles (waves 1..I hold an inverse tile)
       const int m = NTL - 1 - s;
       const int ntri = m * (m + 1) / 2;
-      for (int t = (NTL - 2) - w; t < ((a.dbg & 4) ? 0 : ntri); t += NTL - 1) {
+      int t = (NTL - 2) - w;
+      const int nt_all = (a.dbg & 4) ? 0 : ntri;
+      auto tile_of = [&](int tt, int& i, int& j) {
         int ti = 0;
-        while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-        const int tj = t - ti * (ti + 1) / 2;
-        const int i = s + 1 + ti, j = s + 1 + tj;
+        while ((ti + 1) * (ti + 2) / 2 <= tt) ++ti;
+        i = s + 1 + ti;
+        j = s + 1 + tt - ti * (ti + 1) / 2;
+      };
+      for (; t < nt_all; t += NTL - 1) {
+        int i, j;
+        tile_of(t, i, j);
         d4 acc;
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[q] = A[aidx(i * DB + lk + 4 * q, j * DB + lr)];

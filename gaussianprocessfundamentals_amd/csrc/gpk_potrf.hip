@@ -654,7 +654,7 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 // the task sets ctl[1] and info = -1 and every workgroup drains the list without work.
 enum { CH_D = 0, CH_S = 1, CH_U32 = 2, CH_BLK = 3 };
 #ifndef GPK_CHAIN_SPREF
-#define GPK_CHAIN_SPREF 0  // 1: S stages its slice before waiting for D (0: one wait for both inputs)
+#define GPK_CHAIN_SPREF 1  // S stages its slice before waiting for D (0: one wait for both inputs)
 #endif
 constexpr int CHAIN_SLOT_OFF = (int)((DIAG_LDS_BYTES + 15) / 16 * 16);
 constexpr size_t CHAIN_LDS_BYTES = CHAIN_SLOT_OFF + 16;

@@ -90,6 +90,28 @@ __global__ void probe(double* out, double seed, unsigned long long* cyc) {
                     : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7) : "v"(c) : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47");)
   t1 = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) cyc[11] = t1 - t0;
+  // 13 dependent f64 MFMA 16x16x4 (accumulator chain), 14 independent (4 accumulators)
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  d4 m0 = {a, a, a, a}, m1 = m0, m2 = m0, m3 = m0;
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < 64; ++i) m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, c, m0, 0, 0, 0);
+  asm volatile("s_nop 7" ::: "memory");
+  const double dep = m0[0];
+  asm volatile("" ::"v"(dep));
+  t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) cyc[12] = t1 - t0;
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < 16; ++i) {
+    m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, c, m0, 0, 0, 0);
+    m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, c, m1, 0, 0, 0);
+    m2 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, c, m2, 0, 0, 0);
+    m3 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, c, m3, 0, 0, 0);
+  }
+  const double dep2 = m0[0] + m1[1] + m2[2] + m3[3];
+  asm volatile("" ::"v"(dep2));
+  t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) cyc[13] = t1 - t0;
+  a += dep + dep2;
   // 8 s_memtime back to back
   t0 = __builtin_amdgcn_s_memtime();
   t1 = __builtin_amdgcn_s_memtime();
@@ -105,13 +127,15 @@ int main() {
   unsigned long long h[16];
   for (int it = 0; it < 3; ++it) {
     hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, out, 1.5, cyc);
-    (void)hipMemcpy(h, cyc, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(h, cyc, 14 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
   }
   const char* nm[8] = {"fma f64 dep", "mul f64 dep", "rsq f64 dep", "dpp64 mov dep (+s_nop 1)", "readlane + add_u32 dep",
                        "lds write+read dep", "fma f64 indep (64 instr)", "memtime overhead"};
   for (int i = 0; i < 7; ++i) printf("%-28s %6.1f cycles per step\n", nm[i], (double)h[i] / 64.0);
   const char* nm2[4] = {"fmac dpp64 indep (+s_nop 1)", "fmac dpp64 indep", "readlane indep", "fma f64 sgpr indep"};
   for (int i = 0; i < 4; ++i) printf("%-28s %6.1f cycles per instr\n", nm2[i], (double)h[8 + i] / 64.0);
+  printf("%-28s %6.1f cycles per instr\n", "mfma f64 16x16x4 dep", (double)h[12] / 64.0);
+  printf("%-28s %6.1f cycles per instr\n", "mfma f64 16x16x4 indep", (double)h[13] / 64.0);
   printf("%-28s %6llu cycles\n", nm[7], h[7]);
   return 0;
 }
