@@ -4,7 +4,7 @@
 set -u
 tag=${1:-fin}
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
     > gpurun_out/${tag}_tests.log 2>&1 || { tail -5 gpurun_out/${tag}_tests.log; exit 1; }
 tail -1 gpurun_out/${tag}_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { tail -5 gpurun_out/${tag}_smoke.log; exit 1; }
