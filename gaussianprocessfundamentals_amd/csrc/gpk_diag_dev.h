@@ -674,7 +674,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
       }
       if (s < NTL - 1) stamp(s, 4);  // (profiling: trailing tiles done)
       if (!(a.dbg & 8) && wr) {
-        store_l_rows<T, SC1>(A, Wb, a.ld, I, tid - 64, DT - 64);
+        if (!a.defer_l_store) store_l_rows<T, SC1>(A, Wb, a.ld, I, tid - 64, DT - 64);
         store_inv_diag<T, SC1>(Dinv, Ib, I, tid - 64, DT - 64);
       }
     }
@@ -724,7 +724,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
     store_inv_diag<T, SC1>(Dinv, Ib, NTL - 1, lane, 64);
   }
   if (wr) {
-    store_l_rows<T, SC1>(A, Wb, a.ld, NTL - 1, tid, DT);
+    if (!a.defer_l_store) store_l_rows<T, SC1>(A, Wb, a.ld, NTL - 1, tid, DT);
     if (tid == 0 && *flag != 0) atomicCAS(&a.info[b], 0, *flag);
   }
   stamp(NTL - 1, 4);

@@ -139,6 +139,8 @@ struct DiagArgs {
   const int64_t* mb;
   int32_t* ctr;
   uint64_t* prof;  // (GPK_DIAG_PROF builds) per step and wave: s_memtime stamps of the phases, else NULL
+  int32_t defer_l_store;  // 1: L_kk stays in LDS only (the persistent factorisation stores it after publishing:
+                          // no task of the launch reads it)
   int32_t no_inv_zeros;  // 1: leave the tiles of Winv above the diagonal tiles unwritten (the persistent
                          // factorisation's panel solves never read them; the launch path's TRSM does)
 };

@@ -653,6 +653,9 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 // plain loads behind one agent acquire per task.  Every wait is bounded: on timeout
 // the task sets ctl[1] and info = -1 and every workgroup drains the list without work.
 enum { CH_D = 0, CH_S = 1, CH_U32 = 2, CH_BLK = 3 };
+#ifndef GPK_CHAIN_DEFER_L
+#define GPK_CHAIN_DEFER_L 1  // D publishes L_kk^-1 first and stores L_kk (read by no task of the launch) afterwards
+#endif
 #ifndef GPK_CHAIN_SPREF
 #define GPK_CHAIN_SPREF 1  // S stages its slice before waiting for D (0: one wait for both inputs)
 #endif
@@ -953,6 +956,7 @@ GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, in
   da.dbg = dbg;  // (GPK_CHAIN_DBG: diag2_body's timing ablations -- wrong results)
   da.prof = dprof;
   da.no_inv_zeros = 1;  // (S reads only the lower 16-tiles of L^-1: slab_gemm's skipped pieces; gpk_trsv likewise)
+  da.defer_l_store = GPK_CHAIN_DEFER_L;
   diag2_body<double, false, true>(da, 0, sm);
 }
 GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
@@ -1149,6 +1153,15 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       } else {
         for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl; ++s) st_flag(a.ucnt + co + (int64_t)s * a.nbc + j, k + g);
       }
+    }
+    if (GPK_CHAIN_DEFER_L && ty == CH_D) {
+      // L_kk from LDS (the block's lower tiles; L^-1 sits in the upper ones) to W, after the hand-off: only the
+      // read-out after the launch uses it.  (The next claim's barrier keeps the LDS intact until every wave has
+      // read its rows.)
+      double* Wb = Wm + (int64_t)k * NB * a.ld + (int64_t)k * NB;
+      const int tid = opaque_tid();
+#pragma unroll 1
+      for (int I = 0; I < NTL; ++I) store_l_rows<double, true>(sm, Wb, a.ld, I, tid, DT);
     }
   }
   if (wave == 0) chain_trace(a, 1, 9);
