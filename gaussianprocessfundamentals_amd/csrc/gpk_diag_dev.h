@@ -60,6 +60,15 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
 #define GPK_POTF2_MODE 2  // pivot column broadcast: 2 DPP row_newbcast, 1 v_readlane, 0 LDS (rounds 1-4; A/B builds)
 #endif
 #define GPK_POTF2_READLANE (GPK_POTF2_MODE == 1)
+#ifndef GPK_PIPE_NEWTON
+#define GPK_PIPE_NEWTON 1  // Newton steps after v_rsq_f64 in the pipelined potf2 (2: rounds 1-4)
+#endif
+#ifndef GPK_PIPE_NOINV
+#define GPK_PIPE_NOINV 0  // (timing probes only: the inverse half's FMAs left out -- wrong L^-1)
+#endif
+#ifndef GPK_PIPE_NOBAD
+#define GPK_PIPE_NOBAD 0  // (timing probes only: no non-positive pivot bookkeeping)
+#endif
 #ifndef GPK_POTF2_PIPE
 #define GPK_POTF2_PIPE 1  // mode 2: the software-pipelined issue order (potf2_pipelined)
 #endif
@@ -171,7 +180,7 @@ template <int J, int D>
 struct DeferOp {
   static __device__ __forceinline__ void run(double* w, double* v, double up, double ngw, double ngv) {
     constexpr int ND = (J == 0) ? 0 : 1 + 2 * (DB - 1 - J);
-    if constexpr (D < ND) {
+    if constexpr (D < ND && !(GPK_PIPE_NOINV && (D == 0 || ((D - 1) & 1) != 0))) {  // (NOINV: probe builds only)
       // (entry c takes column entry (c, J - 1), i.e. lane c's u)
       if constexpr (D == 0) {
         fmac_bcast_v<J>(v[J], up, ngv);
@@ -201,7 +210,7 @@ struct PipeStep {
     if constexpr (J < DB) {
       const double u = w[J];
       const double piv = bcast_v<J>(u);
-      bad = (bad == 0 && !(piv > 0.0)) ? J + 1 : bad;
+      if (!GPK_PIPE_NOBAD) bad = (bad == 0 && !(piv > 0.0)) ? J + 1 : bad;
       const double r0 = vrsq(piv);
       const double hn = vmul_mhalf(piv);
       DeferRange<J, 0, 3>::run(w, v, up, ngwp, ngvp);
@@ -211,16 +220,19 @@ struct PipeStep {
       DeferRange<J, 4, 5>::run(w, v, up, ngwp, ngvp);
       const double r1 = vmul(r0, t);
       DeferRange<J, 5, 6>::run(w, v, up, ngwp, ngvp);
-      t = vmul(hn, r1);
-      DeferRange<J, 6, 7>::run(w, v, up, ngwp, ngvp);
-      t = vfma(t, r1, c15);
-      DeferRange<J, 7, 8>::run(w, v, up, ngwp, ngvp);
-      const double ri = vmul(r1, t);  // 1 / L[J][J]
-      DeferRange<J, 8, 9>::run(w, v, up, ngwp, ngvp);
+      double ri = r1;
+      if constexpr (GPK_PIPE_NEWTON >= 2) {
+        t = vmul(hn, r1);
+        DeferRange<J, 6, 7>::run(w, v, up, ngwp, ngvp);
+        t = vfma(t, r1, c15);
+        DeferRange<J, 7, 8>::run(w, v, up, ngwp, ngvp);
+        ri = vmul(r1, t);  // 1 / L[J][J]
+        DeferRange<J, 8, 9>::run(w, v, up, ngwp, ngvp);
+      }
       const double aw = vmul(u, ri), av = vmul(v[J], ri);
       const double ngw = vmul_neg(aw, ri), ngv = vmul_neg(av, ri);
       if constexpr (J + 1 < DB) fmac_bcast_v<J + 1>(w[J + 1], u, ngw);  // the next pivot's input
-      DeferRange<J, 9, 2 * DB>::run(w, v, up, ngwp, ngvp);       // the rest of the previous pivot's FMAs
+      DeferRange<J, (GPK_PIPE_NEWTON >= 2 ? 9 : 6), 2 * DB>::run(w, v, up, ngwp, ngvp);  // the rest of the previous pivot's FMAs
       w[J] = aw;
       v[J] = av;
       PipeStep<J + 1>::run(w, v, bad, u, ngw, ngv, c15);
