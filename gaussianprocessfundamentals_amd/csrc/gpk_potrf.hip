@@ -689,6 +689,34 @@ __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p,
   return true;
 }
 
+// wave 0: wait until *p[i] >= v[i] for every i -- the N counters polled together (all loads in flight at once,
+// one round trip per poll: a task's inputs are usually all published by the time it looks, and polling them one
+// after another cost a cross-XCD round trip each); false on timeout (reported) or after another task's timeout
+template <int N>
+__device__ __forceinline__ bool chain_wait_set(const ChainArgs& a, const int32_t* const (&p)[N], const int32_t (&v)[N],
+                                               uint64_t t0) {
+  for (;;) {
+    int32_t x[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = ld_flag(p[i]);
+    bool all = !a.force_abort;
+#pragma unroll
+    for (int i = 0; i < N; ++i) all = all && __builtin_amdgcn_readfirstlane(x[i]) >= v[i];
+    if (all) return true;
+    if (__builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) return false;
+    if (a.force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout) {
+      st_flag(a.ctl + 1, 1);
+      for (int m = 0; m < a.nmem; ++m) {
+        int32_t zero = 0;
+        __hip_atomic_compare_exchange_strong((gi32*)(a.info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // C[32 x 128] = A[32 x 128] B^T (SUB false) or C -= A B^T (SUB true), B [128 x 128]; A, C with row
 // stride ld, B with ldb.  These tasks are bound by the bytes one CU pulls from the Infinity Cache, so every
 // operand byte is fetched once: A (32 rows, 32 KB) is staged into LDS by LDS-DMA (row stride 1040 B: the
@@ -1013,41 +1041,66 @@ __device__ __forceinline__ int claim_ticket(int32_t* p) {
 // published; false on timeout (reported) or after another task's timeout.
 __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, int r, int j, int g, int64_t co) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  bool ok = true;
   const int32_t* dflag = a.dflag + co;
   const int32_t* sdone = a.sdone + co;
   const int32_t* ucnt = a.ucnt + co;
+  // (slots a task does not need keep the first pointer with value 0: always met, loaded in the same batch)
   if (ty == CH_D) {
-    if (k > 0 && a.uq) {
-      // every quarter update of panel k - 1 on the block's slices (slice s has s - 4 k + 1 of them)
-      const int32_t* qd = a.qdone + co + (int64_t)(k - 1) * a.nsl;
-      for (int s = 4 * k; s <= 4 * k + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, qd + s, s - 4 * k + 1, t0);
-    } else if (k > 0) {
-      for (int s = 4 * k; s <= 4 * k + 3 && ok; ++s) ok = chain_wait(a, ucnt + (int64_t)s * a.nbc + k, k, t0);
+    if (k == 0) return true;
+    const int32_t* p[4];
+    int32_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = 4 * k + i;
+      if (a.uq) {
+        // every quarter update of panel k - 1 on the block's slices (slice s has s - 4 k + 1 of them)
+        p[i] = a.qdone + co + (int64_t)(k - 1) * a.nsl + (s < a.nsl ? s : 4 * k);
+        v[i] = s < a.nsl ? i + 1 : 0;
+      } else {
+        p[i] = ucnt + (int64_t)s * a.nbc + k;
+        v[i] = k;
+      }
     }
+    return chain_wait_set<4>(a, p, v, t0);
   } else if (ty == CH_S) {
-    ok = chain_wait(a, dflag + k, 1, t0);
-    if (ok && k > 0) ok = chain_wait(a, ucnt + (int64_t)r * a.nbc + k, k, t0);
+    const int32_t* p[2] = {dflag + k, ucnt + (int64_t)r * a.nbc + k};
+    const int32_t v[2] = {1, k > 0 ? k : 0};
+    return chain_wait_set<2>(a, p, v, t0);
   } else if (ty == CH_U32) {
     const int32_t* sd = sdone + (int64_t)k * a.nsl;
-    ok = chain_wait(a, sd + r, 1, t0);
-    if (g > 1) {  // UQ, quarter g - 2: slice 4 j + quarter of the panel
-      if (ok) ok = chain_wait(a, sd + 4 * j + (g - 2), 1, t0);
-    } else {
-      for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
+    const int32_t* p[6];
+    int32_t v[6];
+    p[0] = sd + r;
+    v[0] = 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = 4 * j + i;
+      // g > 1: UQ, quarter g - 2 -- slice 4 j + quarter of the panel only
+      const bool need = g > 1 ? (i == g - 2) : (s < a.nsl);
+      p[1 + i] = need ? sd + s : sd + r;
+      v[1 + i] = need ? 1 : 0;
     }
-    if (ok && k > 0) ok = chain_wait(a, ucnt + (int64_t)r * a.nbc + j, k, t0);
-  } else {
-    // BLK over the g panels k .. k + g - 1: the last panel's solves of both blocks' slices (S(q, r) done
-    // implies S(q', r) done for q' < q: S(q, r) waited for the update of panel q - 1, which waited for
-    // S(q - 1, r)), and the tile's previous update
-    const int32_t* sd = sdone + (int64_t)(k + g - 1) * a.nsl;
-    for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
-    for (int s = 4 * j; s <= 4 * j + 3 && s < a.nsl && ok; ++s) ok = chain_wait(a, sd + s, 1, t0);
-    for (int s = 4 * r; s <= 4 * r + 3 && s < a.nsl && ok && k > 0; ++s)
-      ok = chain_wait(a, ucnt + (int64_t)s * a.nbc + j, k, t0);
+    p[5] = ucnt + (int64_t)r * a.nbc + j;
+    v[5] = k > 0 ? k : 0;
+    return chain_wait_set<6>(a, p, v, t0);
   }
-  return ok;
+  // BLK over the g panels k .. k + g - 1: the last panel's solves of both blocks' slices (S(q, r) done implies
+  // S(q', r) done for q' < q: S(q, r) waited for the update of panel q - 1, which waited for S(q - 1, r)), and the
+  // tile's previous update
+  const int32_t* sd = sdone + (int64_t)(k + g - 1) * a.nsl;
+  const int32_t* p[12];
+  int32_t v[12];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int sr = 4 * r + i, sj = 4 * j + i;
+    p[i] = sd + (sr < a.nsl ? sr : 4 * r);
+    v[i] = sr < a.nsl ? 1 : 0;
+    p[4 + i] = sd + (sj < a.nsl ? sj : 4 * j);
+    v[4 + i] = sj < a.nsl ? 1 : 0;
+    p[8 + i] = ucnt + (int64_t)(sr < a.nsl ? sr : 4 * r) * a.nbc + j;
+    v[8 + i] = (sr < a.nsl && k > 0) ? k : 0;
+  }
+  return chain_wait_set<12>(a, p, v, t0);
 }
 
 __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
