@@ -425,7 +425,7 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   // (profiles/r03p_chain_task_profile_n4096.txt); GPK_CHAIN_DUR="d,s,u,b" overrides them (A/B).  A tile
   // update over g panels is estimated at b (0.25 + 0.75 g): the C read / write and the pipeline fill are
   // paid once per task.
-  float dur[4] = {32.f, 7.f, 10.f, 24.f};
+  float dur[4] = {28.f, 6.5f, 12.f, 22.5f};  // round 4: measured D, S, U32 (UQ: half), BLK g = 1 (profiles/r04y_*)
   if (const char* e = getenv("GPK_CHAIN_DUR")) sscanf(e, "%f,%f,%f,%f", &dur[0], &dur[1], &dur[2], &dur[3]);
   // Deferred tile updates: the panels of group [q0, q1) (G panels) are applied to a tile of block column j
   // by ONE task of depth 128 (q1 - q0) when j >= q1 + L -- the column is not needed until L steps after
