@@ -597,7 +597,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
       it = g_chain_plans.emplace(key, p).first;  // owned for the life of the process
     }
     plan = it->second;
-    ctl_ints = 4 + (size_t)lay->batch * ((size_t)plan.nblk + 2 * (size_t)plan.nblk * plan.nsl + (size_t)plan.nsl * plan.nbc);
+    ctl_ints = 4 + (size_t)lay->batch * (2 * (size_t)plan.nblk + 2 * (size_t)plan.nblk * plan.nsl + (size_t)plan.nsl * plan.nbc);
     ctl_ints = (ctl_ints + 3) / 4 * 4;
   }
   {
@@ -627,12 +627,13 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.sdone = a.dflag + plan.nblk;
   a.ucnt = a.sdone + (size_t)plan.nblk * plan.nsl;
   a.qdone = a.ucnt + (size_t)plan.nsl * plan.nbc;
+  a.hflag = a.qdone + (size_t)plan.nblk * plan.nsl;
   a.nsl = plan.nsl;
   a.nbc = plan.nbc;
   a.nmem = lay->batch;
   a.w_bs = lay->w_batch_stride;
   a.inv_bs = lay->inv_batch_stride;
-  a.ctl_stride = (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
+  a.ctl_stride = 2 * (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
   a.uq = tn.chain_uq != 0 ? 1 : 0;
   a.row_end = lay->y_row + 1;
   a.timeout = std::max<int64_t>(1, tn.chain_timeout_ms) * 100000;  // 100 MHz ticks

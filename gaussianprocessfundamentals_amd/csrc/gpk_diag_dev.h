@@ -691,9 +691,16 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
       }
     }
     stamp(s, 1);
+    if (a.half_flag && s == a.half_step && wave != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wg_sync<SC1>();
     // ---------------------------------------------------------------- QR_s
     stamp(s, 2);
+    // (persistent factorisation: block rows 0 .. half_step - 1 of L^-1 went out in P_1 .. P_half_step and every
+    // storing wave drained them before the barrier -- an idle wave of this QR phase publishes them for the panel
+    // solves' first column blocks)
+    if (a.half_flag && s == a.half_step && wave == NTL - 1) {
+      __hip_atomic_store((gi32*)a.half_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     xs = d4{0.0, 0.0, 0.0, 0.0};  // (the old value is dead: nothing keeps it alive across potf2)
     if (s < NTL - 1 && wave < NTL - 1 - s && !(a.dbg & 4)) {
       const int i = s + 1 + wave;

@@ -139,6 +139,8 @@ struct DiagArgs {
   const int64_t* mb;
   int32_t* ctr;
   uint64_t* prof;  // (GPK_DIAG_PROF builds) per step and wave: s_memtime stamps of the phases, else NULL
+  int32_t* half_flag;     // (persistent factorisation) set once block rows 0 .. half_step - 1 of L_kk^-1 are stored
+  int32_t half_step;      //   (P phase after which they are; half_flag NULL: no early flag)
   int32_t defer_l_store;  // 1: L_kk stays in LDS only (the persistent factorisation stores it after publishing:
                           // no task of the launch reads it)
   int32_t no_inv_zeros;  // 1: leave the tiles of Winv above the diagonal tiles unwritten (the persistent
@@ -158,6 +160,7 @@ struct ChainArgs {
   int32_t* sdone;        // [nblk][nsl]: S(k, r) done
   int32_t* ucnt;         // [nsl][nbc]: panels applied to slice r of block column j
   int32_t* qdone;        // [nblk][nsl]: quarter updates (UQ) of panel k done on slice r of diagonal block k + 1
+  int32_t* hflag;        // [nblk]: rows 0..63 of L_kk^-1 stored (D(k) mid-way; the first half of S(k, .) may start)
   int32_t uq;            // D(k) waits for the UQ tasks of panel k - 1 (else for ucnt)
   int32_t nsl, nbc;      // live 32-row slices (the last one holds the y row), live block columns
   int32_t nmem;          // members (task word bits 8..): W + m w_bs, Winv + m inv_bs, info + m, counters + m ctl_stride

@@ -656,6 +656,12 @@ enum { CH_D = 0, CH_S = 1, CH_U32 = 2, CH_BLK = 3 };
 #ifndef GPK_CHAIN_DEFER_L
 #define GPK_CHAIN_DEFER_L 1  // D publishes L_kk^-1 first and stores L_kk (read by no task of the launch) afterwards
 #endif
+#ifndef GPK_CHAIN_SHALF
+#define GPK_CHAIN_SHALF 1  // the diagonal chain's S tasks start their first column blocks on D's early flag
+#endif
+#ifndef GPK_CHAIN_SHALF_ROWS
+#define GPK_CHAIN_SHALF_ROWS 96  // rows of L_kk^-1 behind that flag (a multiple of 16; D publishes after P_(rows/16))
+#endif
 #ifndef GPK_CHAIN_SPREF
 #define GPK_CHAIN_SPREF 1  // S stages its slice before waiting for D (0: one wait for both inputs)
 #endif
@@ -669,17 +675,19 @@ __device__ __forceinline__ void st_flag(int32_t* p, int32_t v) {
   __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// wave 0: wait until *p >= v; false on timeout (which it reports) or after another task's timeout
-__device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p, int32_t v, uint64_t t0) {
+// one wave: wait until *p >= v; false on timeout (which it reports) or after another task's timeout.  Plain
+// values (the task bodies call it too, and they must not take the kernel argument by reference)
+__device__ __forceinline__ bool chain_wait_v(const int32_t* p, int32_t v, int32_t* ctl, int32_t* info, int nmem,
+                                             int64_t timeout, int force_abort, uint64_t t0) {
   // (polled values through readfirstlane: the loop is wave-uniform, as every branch of chain_kernel)
-  while (a.force_abort || __builtin_amdgcn_readfirstlane(ld_flag(p)) < v) {
-    if (__builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) return false;
-    if (a.force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout) {
-      st_flag(a.ctl + 1, 1);
+  while (force_abort || __builtin_amdgcn_readfirstlane(ld_flag(p)) < v) {
+    if (__builtin_amdgcn_readfirstlane(ld_flag(ctl + 1)) != 0) return false;
+    if (force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)timeout) {
+      st_flag(ctl + 1, 1);
       // every member may be incomplete now: info = -1 wherever no non-positive pivot was found first
-      for (int m = 0; m < a.nmem; ++m) {
+      for (int m = 0; m < nmem; ++m) {
         int32_t zero = 0;
-        __hip_atomic_compare_exchange_strong((gi32*)(a.info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+        __hip_atomic_compare_exchange_strong((gi32*)(info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
       }
       return false;
@@ -688,6 +696,18 @@ __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p,
   }
   return true;
 }
+__device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p, int32_t v, uint64_t t0) {
+  return chain_wait_v(p, v, a.ctl, a.info, a.nmem, a.timeout, a.force_abort, t0);
+}
+// the wait of a panel solve's second column half (waves 4..7) for the whole of L_kk^-1
+struct HalfWait {
+  const int32_t* full;  // NULL: no split (the whole panel solve already waited)
+  int32_t* ctl;
+  int32_t* info;
+  int nmem;
+  int64_t timeout;
+  int force_abort;
+};
 
 // wave 0: wait until *p[i] >= v[i] for every i -- the N counters polled together (all loads in flight at once,
 // one round trip per poll: a task's inputs are usually all published by the time it looks, and polling them one
@@ -741,9 +761,9 @@ __device__ __forceinline__ void slab_stage_a(const double* A, int64_t ld, char* 
     glds16a<kLdAux>(A + (int64_t)row * ld + 2 * lane, smem + row * SLAB_LDS_ROW);
   }
 }
-template <bool SUB, bool STAGED = false>
+template <bool SUB, bool STAGED = false, bool HALF = false>
 __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int64_t ldb, double* C, int64_t ld,
-                                          int diag_off, uint64_t* st, char* smem) {
+                                          int diag_off, uint64_t* st, char* smem, HalfWait hw = HalfWait{}) {
   typedef double dbl2 __attribute__((ext_vector_type(2)));
   const int tid = opaque_tid();
   const int lane = tid & 63;
@@ -769,11 +789,19 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
       acc1[i] = ld8_buf(crs, cvo, ldc16 + i * ldc4);
     }
   }
+  // HALF (S, its slice already in LDS behind the caller's barrier): column blocks below GPK_CHAIN_SHALF_ROWS / 16
+  // need only the rows of L^-1 that D publishes before its last steps, and go at once; the others wait for all of it
+  if (HALF && cb >= GPK_CHAIN_SHALF_ROWS / 16) {
+    if (chain_wait_v(hw.full, 1, hw.ctl, hw.info, hw.nmem, hw.timeout, hw.force_abort,
+                     __builtin_amdgcn_s_memrealtime()) && !kChainSc1Ld) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
   dbl2 bv[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) bv[j] = ld16_buf(brs, j <= jm ? bvo + j * 64 : kRsrcBytes, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA writes are not tracked by hipcc)
-  __syncthreads();
+  if (!HALF) __syncthreads();
   if (st && w == 0) st[4] = __builtin_amdgcn_s_memrealtime();  // (profiling: operands in place)
   const char* a0 = smem + lr * SLAB_LDS_ROW + q * 16;
   const char* a1 = a0 + 16 * SLAB_LDS_ROW;
@@ -972,7 +1000,7 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
 // turned the claim loop's exit into an exec-mask-controlled loop whose barriers the waves no longer
 // executed the same number of times (the deadlock of the first versions).
 GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, int dbg, int k, uint64_t* dprof,
-                                    double* sm) {
+                          int32_t* half_flag, double* sm) {
   DiagArgs da{};
   da.W = W;
   da.ld = ld;
@@ -985,6 +1013,8 @@ GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, in
   da.prof = dprof;
   da.no_inv_zeros = 1;  // (S reads only the lower 16-tiles of L^-1: slab_gemm's skipped pieces; gpk_trsv likewise)
   da.defer_l_store = GPK_CHAIN_DEFER_L;
+  da.half_flag = half_flag;
+  da.half_step = GPK_CHAIN_SHALF_ROWS / 16;
   diag2_body<double, false, true>(da, 0, sm);
 }
 GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
@@ -994,6 +1024,11 @@ GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int 
 GPK_CHAIN_FN void chain_s_staged(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
   double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
   slab_gemm<false, true>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem);
+}
+GPK_CHAIN_FN void chain_s_half(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem,
+                               HalfWait hw) {
+  double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
+  slab_gemm<false, true, true>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem, hw);
 }
 GPK_CHAIN_FN void chain_s_stage(double* W, int64_t ld, int k, int r, char* smem) {
   slab_stage_a(W + (int64_t)r * 32 * ld + (int64_t)k * NB, ld, smem);
@@ -1130,6 +1165,7 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     // L_kk^-1 is: wait for that first, start the slice's LDS-DMA, then wait for D(k) -- the slice's load leaves
     // the critical chain D(k) -> S
     const bool spref = GPK_CHAIN_SPREF && ty == CH_S;
+    const bool shalf = GPK_CHAIN_SHALF && spref && (r >> 2) == k + 1;  // (the S tasks on the diagonal chain)
     if (wave == 0) {
       if (a.times) a.times[6 * t] = __builtin_amdgcn_s_memrealtime();
       const bool ok = spref ? (k == 0 || chain_wait(a, a.ucnt + co + (int64_t)r * a.nbc + k, k,
@@ -1152,7 +1188,8 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     if (spref) {
       chain_s_stage(Wm, a.ld, k, r, reinterpret_cast<char*>(sm));
       if (wave == 0) {
-        const bool ok = chain_wait(a, a.dflag + co + k, 1, __builtin_amdgcn_s_memrealtime());
+        // (GPK_CHAIN_SHALF: rows 0..63 of L_kk^-1 suffice for the first column half; the rest waits in the body)
+        const bool ok = chain_wait(a, (shalf ? a.hflag : a.dflag) + co + k, 1, __builtin_amdgcn_s_memrealtime());
         if (a.times) a.times[6 * t + 1] = __builtin_amdgcn_s_memrealtime();
         if (ok && !kChainSc1Ld) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1167,7 +1204,12 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       }
     }
     if (ty == CH_D) {
-      chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, a.dprof, sm);
+      chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, a.dprof,
+              GPK_CHAIN_SHALF ? a.hflag + co + k : nullptr, sm);
+    } else if (shalf) {
+      chain_s_half(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
+                   reinterpret_cast<char*>(sm),
+                   HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort});
     } else if (spref) {
       chain_s_staged(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
                      reinterpret_cast<char*>(sm));
@@ -1294,7 +1336,7 @@ hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipSt
 
 __global__ __launch_bounds__(DT) void chain_d_only_kernel(ChainArgs a) {  // (debugging: GPK_CHAIN_DBG=4)
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, 0, a.dprof, sm);
+  chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, 0, a.dprof, nullptr, sm);
 }
 
 hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {
