@@ -407,6 +407,35 @@ __device__ __forceinline__ int opaque_tid() {
   asm volatile("" : "+v"(t));
   return t;
 }
+// Hand-off words of the persistent factorisation (gpk_potrf.hip, chain_kernel): agent-scope relaxed atomics
+__device__ __forceinline__ int32_t ld_flag(const int32_t* p) {
+  return __hip_atomic_load((gi32*)const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(int32_t* p, int32_t v) {
+  __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one wave: wait until *p >= v; false on timeout (which it reports) or after another task's timeout.  Plain
+// values (the task bodies call it too, and they must not take the kernel argument by reference)
+__device__ __forceinline__ bool chain_wait_v(const int32_t* p, int32_t v, int32_t* ctl, int32_t* info, int nmem,
+                                             int64_t timeout, int force_abort, uint64_t t0) {
+  // (polled values through readfirstlane: the loop is wave-uniform, as every branch of chain_kernel)
+  while (force_abort || __builtin_amdgcn_readfirstlane(ld_flag(p)) < v) {
+    if (__builtin_amdgcn_readfirstlane(ld_flag(ctl + 1)) != 0) return false;
+    if (force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)timeout) {
+      st_flag(ctl + 1, 1);
+      // every member may be incomplete now: info = -1 wherever no non-positive pivot was found first
+      for (int m = 0; m < nmem; ++m) {
+        int32_t zero = 0;
+        __hip_atomic_compare_exchange_strong((gi32*)(info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
 // Workgroup barrier.  SC1: an LDS-only one -- __syncthreads() also waits for every outstanding global
 // access of the wave (vmcnt(0)), and with write-through stores in flight each of the block's 17 barriers
 // waited for their acknowledgement from beyond the L2.  Nothing in the block body reads back what it

@@ -668,34 +668,6 @@ enum { CH_D = 0, CH_S = 1, CH_U32 = 2, CH_BLK = 3 };
 constexpr int CHAIN_SLOT_OFF = (int)((DIAG_LDS_BYTES + 15) / 16 * 16);
 constexpr size_t CHAIN_LDS_BYTES = CHAIN_SLOT_OFF + 16;
 
-__device__ __forceinline__ int32_t ld_flag(const int32_t* p) {
-  return __hip_atomic_load((gi32*)const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_flag(int32_t* p, int32_t v) {
-  __hip_atomic_store((gi32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// one wave: wait until *p >= v; false on timeout (which it reports) or after another task's timeout.  Plain
-// values (the task bodies call it too, and they must not take the kernel argument by reference)
-__device__ __forceinline__ bool chain_wait_v(const int32_t* p, int32_t v, int32_t* ctl, int32_t* info, int nmem,
-                                             int64_t timeout, int force_abort, uint64_t t0) {
-  // (polled values through readfirstlane: the loop is wave-uniform, as every branch of chain_kernel)
-  while (force_abort || __builtin_amdgcn_readfirstlane(ld_flag(p)) < v) {
-    if (__builtin_amdgcn_readfirstlane(ld_flag(ctl + 1)) != 0) return false;
-    if (force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)timeout) {
-      st_flag(ctl + 1, 1);
-      // every member may be incomplete now: info = -1 wherever no non-positive pivot was found first
-      for (int m = 0; m < nmem; ++m) {
-        int32_t zero = 0;
-        __hip_atomic_compare_exchange_strong((gi32*)(info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return true;
-}
 __device__ __forceinline__ bool chain_wait(const ChainArgs& a, const int32_t* p, int32_t v, uint64_t t0) {
   return chain_wait_v(p, v, a.ctl, a.info, a.nmem, a.timeout, a.force_abort, t0);
 }
