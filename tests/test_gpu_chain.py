@@ -82,6 +82,21 @@ def test_chain_bitwise_vs_launch_path(n, m):
     assert fc.out.cpu()[0].item() == fl.out.cpu()[0].item()
 
 
+@pytest.mark.parametrize("group,uq", [(1, 0), (1, 1), (4, 0), (8, 1)])
+@pytest.mark.parametrize("n,m", [(2100, 40), (5000, 0)])
+def test_chain_plan_variants_bitwise_vs_launch_path(n, m, group, uq):
+    """Every planner variant (deferred-update depth chain_group, the next diagonal block's update as quarter tasks or
+    one task per slice) reproduces the launch path bit for bit: the same per-tile MFMA k-order in every variant."""
+    with engine.nat.thread_tune(chain_group=group, chain_uq=uq):
+        before = engine.nat.chain_stats()["launches"]
+        fc, _ = _run(n, m, 1)
+        assert engine.nat.chain_stats()["launches"] > before
+    fl, _ = _run(n, m, 0)
+    a, b = _lower(fc), _lower(fl)
+    assert int(np.count_nonzero(a.view(np.uint64) != b.view(np.uint64))) == 0
+    assert fc.out.cpu()[0].item() == fl.out.cpu()[0].item()
+
+
 def test_chain_noise_1e8_matches_the_oracle():
     """The reference's default jitter (1e-8, cond(K) ~ 1e10 at N = 256) through the persistent launch."""
     f, (x, y) = _run(1000, 0, 1, noise=1e-8)
