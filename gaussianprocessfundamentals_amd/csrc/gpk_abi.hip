@@ -635,6 +635,10 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.inv_bs = lay->inv_batch_stride;
   a.ctl_stride = 2 * (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
   a.uq = tn.chain_uq != 0 ? 1 : 0;
+  // rows of L_kk^-1 behind D's early flag: later (more of the panel solve early) for short chains, where the
+  // diagonal chain is all there is; earlier for long ones, where the S tasks' waiting CUs cost tile-update time
+  // (N = 4096: 112 rows 1.501 vs 96 rows 1.515 ms; 6144 / 8192 2.42 / 4.44 vs 2.37 / 4.39, profiles/r04ab_*)
+  a.half_step = (plan.nblk <= 32 ? GPK_CHAIN_SHALF_ROWS_SMALL : GPK_CHAIN_SHALF_ROWS) / 16;
   a.row_end = lay->y_row + 1;
   a.timeout = std::max<int64_t>(1, tn.chain_timeout_ms) * 100000;  // 100 MHz ticks
   for (int64_t f = g_chain_force_timeout.load(); f > 0;)

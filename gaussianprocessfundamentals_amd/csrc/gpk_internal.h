@@ -147,6 +147,15 @@ struct DiagArgs {
                          // factorisation's panel solves never read them; the launch path's TRSM does)
 };
 
+// rows of L_kk^-1 behind the diagonal task's early flag (multiples of 16; D publishes after its step rows / 16), for
+// chains of more than / at most 32 diagonal blocks
+#ifndef GPK_CHAIN_SHALF_ROWS
+#define GPK_CHAIN_SHALF_ROWS 96
+#endif
+#ifndef GPK_CHAIN_SHALF_ROWS_SMALL
+#define GPK_CHAIN_SHALF_ROWS_SMALL 112
+#endif
+
 // persistent factorisation (gpk_potrf.hip chain_kernel): one f64 member, tasks in host-computed order
 struct ChainArgs {
   double* W;
@@ -160,7 +169,9 @@ struct ChainArgs {
   int32_t* sdone;        // [nblk][nsl]: S(k, r) done
   int32_t* ucnt;         // [nsl][nbc]: panels applied to slice r of block column j
   int32_t* qdone;        // [nblk][nsl]: quarter updates (UQ) of panel k done on slice r of diagonal block k + 1
-  int32_t* hflag;        // [nblk]: rows 0..63 of L_kk^-1 stored (D(k) mid-way; the first half of S(k, .) may start)
+  int32_t* hflag;        // [nblk]: rows 0 .. 16 half_step - 1 of L_kk^-1 stored (D(k) before its end: the diagonal
+                         // chain's S(k, .) start their first column blocks)
+  int32_t half_step;     //   (D's step after which it sets hflag)
   int32_t uq;            // D(k) waits for the UQ tasks of panel k - 1 (else for ucnt)
   int32_t nsl, nbc;      // live 32-row slices (the last one holds the y row), live block columns
   int32_t nmem;          // members (task word bits 8..): W + m w_bs, Winv + m inv_bs, info + m, counters + m ctl_stride

@@ -659,9 +659,7 @@ enum { CH_D = 0, CH_S = 1, CH_U32 = 2, CH_BLK = 3 };
 #ifndef GPK_CHAIN_SHALF
 #define GPK_CHAIN_SHALF 1  // the diagonal chain's S tasks start their first column blocks on D's early flag
 #endif
-#ifndef GPK_CHAIN_SHALF_ROWS
-#define GPK_CHAIN_SHALF_ROWS 96  // rows of L_kk^-1 behind that flag (a multiple of 16; D publishes after P_(rows/16))
-#endif
+
 #ifndef GPK_CHAIN_SPREF
 #define GPK_CHAIN_SPREF 1  // S stages its slice before waiting for D (0: one wait for both inputs)
 #endif
@@ -679,6 +677,7 @@ struct HalfWait {
   int nmem;
   int64_t timeout;
   int force_abort;
+  int split;  // the first column block that waits for all of L^-1 (rows of the early flag / 16)
 };
 
 // wave 0: wait until *p[i] >= v[i] for every i -- the N counters polled together (all loads in flight at once,
@@ -763,7 +762,7 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
   }
   // HALF (S, its slice already in LDS behind the caller's barrier): column blocks below GPK_CHAIN_SHALF_ROWS / 16
   // need only the rows of L^-1 that D publishes before its last steps, and go at once; the others wait for all of it
-  if (HALF && cb >= GPK_CHAIN_SHALF_ROWS / 16) {
+  if (HALF && cb >= hw.split) {
     if (chain_wait_v(hw.full, 1, hw.ctl, hw.info, hw.nmem, hw.timeout, hw.force_abort,
                      __builtin_amdgcn_s_memrealtime()) && !kChainSc1Ld) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -972,7 +971,7 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
 // turned the claim loop's exit into an exec-mask-controlled loop whose barriers the waves no longer
 // executed the same number of times (the deadlock of the first versions).
 GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, int dbg, int k, uint64_t* dprof,
-                          int32_t* half_flag, double* sm) {
+                          int32_t* half_flag, int half_step, double* sm) {
   DiagArgs da{};
   da.W = W;
   da.ld = ld;
@@ -986,7 +985,7 @@ GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, in
   da.no_inv_zeros = 1;  // (S reads only the lower 16-tiles of L^-1: slab_gemm's skipped pieces; gpk_trsv likewise)
   da.defer_l_store = GPK_CHAIN_DEFER_L;
   da.half_flag = half_flag;
-  da.half_step = GPK_CHAIN_SHALF_ROWS / 16;
+  da.half_step = half_step;
   diag2_body<double, false, true>(da, 0, sm);
 }
 GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
@@ -1177,11 +1176,11 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     }
     if (ty == CH_D) {
       chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, a.dprof,
-              GPK_CHAIN_SHALF ? a.hflag + co + k : nullptr, sm);
+              GPK_CHAIN_SHALF ? a.hflag + co + k : nullptr, a.half_step, sm);
     } else if (shalf) {
       chain_s_half(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
                    reinterpret_cast<char*>(sm),
-                   HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort});
+                   HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort, a.half_step});
     } else if (spref) {
       chain_s_staged(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
                      reinterpret_cast<char*>(sm));
@@ -1308,7 +1307,7 @@ hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipSt
 
 __global__ __launch_bounds__(DT) void chain_d_only_kernel(ChainArgs a) {  // (debugging: GPK_CHAIN_DBG=4)
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, 0, a.dprof, nullptr, sm);
+  chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, 0, a.dprof, nullptr, 0, sm);
 }
 
 hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {
