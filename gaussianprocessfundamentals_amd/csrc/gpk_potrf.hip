@@ -636,15 +636,19 @@ hipError_t launch_gemm_t(const GemmArgs& a, int32_t batch, hipStream_t s) {
 // inputs on per-task counters, and publish their outputs with write-through stores.  Tasks (block =
 // 128 rows / columns, slice = 32 rows, panel k = block column k):
 //   D(k)          diagonal block k, the diag2 body (factor + inverse) on the block as the earlier tasks
-//                 left it; L_kk to W, L_kk^-1 to Winv; dflag[k]
-//   S(k, r)       slice r below block k: X = A(r, k) L_kk^-T, in place; sdone[k][r]
+//                 left it; L_kk^-1 to Winv (its lower tiles), hflag[k] once its first half_step block rows are
+//                 out, dflag[k] at the end; L_kk to W after the hand-off (no task of the launch reads it)
+//   S(k, r)       slice r below block k: X = A(r, k) L_kk^-T, in place; sdone[k][r].  It stages its slice once
+//                 the slice's last update is in; on the diagonal chain (r in block k + 1) its first column
+//                 blocks start on hflag[k], the others on dflag[k]
 //   U32(q, r, j)  slice r of block column j = q + 1: C -= X(r, q) X(j, q)^T; ucnt[r][j] = q + 1
 //   UQ(q, r, j, c) the same on the 32-column quarter c only, for the slices r of diagonal block j (round 4);
 //                 qdone[q][r] += 1 -- D(j) waits for all of them
 //   BLK(q, i, j)  128 x 128 tile (i, j), j >= q + 2: C -= X(i, q..) X(j, q..)^T over g panels q .. q + g - 1
 //                 (g = 1 for the columns the diagonal chain needs soon, g = the planner's group for the deferred
 //                 ones: the launch path's deep group update); ucnt[r][j] = q + g for the slices r of block i
-// The chain D(k) -> S(k, block k + 1) -> U32(k, block k + 1, k + 1) -> D(k + 1) runs on slices spread
+// Every task polls all its input counters together (chain_wait_set: one round trip per poll).
+// The chain D(k) -> S(k, block k + 1) -> UQ(k, block k + 1, k + 1) -> D(k + 1) runs on slices spread
 // over CUs (a 128-row panel solve or update on one CU would take ~14 us of f64 MFMA), the BLK tiles of
 // older panels fill the rest of the chip -- the look-ahead that launches cannot give a single
 // evaluation (persistent factorisation).  Hand-offs (MI355X guide, inter-workgroup
