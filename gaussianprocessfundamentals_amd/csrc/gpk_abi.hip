@@ -171,7 +171,8 @@ struct Tune {
   int64_t chain_max_p;    //   ... while the augmented matrix has at most this many rows
   int64_t chain_grid;     //   workgroups of that launch (0: one per CU)
   int64_t chain_timeout_ms;  // bound of every wait inside it (then info = -1)
-  int64_t chain_group;    //   panels per deferred tile update (1: every tile update one panel deep)
+  int64_t chain_group;    //   panels per deferred tile update (1: every tile update one panel deep; 0: auto,
+                          //   chain_group_for)
   int64_t chain_max_batch;   // batches of up to this many members run as one persistent launch too ...
   int64_t chain_batch_max_rows;  // ... while batch x (rows of the augmented matrix) stays within this
                                  // (batch x span, persistent vs launch path: N = 2048 x 8 1.15 vs 1.38 ms,
@@ -198,7 +199,7 @@ Tune& tune() {
                          env_i64("GPK_GROUP_EYE", 4), env_i64("GPK_ASM_GENERIC", 0),
                          env_i64("GPK_PANEL_STREAM", 0), env_i64("GPK_TRD_SPLIT_M", 1024),
                          env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 12416), env_i64("GPK_CHAIN_GRID", 0),
-                         env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 4),
+                         env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 0),
                          env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500),
                          env_i64("GPK_CHAIN_UQ", 1)};
   return t;
@@ -408,6 +409,14 @@ int64_t g_chain_times_n = 0;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
+// panels per deferred tile update: the knob, or (0) 4 below 80 diagonal blocks and 8 from there -- the deep
+// updates' MFMA rate starts to matter more than the columns they hold back (N = 8192 4.46 / 4.49 ms with 4 / 8,
+// 10240 7.74 / 7.62, 12288 12.56 / 12.17, profiles/r04af_chain_group_large.jsonl)
+int chain_group_for(int64_t knob, int64_t n_pad) {
+  if (knob > 0) return (int)knob;
+  return n_pad / NB >= 80 ? 8 : 4;
+}
+
 std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group, int nmem, int chain_uq) {
   const int nblk = (int)(n_pad / NB), yb = (int)(y_row / NB), rlast = (int)(y_row / 32);
   struct Task {
@@ -582,7 +591,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   size_t ctl_ints = 0;
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
-    const int group = (int)tn.chain_group, nmem = lay->batch;
+    const int group = chain_group_for(tn.chain_group, lay->n_pad), nmem = lay->batch;
     auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
@@ -1901,7 +1910,8 @@ int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_ou
   if (y_row < n_pad) return fail_arg(2, "y_row (>= n_pad)");
   if (grid <= 0) return fail_arg(3, "grid");
   if (!ntasks) return fail_arg(6, "ntasks");
-  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, (int)tune_now().chain_group, 1, (int)tune_now().chain_uq);
+  const std::vector<int32_t> ord =
+      chain_order(n_pad, y_row, grid, chain_group_for(tune_now().chain_group, n_pad), 1, (int)tune_now().chain_uq);
   *ntasks = (int64_t)(ord.size() / 4);
   if (tasks_out) {
     if (cap < *ntasks) return fail_arg(5, "cap (fewer than ntasks)");

@@ -395,7 +395,7 @@ int gpk_timing_reset(void);
  * workgroups (0: one per CU), every wait bounded by "chain_timeout_ms": 1, the default, auto: unless a
  * factorisation this library enqueued on another stream of the device is still in flight (each
  * persistent launch claims every CU); 2 always; 0 never), with "chain_group" panels per deferred tile update
- * (4), "chain_uq" (1: the next diagonal block's update by each panel as 32-column quarter tasks; 0: one task
+ * (0, the default: 4 below 80 diagonal blocks, 8 from there), "chain_uq" (1: the next diagonal block's update by each panel as 32-column quarter tasks; 0: one task
  * per 32-row slice) and, for batches, "chain_max_batch" members (8) while batch x p <= "chain_batch_max_rows"
  * (17500).
  * A persistent launch whose wait timed out

@@ -131,7 +131,7 @@ def test_knob_defaults_land_in_their_fields(lib):
     """tune() initialises its struct positionally: every knob reads back its documented default (a field
     inserted out of order shifts the values of the ones after it)."""
     import os
-    expect = {"chain": 1, "chain_max_p": 12416, "chain_grid": 0, "chain_timeout_ms": 1000, "chain_group": 4,
+    expect = {"chain": 1, "chain_max_p": 12416, "chain_grid": 0, "chain_timeout_ms": 1000, "chain_group": 0,
               "chain_max_batch": 8, "chain_batch_max_rows": 17500, "chain_uq": 1, "group": 8, "lookahead": 2,
               "fuse_kbuild": 1, "diag_version": 2}
     for k, v in expect.items():
