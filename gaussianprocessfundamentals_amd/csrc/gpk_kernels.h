@@ -219,7 +219,12 @@ __device__ __forceinline__ double per_sc_value(const FastNode& f, SA sa, CA ca, 
 #pragma clang fp contract(on)  // fuse within an expression only: every caller rounds alike
   double sn = 0.0;
   for (int k = 0; k < f.d; ++k) {
-    const double t = sa(k) * cb(k) - ca(k) * sb(k);
+    // sin(pi (a - b) / p) = sa cb - ca sb, the two products rounded separately (no FMA between them): swapping
+    // the points swaps them exactly, so t(b, a) = -t(a, b) and K stays exactly symmetric (a contracted
+    // fma(sa, cb, -ca sb) left 1-ulp asymmetries, found by tests/test_gpu_properties.py)
+    const double p1 = sa(k) * cb(k);
+    const double p2 = ca(k) * sb(k);
+    const double t = p1 - p2;
     sn += t * t;
   }
   return f.sg * exp((-2.0 * sn) * f.il2);
