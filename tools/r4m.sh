@@ -1,4 +1,5 @@
 # software-pipelined DPP potf2: correctness, spans (vs unpipelined DPP), D phase timeline
+# (historical A/B script of round 4: the variant libraries it names were built with tools/build_variant.sh and removed after the measurement -- see DESIGN §4 for the outcome)
 set -o pipefail
 O=gpurun_out/r4m; mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_chain.py tests/test_gpu_parity.py tests/test_gpu_diag_versions.py -m gpu > $O/tests.log 2>&1 || { echo "tests failed" >> $O/tests.log; exit 1; }

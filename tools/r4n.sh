@@ -1,4 +1,5 @@
 # packed potf2 (factor + inverse in the two halves of the wave) and one-Newton-step variants
+# (historical A/B script of round 4: the variant libraries it names were built with tools/build_variant.sh and removed after the measurement -- see DESIGN §4 for the outcome)
 set -o pipefail
 O=gpurun_out/r4n; mkdir -p $O
 timeout -k 5 60 ./tools/probe/permlane_probe > $O/permlane.txt 2>&1 && timeout -k 5 60 ./tools/probe/lat_probe > $O/lat.txt 2>&1 || exit 1

@@ -1,4 +1,5 @@
 # S prefetch on by default (tests), then the diagonal body's split accumulators / paired trailing tiles
+# (historical A/B script of round 4: the variant libraries it names were built with tools/build_variant.sh and removed after the measurement -- see DESIGN §4 for the outcome)
 set -o pipefail
 O=gpurun_out/r4p; mkdir -p $O
 true

@@ -1,4 +1,5 @@
 # one Newton step + the non-positive pivot from the diagonal after the tile: probes, tests, spans
+# (historical A/B script of round 4: the variant libraries it names were built with tools/build_variant.sh and removed after the measurement -- see DESIGN §4 for the outcome)
 set -o pipefail
 O=gpurun_out/r4u; mkdir -p $O
 for b in lb_n1 lb_n2 oldbad_n2; do timeout -k 5 30 ./tools/probe/potf2_$b >> $O/probe.txt 2>&1 || exit 1; done
