@@ -91,34 +91,43 @@ class NystroemAdjoint:
         self.noise_bar.add_(torch.dot(a, a), alpha=-w)
 
     def nystroem_logdet(self, w: float):
-        """(n - m) log noise + logdet(C), C = noise I_m + D S~ D in K_mm's eigenbasis (S~ = V^T K_mn K_nm V,
-        D = diag(lam^-1/2) on the kept eigenvalues, 0 on the dropped ones; the similar symmetric form of
-        the reference's noise I + K_mn K_nm pinv(K_mm)):
-          d/d noise = (n - m) / noise + tr C^-1,   d/d K_nm = 2 G C^-1 U^T   (U = V D, G = K_nm U),
-          d/d pinv(K_mm) in the eigenbasis: (S~ - S~ D C^-1 D S~) / noise, written without its cancellation
-          as D^-1 (I - noise C^-1) D^-1 on the kept block and D^-1 C^-1 D S~ on the kept x dropped one
-          (the dropped block is multiplied by 0 in pinv's reverse mode)."""
+        """(n - m) log noise + log|det C|, C = noise S + D S~ D in K_mm's eigenbasis (S~ = V^T K_mn K_nm V,
+        D = diag(|lam|^-1/2) on the kept eigenvalues, 0 on the dropped ones, S = diag(sign lam) with +1 on the
+        dropped ones; log|det C| equals the reference's slogdet(noise I + K_mn K_nm pinv(K_mm))[1], Nystroem_K.py):
+          d/d noise = (n - m) / noise + tr(C^-1 S),   d/d K_nm = 2 G C^-1 U^T   (U = V D, G = K_nm U),
+          d/d pinv(K_mm) in the eigenbasis: (I + S~ F / noise)^-1 S~ / noise (F = D S D), written without its
+          cancellation as D^-1 S (S - noise C^-1) S D^-1 on the kept block and D^-1 S C^-1 D S~ on the kept x
+          dropped one (the dropped block is multiplied by 0 in pinv's reverse mode).  For a kernel matrix K_mm
+          S = I and C = noise I + G^T G is positive definite (augmented Cholesky); an indefinite K_mm (the
+          reference's L1 forms at D > 1) takes C^-1 from the eigendecomposition."""
+        from ..Statistics.Nystroem_K import signed_pinv_factor, sym_inverse
         knm, lam, V, mu0, P = self.nystroem()
         n, m = self.n, int(V.shape[0])
-        U1, rank, mu1 = engine.pinv_factor(lam, V, 1, return_mu=True)
-        if int(rank.cpu()[0]) < 0:
-            raise NotImplementedError("K_mm has a negative eigenvalue above the pinv cutoff")
+        U1, sgn, n_neg, mu1 = signed_pinv_factor(lam, V)
         G = engine.dgemm(knm, U1)
         S = engine.dgemm(G, G, trans_a=True)
-        cinv = engine.DenseFactorization(m, inverse=True).run(S.contiguous(), self.noise)
-        cinv.check_info()
-        Ci = cinv.k_inv(0).to(torch.float64).contiguous()
-        self.noise_bar.add_((n - m) / self.noise + torch.trace(Ci), alpha=w)
+        if n_neg == 0:
+            cinv = engine.DenseFactorization(m, inverse=True).run(S.contiguous(), self.noise)
+            cinv.check_info()
+            Ci = cinv.k_inv(0).to(torch.float64).contiguous()
+            tr = torch.trace(Ci)
+        else:
+            C = S.clone()
+            C.diagonal().add_(self.noise * sgn)
+            Ci = sym_inverse(C).contiguous()
+            tr = torch.sum(torch.diagonal(Ci) * sgn)
+        self.noise_bar.add_((n - m) / self.noise + tr, alpha=w)
         self._acc_knm(engine.dgemm(engine.dgemm(G, Ci), U1, trans_b=True), 2.0 * w)
         kept = mu1 != 0
         dinv = torch.where(kept, 1.0 / torch.where(kept, mu1, torch.ones_like(mu1)), torch.zeros_like(mu1))
+        ds = dinv * sgn
         T = -self.noise * Ci
-        T.diagonal().add_(1.0)
-        T = dinv[:, None] * T * dinv[None, :]
+        T.diagonal().add_(sgn)
+        T = ds[:, None] * T * ds[None, :]
         if not bool(kept.all()):
             KV = engine.dgemm(knm, V)
             St = engine.dgemm(KV, KV, trans_a=True)
-            Q = engine.dgemm((dinv[:, None] * Ci * mu1[None, :]).contiguous(), St)
+            Q = engine.dgemm((ds[:, None] * Ci * mu1[None, :]).contiguous(), St)
             Q = Q * (kept[:, None] & ~kept[None, :])
             T = T + Q + Q.T
         self._acc_t(T, w)

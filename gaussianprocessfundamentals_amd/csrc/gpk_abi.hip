@@ -362,7 +362,21 @@ std::map<std::tuple<int, int64_t, int64_t, int, int, int, int>, ChainPlan> g_cha
 // by a memset enqueued before each launch, so two threads enqueueing on one stream (torch's null stream
 // is shared by every thread) must never share them -- memset A, memset B, launch A, launch B would hand
 // launch B counters already past its task count.  A thread's own calls on one stream are stream-ordered.
-thread_local std::map<std::pair<int, hipStream_t>, std::pair<int32_t*, size_t>> t_chain_ctl;
+// The blocks are freed when their thread exits (hipFree waits for the device, so no launch still reads them).
+struct ChainCtl {
+  std::map<std::pair<int, hipStream_t>, std::pair<int32_t*, size_t>> blocks;
+  ~ChainCtl() {
+    for (auto& kv : blocks)
+      if (kv.second.first) {
+        int cur = 0;
+        if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first.first) == hipSuccess) {
+          (void)hipFree(kv.second.first);
+          (void)hipSetDevice(cur);
+        }
+      }
+  }
+};
+thread_local ChainCtl t_chain_ctl;
 std::atomic<int64_t> g_chain_launches{0};      // persistent launches enqueued
 std::atomic<int64_t> g_chain_declined{0};      // auto mode: launch path taken, another stream busy
 std::atomic<int64_t> g_chain_force_timeout{0};  // testing: the next N persistent launches time out
@@ -394,14 +408,26 @@ void note_factorisation(hipStream_t s) {
   hipEventRecord(e, s);
 }
 
+// (entries of other streams whose last factorisation has completed are dropped -- streams come and go, e.g. a
+// pipelined sweep's -- once the map holds more than a few; the caller's own entry is kept for its next record)
 bool other_stream_busy(hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return true;
   std::lock_guard<std::mutex> lk(g_busy_mu);
-  for (const auto& kv : g_busy)
-    if (kv.first.first == dev && kv.first.second != s && kv.second && hipEventQuery(kv.second) == hipErrorNotReady)
-      return true;
-  return false;
+  const bool prune = g_busy.size() > 16;
+  bool busy = false;
+  for (auto it = g_busy.begin(); it != g_busy.end();) {
+    const bool other = !(it->first.first == dev && it->first.second == s);
+    const hipError_t q = it->second ? hipEventQuery(it->second) : hipSuccess;
+    if (other && it->first.first == dev && q == hipErrorNotReady) busy = true;
+    if (prune && other && q != hipErrorNotReady) {
+      if (it->second) hipEventDestroy(it->second);
+      it = g_busy.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  return busy;
 }
 int32_t* g_chain_trace = nullptr;  // GPK_CHAIN_TRACE=1: pinned host words the kernel writes its progress to
 uint64_t* g_chain_times = nullptr;  // GPK_CHAIN_TIMES=1: device stamps per task of the last profiled launch
@@ -610,7 +636,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     ctl_ints = (ctl_ints + 3) / 4 * 4;
   }
   {
-    auto& c = t_chain_ctl[{dev, s}];  // this thread's own (see t_chain_ctl)
+    auto& c = t_chain_ctl.blocks[{dev, s}];  // this thread's own (see t_chain_ctl)
     if (c.second < ctl_ints) {
       // (hipFree synchronises the device: no launch of this thread still uses the old block)
       if (c.first) GPK_HIP(hipFree(c.first), "chain scratch");

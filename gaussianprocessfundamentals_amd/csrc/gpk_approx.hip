@@ -236,8 +236,9 @@ __global__ __launch_bounds__(256) void jacobi_out_kernel(const double* Af, const
   if (i == j) lam[(int64_t)b * m + i] = Af[b * mm + e];
 }
 
-// per member: mu_i = 1 / lam_i (mode 0) or 1 / sqrt(lam_i) (mode 1) for |lam_i| > rcond max|lam|,
-// else 0 (tf.linalg.pinv's cutoff); rank[b] = kept count, -1 if mode 1 keeps a negative value
+// per member: mu_i = 1 / lam_i (mode 0), 1 / sqrt(lam_i) (mode 1) or 1 / sqrt(|lam_i|) (mode 2: the symmetric
+// factor of an indefinite pinv, whose signs the caller keeps) for |lam_i| > rcond max|lam|, else 0
+// (tf.linalg.pinv's cutoff); rank[b] = kept count, -1 if mode 1 keeps a negative value
 __global__ __launch_bounds__(256) void pinv_mu_kernel(const double* lam, int m, double rcond, int mode, double* mu,
                                                       int32_t* rank) {
   __shared__ double red[256];
@@ -260,6 +261,7 @@ __global__ __launch_bounds__(256) void pinv_mu_kernel(const double* lam, int m, 
     if (fabs(v) > cut) {
       kept += 1;
       if (mode == 0) u = 1.0 / v;
+      else if (mode == 2) u = 1.0 / sqrt(fabs(v));
       else if (v > 0.0) u = 1.0 / sqrt(v);
       else neg = 1;
     }

@@ -922,6 +922,10 @@ hipError_t launch_vjp(const gpk_kdesc& kd, const VjpArgs& g0, const double* X, i
   const size_t lds = sizeof(double) * (GPK_MAX_HYP + 4 * GNP + 4 * (size_t)ATILE * d +
                                        2 * (size_t)(1 + kd.n_ard) * ATILE * a.dp +
                                        (has_mul ? (size_t)kd.n_nodes * 256 : 0));
+  {
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(vjp_kernel), lds);  // (d = 16, two ARD nodes: 118 KB)
+    if (e != hipSuccess) return e;
+  }
   if (kd.n_hyp > 0) {
     hipLaunchKernelGGL(vjp_kernel, dim3((unsigned)tc, (unsigned)tr), dim3(256), lds, s, kd, a, g);
     hipError_t e = hipGetLastError();
@@ -965,6 +969,11 @@ hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_
                                        2 * (size_t)(1 + kd.n_ard) * ATILE * a.dp +
                                        (has_mul ? (size_t)kd.n_nodes * 256 : 0));
   dim3 grid((unsigned)ntri, (unsigned)batch, 1);
+  {
+    hipError_t e = ensure_dyn_lds(dtype == GPK_F64 ? reinterpret_cast<const void*>(grad_kernel<double>)
+                                                   : reinterpret_cast<const void*>(grad_kernel<float>), lds);
+    if (e != hipSuccess) return e;
+  }
   if (dtype == GPK_F64)
     hipLaunchKernelGGL(grad_kernel<double>, grid, dim3(256), lds, s, kd, a, g);
   else
@@ -1002,6 +1011,19 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
   // instantiation: 0 single base node, 2 two leaves under one ADD / MUL, 1 any other tree
   const bool pair = kd.n_nodes == 3 && (kd.nodes[2].op == GPK_OP_ADD || kd.nodes[2].op == GPK_OP_MUL);
   const int tree = kd.n_nodes == 1 ? 0 : (pair && !tune_pair_off() ? 2 : 1);
+  // (above 64 KB -- e.g. an ARD node beside a standard PER node, whose per-point sin / cos take two more point
+  // slots, at d = 16: 71 KB; two ARD nodes: 87 KB -- the kernel's dynamic-LDS limit must be raised first)
+  {
+    const void* fn = dtype == GPK_F64
+                         ? (tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<double, 2>)
+                                      : tree == 1 ? reinterpret_cast<const void*>(assemble_kernel<double, 1>)
+                                                  : reinterpret_cast<const void*>(assemble_kernel<double, 0>))
+                         : (tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<float, 2>)
+                                      : tree == 1 ? reinterpret_cast<const void*>(assemble_kernel<float, 1>)
+                                                  : reinterpret_cast<const void*>(assemble_kernel<float, 0>));
+    hipError_t e = ensure_dyn_lds(fn, lds);
+    if (e != hipSuccess) return e;
+  }
   if (dtype == GPK_F64) {
     if (tree == 2)
       hipLaunchKernelGGL((assemble_kernel<double, 2>), grid, dim3(256), lds, s, kd, a);

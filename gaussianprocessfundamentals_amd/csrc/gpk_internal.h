@@ -4,9 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
 #include <mutex>
-#include <set>
-#include <tuple>
+#include <utility>
 
 #include "gpk.h"
 
@@ -16,18 +16,20 @@ constexpr int NB = 128;     // panel width == update tile edge == diagonal block
 constexpr int ATILE = 64;   // assemble tile edge
 
 // Dynamic LDS above 64 KB needs hipFuncAttributeMaxDynamicSharedMemorySize, which is a per-device
-// attribute of the kernel: set it once per (device, kernel, size) before the first launch on a device.
+// attribute of the kernel: raised (never lowered -- one kernel may be launched with several sizes) to the
+// largest size requested so far on the device, before the launch that needs it.
 inline hipError_t ensure_dyn_lds(const void* fn, size_t bytes) {
   static std::mutex mu;
-  static std::set<std::tuple<int, const void*, size_t>> done;
+  static std::map<std::pair<int, const void*>, size_t> done;
+  if (bytes <= 65536) return hipSuccess;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_tuple(dev, fn, bytes);
-  if (done.count(key)) return hipSuccess;
+  size_t& have = done[{dev, fn}];
+  if (have >= bytes) return hipSuccess;
   e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e == hipSuccess) done.insert(key);
+  if (e == hipSuccess) have = bytes;
   return e;
 }
 

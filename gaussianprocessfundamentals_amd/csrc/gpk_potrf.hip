@@ -1172,11 +1172,11 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
         }
         slot[1] = ok ? 1 : 0;
       }
+      // every wave's own slice rows have landed before the barrier: the panel solve reads all 32 rows from LDS,
+      // and its HALF form has no barrier of its own after the operand loads (each wave drains only its own DMA)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (!__builtin_amdgcn_readfirstlane(slot[1])) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the staged slice lands before anything else)
-        continue;
-      }
+      if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
     }
     if (ty == CH_D) {
       chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, a.dprof,

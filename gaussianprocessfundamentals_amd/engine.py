@@ -23,9 +23,12 @@ from . import global_parameters as gp
 # A single f64 factorisation may run as ONE persistent launch (gpk_tune "chain", include/gpk.h).  Its
 # inter-workgroup waits are bounded; a wait that times out (the device shared with another process past
 # chain_timeout_ms, a preempted workgroup) leaves info = -1 and the factorisation incomplete.  With
-# CHAIN_VERIFY (default) every run that took the persistent launch reads its info back (one 4-byte
-# device-to-host copy) and, on -1, assembles and factors again on the launch path in the same call;
-# CHAIN_FALLBACKS counts those re-runs.  The reference's tf.linalg.cholesky never fails spuriously
+# CHAIN_VERIFY (default) a run that took the persistent launch is verified lazily: run() itself never
+# synchronises (calls enqueue ahead of the device), and the FIRST read of its results -- info, out, W and every
+# read-out accessor -- reads info back (one 4-byte device-to-host copy, which waits for that run) and, on -1,
+# assembles and factors again on the launch path, on the run's own stream, before returning; CHAIN_FALLBACKS
+# counts those re-runs.  (The re-run reads the operands passed to run(): they must not be overwritten in
+# between.)  The reference's tf.linalg.cholesky never fails spuriously
 # (gpbasics/Statistics/CovarianceMatrix.py:250), so neither may this.
 CHAIN_VERIFY = True
 CHAIN_FALLBACKS = 0
@@ -174,38 +177,84 @@ class AugmentedFactorization:
         lay = self.layout
         dev = device()
         es = 8 if self.code == nat.GPK_F64 else 4
-        self.W = torch.empty(lay.w_bytes // es, dtype=self.dtype, device=dev)
-        self.Winv = torch.empty(max(1, lay.inv_bytes // es), dtype=self.dtype, device=dev)
-        self.info = torch.zeros(self.batch, dtype=torch.int32, device=dev)
-        self.out = torch.empty(self.batch * 4, dtype=torch.float64, device=dev)
-        self.mu = torch.empty(max(1, self.batch * self.m), dtype=torch.float64, device=dev)
-        self.var = torch.empty(max(1, self.batch * self.m), dtype=torch.float64, device=dev)
+        self._pending = None   # (rerun, stream) of a persistent run not yet verified (see CHAIN_VERIFY)
+        self._W = torch.empty(lay.w_bytes // es, dtype=self.dtype, device=dev)
+        self._Winv = torch.empty(max(1, lay.inv_bytes // es), dtype=self.dtype, device=dev)
+        self._info = torch.zeros(self.batch, dtype=torch.int32, device=dev)
+        self._out = torch.empty(self.batch * 4, dtype=torch.float64, device=dev)
+        self._mu = torch.empty(max(1, self.batch * self.m), dtype=torch.float64, device=dev)
+        self._var = torch.empty(max(1, self.batch * self.m), dtype=torch.float64, device=dev)
         self.kd = None
         self.done = False
         self.shape_key = None
 
+    # -- result buffers: every read settles a pending persistent run first ---------------------
+    @property
+    def W(self) -> torch.Tensor:
+        self._settle()
+        return self._W
+
+    @property
+    def Winv(self) -> torch.Tensor:
+        self._settle()
+        return self._Winv
+
+    @property
+    def info(self) -> torch.Tensor:
+        self._settle()
+        return self._info
+
+    @property
+    def out(self) -> torch.Tensor:
+        self._settle()
+        return self._out
+
+    @property
+    def mu(self) -> torch.Tensor:
+        self._settle()
+        return self._mu
+
+    @property
+    def var(self) -> torch.Tensor:
+        self._settle()
+        return self._var
+
     # -- launches ---------------------------------------------------------------------------
-    def _verify_chain(self, rerun) -> None:
-        """After a run: if libgpk took the persistent launch for it and a wait timed out (info = -1), run
-        it again on the launch path (same call, same buffers) and count the fallback."""
+    def _defer_verify(self, rerun) -> None:
+        """After a run: if libgpk took the persistent launch for it, remember how to re-run it; the first read
+        of a result verifies it (:meth:`_settle`).  No synchronisation here."""
+        self._pending = None
+        if CHAIN_VERIFY and nat.last_factorisation_was_chain():
+            self._pending = (rerun, torch.cuda.current_stream(self._W.device))
+
+    def _settle(self) -> None:
+        """Verify a pending persistent run: if a wait timed out (info = -1), run it again on the launch path on
+        the run's own stream and count the fallback.  Synchronises with that run."""
         global CHAIN_FALLBACKS
-        if not CHAIN_VERIFY or not nat.last_factorisation_was_chain():
+        pend = self._pending
+        if pend is None:
             return
-        if not bool((self.info == -1).any()):   # (synchronises the stream)
-            return
-        CHAIN_FALLBACKS += 1
-        logging.warning("persistent factorisation timed out (gpk_tune chain_timeout_ms): re-running it on the "
-                        "launch path (%d fallbacks so far)", CHAIN_FALLBACKS)
-        with nat.thread_tune(chain=0):
-            rerun()
+        self._pending = None
+        rerun, stream = pend
+        with torch.cuda.stream(stream):
+            if not bool((self._info == -1).any()):   # (waits for the run)
+                return
+            CHAIN_FALLBACKS += 1
+            logging.warning("persistent factorisation timed out (gpk_tune chain_timeout_ms): re-running it on the "
+                            "launch path (%d fallbacks so far)", CHAIN_FALLBACKS)
+            with nat.thread_tune(chain=0):
+                rerun()
 
     def run(self, kd: nat.GpkKdesc, hyp: torch.Tensor, hyp_stride: int, noise: torch.Tensor,
             noise_stride: int, X: torch.Tensor, x_bstride: int, y: torch.Tensor, y_bstride: int,
             Xs: Optional[torch.Tensor] = None, xs_bstride: int = 0,
             E: Optional[torch.Tensor] = None, e_bstride: int = 0):
+        """Enqueue the factorisation (asynchronous: a persistent run is verified at the first read, see
+        CHAIN_VERIFY)."""
         args = (kd, hyp, hyp_stride, noise, noise_stride, X, x_bstride, y, y_bstride, Xs, xs_bstride, E, e_bstride)
+        self._pending = None   # (the previous run's results are overwritten unread)
         self._run_once(*args)
-        self._verify_chain(lambda: self._run_once(*args))
+        self._defer_verify(lambda: self._run_once(*args))
         return self
 
     def _run_once(self, kd, hyp, hyp_stride, noise, noise_stride, X, x_bstride, y, y_bstride, Xs, xs_bstride,
@@ -339,6 +388,7 @@ class InverseFactorization(AugmentedFactorization):
     def run(self, kd: nat.GpkKdesc, hyp: torch.Tensor, hyp_stride: int, noise: torch.Tensor,
             noise_stride: int, X: torch.Tensor, x_bstride: int, y: torch.Tensor, y_bstride: int,
             gradient: bool = True, **unused):
+        self._pending = None
         lay = self.layout
         B, n, d = self.batch, self.n, self.d
         dev = self.W.device
@@ -422,6 +472,7 @@ class RaggedFactorization(AugmentedFactorization):
     def run(self, members: Sequence, noise) -> "RaggedFactorization":
         """members[b] = (kdesc, hyp [n_hyp] fp64, X_b [n_b, d], y_b [n_b], Xs_b [m_b, d] or None);
         noise: rank-0 or one value per member."""
+        self._pending = None
         B, n, m, d = self.batch, self.n, self.m, self.d
         self._alphas = None
         if len(members) != B:
@@ -636,7 +687,8 @@ def eigh(A: torch.Tensor):
 
 def pinv_factor(lam: torch.Tensor, V: torch.Tensor, mode: int, rcond: float = -1.0, return_mu: bool = False):
     """U = V diag(mu) with tf.linalg.pinv's cutoff (gpk_pinv_factor): mode 0 mu = 1/lam (pinv = U V^T),
-    mode 1 mu = lam^-1/2 (pinv = U U^T).  Returns (U, rank [B] int32 device tensor) (+ mu)."""
+    mode 1 mu = lam^-1/2 (pinv = U U^T), mode 2 mu = |lam|^-1/2 (pinv = U diag(sign lam) U^T).  Returns (U, rank
+    [B] int32 device tensor) (+ mu)."""
     squeeze = V.dim() == 2
     V3 = V.unsqueeze(0) if squeeze else V
     lam2 = lam.unsqueeze(0) if lam.dim() == 1 else lam
@@ -744,8 +796,9 @@ class DenseFactorization(AugmentedFactorization):
         super().__init__(n, 1, n if inverse else m, batch, torch.float64)
 
     def run(self, A: torch.Tensor, noise, y: Optional[torch.Tensor] = None, E: Optional[torch.Tensor] = None):
+        self._pending = None
         self._run_once(A, noise, y, E)
-        self._verify_chain(lambda: self._run_once(A, noise, y, E))
+        self._defer_verify(lambda: self._run_once(A, noise, y, E))
         return self
 
     def _run_once(self, A, noise, y, E):

@@ -29,7 +29,12 @@
  *  - Return value: 0 on success, -i for an invalid i-th argument, > 0 for a HIP error
  *    code.  A matrix that is not positive definite is NOT an error of the call: it is
  *    reported through info_dev[b] (LAPACK convention: 1-based index of the first
- *    non-positive pivot, 0 when the factorisation succeeded).
+ *    non-positive pivot, 0 when the factorisation succeeded).  info_dev[b] = -1 is an
+ *    infrastructure failure of the persistent factorisation (a bounded wait timed out, gpk_tune
+ *    "chain"), never "not positive definite": that member's results are undefined and the call must
+ *    be repeated with gpk_tune("chain", 0) (or gpk_tune_thread).  Every entry that factors a single
+ *    f64 member, or a batch of at most "chain_max_batch" members, can report it -- gpk_nlml,
+ *    gpk_potrf_aug(_ex), gpk_nlml_batched, gpk_potrf_lower included.
  *  - gpk_last_error() returns a thread-local description of the last failure.
  *  - `stream` is a hipStream_t passed as void* (0 = the null stream).
  *
@@ -257,7 +262,8 @@ int gpk_posterior(const gpk_kdesc* kd, const double* hyp_dev, int dtype, const d
                   void* stream);
 
 /* -LML of `batch` hyperparameter / noise candidates on shared X [n, d], y [n] (device):
- * hyp_dev [batch][kd->n_hyp], noise_dev [batch], nlml_dev [batch] (+inf where info_dev[b] != 0).
+ * hyp_dev [batch][kd->n_hyp], noise_dev [batch], nlml_dev [batch] (+inf where info_dev[b] != 0; info_dev[b] = -1:
+ * the persistent launch timed out, see Conventions -- repeat the call with gpk_tune("chain", 0)).
  * LogLikelihood.get_metric for each candidate (Metrics/LogLikelihood.py:30-65). */
 int gpk_nlml_batched(const gpk_kdesc* kd, int32_t batch, const double* hyp_dev, const double* noise_dev, int dtype,
                      const double* X, const double* y, int64_t n, int32_t d, void* work, size_t work_bytes,
@@ -267,7 +273,8 @@ int gpk_nlml_batched(const gpk_kdesc* kd, int32_t batch, const double* hyp_dev, 
  * MFMA path) A [n, lda] (upper triangle untouched, LAPACK potrf semantics) through the blocked MFMA
  * factorisation: tf.linalg.cholesky of get_L_K
  * (Statistics/CovarianceMatrix.py:247-254).  *info_dev: 0 or the first non-positive pivot
- * (1-based); *logdet_dev (may be NULL) = 2 sum log diag L (Metrics/Metrics.py:152-154). */
+ * (1-based), or -1 when the persistent launch timed out (A undefined; see Conventions); *logdet_dev (may be
+ * NULL) = 2 sum log diag L (Metrics/Metrics.py:152-154). */
 int gpk_potrf_lower(int dtype, void* A, int64_t n, int64_t lda, void* work, size_t work_bytes, int32_t* info_dev,
                     double* logdet_dev, void* stream);
 
@@ -310,9 +317,10 @@ size_t gpk_syevd_workspace_bytes(int64_t m);
 int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
               void* work, size_t work_bytes, void* stream);
 
-/* U = V diag(mu) with mu_i = 1 / lam_i (mode 0; pinv = U V^T) or 1 / sqrt(lam_i) (mode 1;
- * pinv = U U^T) for |lam_i| > rcond max|lam| and 0 otherwise -- tf.linalg.pinv's cutoff (rcond < 0:
- * its default 10 m eps).  rank_dev[b] = kept eigenvalues, -1 if mode 1 keeps a negative one. */
+/* U = V diag(mu) with mu_i = 1 / lam_i (mode 0; pinv = U V^T), 1 / sqrt(lam_i) (mode 1;
+ * pinv = U U^T) or 1 / sqrt(|lam_i|) (mode 2; pinv = U diag(sign lam) U^T, for an indefinite matrix) for
+ * |lam_i| > rcond max|lam| and 0 otherwise -- tf.linalg.pinv's cutoff (rcond < 0: its default 10 m eps).
+ * rank_dev[b] = kept eigenvalues, -1 if mode 1 keeps a negative one. */
 int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam, double rcond, int32_t mode,
                     double* mu, double* U, int32_t* rank_dev, void* stream);
 

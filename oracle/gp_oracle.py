@@ -529,6 +529,16 @@ def nystroem_det(tree, hyp, noise, x, z, scaled=False, se_expanded=False) -> flo
     return float((n - m) * math.log(noise) + np.linalg.slogdet(to_det)[1])
 
 
+def nystroem_k_approx_inv(tree, hyp, noise, x, z, scaled=False, se_expanded=False) -> np.ndarray:
+    """get_K_approx_inv (Statistics/Nystroem_K.py:73-90), the reference's Woodbury form op for op:
+    (1 / noise) (I - K_nm (pinv(noise I_m + pinv(K_mm) K_nm^T K_nm) (pinv(K_mm) K_nm^T)))."""
+    _, knm, kmm = nystroem_k_approx(tree, hyp, x, z, scaled, se_expanded)
+    n, m = knm.shape
+    dot_aux = tf_pinv(kmm) @ knm.T
+    inner = tf_pinv(np.eye(m) * noise + dot_aux @ knm)
+    return (1.0 / noise) * (np.eye(n) - knm @ (inner @ dot_aux))
+
+
 def nystroem_nlml(tree, hyp, noise, x, y, z, handling: str = "CHOLESKY_BASED", lower_bound: bool = False,
                   jitter: float = 1e-8, scaled=False, se_expanded=False) -> float:
     """LogLikelihood.get_metric with BASIC_NYSTROEM / SKC_LOWER_BOUND (Metrics/LogLikelihood.py:30-65,

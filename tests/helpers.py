@@ -37,3 +37,14 @@ def set_flags(scaled=False, expanded=False, dtype=torch.float64):
     gp.p_scaled_base_kernel = scaled
     gp.p_se_expanded_norm = expanded
     gp.p_dtype = dtype
+
+
+def jitter_nll_bar(K, y, nlml, c=4.0):
+    """Relative -LML error bar for an ill-conditioned K (the reference's default jitter 1e-8, cond(K) ~ 1e10):
+    a backward-stable Cholesky returns the factor of K + E with |E| ~ eps |K|, which moves the data fit
+    y^T K^-1 y by about alpha^T E alpha <= eps ||K||_2 ||alpha||^2, i.e. the -LML by half of it.  The bar is c times
+    that first-order estimate relative to |nlml| (c = 4: a few rounding errors per entry of E) -- derived from the
+    conditioning of this K and y, not a fixed number.  K, y: the oracle's fp64 arrays."""
+    yv = np.asarray(y, dtype=np.float64).reshape(-1)
+    alpha = np.linalg.solve(K, yv)
+    return c * np.finfo(np.float64).eps * 0.5 * np.linalg.norm(K, 2) * float(alpha @ alpha) / abs(nlml)

@@ -89,6 +89,25 @@ def test_nystroem_with_all_points_is_exact():
     assert abs(lb - (exact + 12 * 1e-2 / (2 * 1e-8))) < 1e-6 * abs(lb)
 
 
+def test_nystroem_indefinite_kmm_known_answers():
+    """The reference's default L1 Matern-5/2 at D = 4 gives an indefinite K_mm (negative eigenvalues above
+    tf.linalg.pinv's cutoff).  The restated Woodbury inverse (Nystroem_K.py:73-90) is then still the inverse of
+    K_hat + noise I, and the restated determinant (:92-108) its log|det| (Sylvester: det(noise I_n + K_nm P K_mn)
+    = noise^(n - m) det(noise I_m + K_mn K_nm P)) -- the identities the device's symmetric forms rely on."""
+    rng = np.random.default_rng(21)
+    x, z = rng.uniform(0, 1, (120, 4)), rng.uniform(0, 1, (30, 4))
+    tree, hyp = ("MAT52", {"ard": True}), [[1.0, 1.0, 1.0, 1.0]]
+    kmm = o.kernel_matrix(tree, hyp, z, z)
+    lam = np.linalg.eigvalsh(kmm)
+    assert lam[0] < -10 * 30 * np.finfo(np.float64).eps * np.abs(lam).max()
+    for noise in (0.5, 1e-2):
+        khat, _, _ = o.nystroem_k_approx(tree, hyp, x, z)
+        A = khat + noise * np.eye(120)
+        inv = o.nystroem_k_approx_inv(tree, hyp, noise, x, z)
+        np.testing.assert_allclose(inv @ A, np.eye(120), atol=1e-8 * np.abs(inv).max() * np.abs(A).max())
+        assert abs(o.nystroem_det(tree, hyp, noise, x, z) - np.linalg.slogdet(A)[1]) < 1e-9 * 120
+
+
 def test_ski_weights_on_inducing_points_and_midpoints():
     z = np.array([[0.0], [1.0], [2.0]])
     w = o.ski_weight_matrix(z, z)

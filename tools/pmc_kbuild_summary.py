@@ -1,4 +1,4 @@
-"""Summary of tools/r4d_kbuild_pmc.sh (rocprofv3 PMC passes over tools/bench_kbuild.py C5): per assemble_kernel
+"""Summary of tools/rounds/r4/r4d_kbuild_pmc.sh (rocprofv3 PMC passes over tools/bench_kbuild.py C5): per assemble_kernel
 dispatch, the VALU / SALU / LDS instruction counts per matrix element, the VALU issue utilisation, and HBM bytes
 (2 x FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction) against the algorithmic bytes and 8 TB/s.
 
