@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must be loaded first: libgpk binds to torch's HIP r
 
 from . import _build
 
-GPK_ABI_VERSION = 5
+GPK_ABI_VERSION = 6
 GPK_F64, GPK_F32 = 0, 1
 OP_PER, OP_SE, OP_MAT32, OP_MAT52, OP_ADD, OP_MUL = 104, 105, 107, 108, 201, 202
 NODE_SCALED, NODE_ARD, NODE_SE_EXPANDED, NODE_STANDARD = 1, 2, 4, 8
@@ -33,7 +33,7 @@ EXPORTS = (
     "gpk_assemble_dense", "gpk_dgemm", "gpk_syevj_workspace_bytes", "gpk_syevj", "gpk_pinv_factor",
     "gpk_ski_weights", "gpk_add_diagonal", "gpk_distance_matrix", "gpk_workspace_bytes", "gpk_nlml_batched", "gpk_potrf_lower", "gpk_trsv_lower", "gpk_posterior",
     "gpk_kernel_vjp_workspace_bytes", "gpk_kernel_vjp", "gpk_pinv_backward_scale", "gpk_syevd_workspace_bytes",
-    "gpk_syevd", "gpk_chain_plan", "gpk_tune_thread", "gpk_chain_stats",
+    "gpk_syevd", "gpk_chain_plan", "gpk_tune_thread", "gpk_chain_stats", "gpk_chain_plan_ex",
 )
 
 
@@ -120,6 +120,7 @@ def _declare(lib):
         "gpk_syevd_workspace_bytes": (c_size_t, [c_int64]),
         "gpk_syevd": (c_int, [c_int64, c_int32, P, c_int64, c_int64, P, P, P, c_size_t, P]),
         "gpk_chain_plan": (c_int, [c_int64, c_int64, c_int32, P, c_int64, POINTER(c_int64)]),
+        "gpk_chain_plan_ex": (c_int, [c_int64, c_int64, c_int32, c_int32, P, c_int64, POINTER(c_int64)]),
         "gpk_tune_thread": (c_int, [ctypes.c_char_p, c_int64, c_int32, POINTER(c_int64), POINTER(c_int32)]),
         "gpk_chain_stats": (c_int, [POINTER(c_int64), c_int32]),
         "gpk_chain_trace": (c_int, [P, c_int64]),
@@ -246,16 +247,17 @@ def last_factorisation_was_chain() -> bool:
     return bool(out[2])
 
 
-def chain_plan(n_pad: int, y_row: int, grid: int):
-    """Task list of the persistent single-member factorisation (gpk_chain_plan; host only): an
-    [ntasks, 4] int32 array of (type, k, r, j) in claim order."""
+def chain_plan(n_pad: int, y_row: int, grid: int, eye: bool = False):
+    """Task list of the persistent single-member factorisation (gpk_chain_plan_ex; host only): an
+    [ntasks, 4] int32 array of (type word, k, r, j) in claim order; eye: the identity-augmented list."""
     import numpy as np
     L = load_library()
     nt = c_int64(0)
-    check(L.gpk_chain_plan(int(n_pad), int(y_row), int(grid), None, 0, ctypes.byref(nt)), "gpk_chain_plan")
+    fl = AUG_EXTRA_IDENTITY if eye else 0
+    check(L.gpk_chain_plan_ex(int(n_pad), int(y_row), int(grid), fl, None, 0, ctypes.byref(nt)), "gpk_chain_plan_ex")
     out = np.zeros((int(nt.value), 4), dtype=np.int32)
-    check(L.gpk_chain_plan(int(n_pad), int(y_row), int(grid), c_void_p(out.ctypes.data), int(nt.value),
-                           ctypes.byref(nt)), "gpk_chain_plan")
+    check(L.gpk_chain_plan_ex(int(n_pad), int(y_row), int(grid), fl, c_void_p(out.ctypes.data), int(nt.value),
+                              ctypes.byref(nt)), "gpk_chain_plan_ex")
     return out
 
 

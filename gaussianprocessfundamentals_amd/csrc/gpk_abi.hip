@@ -179,6 +179,9 @@ struct Tune {
                                  // 4096 x 2 1.87 vs 2.53, 4096 x 4 2.83 vs 3.51; 4096 x 8 5.32 vs 5.07,
                                  // 2048 x 16 2.02 vs 1.94 -- profiles/r04_chain_batch.jsonl)
   int64_t chain_uq;       //   the next diagonal block's update split by 32-column quarter (0: one task per slice)
+  int64_t chain_eye;      //   identity-augmented factorisations (the gradient / explicit inverse) too (1: auto as
+                          //   above, 0: never)
+  int64_t chain_max_p_eye;  // ... while their augmented matrix has at most this many rows
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -201,7 +204,8 @@ Tune& tune() {
                          env_i64("GPK_CHAIN", 1), env_i64("GPK_CHAIN_MAX_P", 12416), env_i64("GPK_CHAIN_GRID", 0),
                          env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 0),
                          env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500),
-                         env_i64("GPK_CHAIN_UQ", 1)};
+                         env_i64("GPK_CHAIN_UQ", 1), env_i64("GPK_CHAIN_EYE", 1),
+                         env_i64("GPK_CHAIN_MAX_P_EYE", 16640)};
   return t;
 }
 
@@ -226,6 +230,7 @@ const Knob kKnobs[] = {
     {"chain_grid", &Tune::chain_grid},       {"chain_timeout_ms", &Tune::chain_timeout_ms},
     {"chain_group", &Tune::chain_group},     {"chain_max_batch", &Tune::chain_max_batch},
     {"chain_batch_max_rows", &Tune::chain_batch_max_rows}, {"chain_uq", &Tune::chain_uq},
+    {"chain_eye", &Tune::chain_eye},         {"chain_max_p_eye", &Tune::chain_max_p_eye},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -357,7 +362,7 @@ struct ChainPlan {
   int32_t nblk = 0, nsl = 0, nbc = 0;
 };
 std::mutex g_chain_mu;
-std::map<std::tuple<int, int64_t, int64_t, int, int, int, int>, ChainPlan> g_chain_plans;
+std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int>, ChainPlan> g_chain_plans;
 // Counter scratch of the persistent launch, per (host thread, device, stream): the counters are zeroed
 // by a memset enqueued before each launch, so two threads enqueueing on one stream (torch's null stream
 // is shared by every thread) must never share them -- memset A, memset B, launch A, launch B would hand
@@ -443,8 +448,22 @@ int chain_group_for(int64_t knob, int64_t n_pad) {
   return n_pad / NB >= 80 ? 8 : 4;
 }
 
-std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group, int nmem, int chain_uq) {
+// Type word of a task: ty (bits 0..1) | (g - 1) << 2 (BLK over g panels; UQ: quarter + 1, bits 2..5) |
+// kChainFirst (bit 6: the (slice, block column) cells the task updates have no earlier update -- its counter
+// wait is for 0, not for the task's first panel; identity-augmented lists only) | member << 8.
+constexpr int kChainFirst = 1 << 6;
+
+// eye: identity extra rows (m = n, gpk_potrf_aug_ex GPK_AUG_EXTRA_IDENTITY).  Extra row t (row n_pad + t) of
+// E L^-T is zero left of column t, so block i >= nblk (extra block e = i - nblk) is zero in every panel q < e
+// (its rows' panel columns are zero until panel e, where its identity entries are solved): the list leaves out
+// every task that would only move zeros -- the panel solves of such slices and the tile updates where either
+// block is still zero -- so the factorisation does n^3 flops (potrf + trtri + lauum) like the launch path's
+// band skip.  The block holding the y row is live in every panel.
+std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group, int nmem, int chain_uq,
+                                 bool eye = false) {
   const int nblk = (int)(n_pad / NB), yb = (int)(y_row / NB), rlast = (int)(y_row / 32);
+  // block i holds a nonzero row in the columns of panel q (monotone in q)
+  auto live = [&](int i, int q) { return !eye || i < nblk || i == yb || i - nblk <= q; };
   struct Task {
     int ty, k, r, j;
     float dur;
@@ -474,13 +493,17 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   };
   // BLK tasks carry ty = 3 | (g - 1) << 2 for an update over the g panels k .. k + g - 1
   auto blk = [&](int q0, int g, int i, int jj) {
+    const int ql = q0 + g - 1;  // (S(ql, r) done implies S(q, r) done for every q < ql that has an S task)
+    if (!live(i, ql) || !live(jj, ql)) return;  // (identity rows: zero in every panel of the group)
     Task t{CHT_BLK | ((g - 1) << 2), q0, i, jj, dur[3] * (0.25f + 0.75f * (float)g), {}};
-    const int ql = q0 + g - 1;  // (S(ql, r) done implies S(q, r) done for every q < ql)
     for (int s = 4 * i; s <= std::min(4 * i + 3, rlast); ++s) t.deps.push_back(s_of(ql, s));
     if (jj != i)
       for (int s = 4 * jj; s <= std::min(4 * jj + 3, rlast); ++s) t.deps.push_back(s_of(ql, s));
     auto it = last_upd.find({i, jj});
-    if (it != last_upd.end()) t.deps.push_back(it->second);
+    if (it != last_upd.end())
+      t.deps.push_back(it->second);
+    else if (q0 > 0)
+      t.ty |= kChainFirst;
     last_upd[{i, jj}] = add(t);
   };
   // the next diagonal block's update by panel k, split by 32-column quarter (UQ: U32 with the quarter + 1 in
@@ -499,16 +522,22 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
       }
     D[k] = add(d);
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
+      if (!live(r / 4, k)) continue;
       Task t{CHT_S, k, r, 0, dur[1], {D[k]}};
-      if (k > 0) t.deps.push_back(u_of(k - 1, r));
+      if (k > 0 && live(r / 4, k - 1))
+        t.deps.push_back(u_of(k - 1, r));
+      else if (k > 0)
+        t.ty |= kChainFirst;  // (the slice's first live panel: nothing updated it before)
       S[(size_t)k * nr + r] = add(t);
     }
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
+      if (!live(r / 4, k)) continue;
       auto it = last_upd.find({r / 4, k + 1});
+      const int first = (it == last_upd.end() && k > 0) ? kChainFirst : 0;
       if (uq && k + 1 < nblk && r < 4 * (k + 2)) {
         const int rl = r - 4 * (k + 1);
         for (int q = 0; q <= rl; ++q) {  // lower quarters of the diagonal block's slice r
-          Task t{CHT_U32 | ((q + 1) << 2), k, r, k + 1, dur[2] * 0.5f, {s_of(k, r)}};
+          Task t{CHT_U32 | ((q + 1) << 2) | first, k, r, k + 1, dur[2] * 0.5f, {s_of(k, r)}};
           if (q != rl) t.deps.push_back(s_of(k, 4 * (k + 1) + q));
           if (it != last_upd.end()) t.deps.push_back(it->second);
           uq_of[r].push_back(add(t));
@@ -516,7 +545,7 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
         U[(size_t)k * nr + r] = uq_of[r].back();  // (not read: D(k + 1) waits for every quarter)
         continue;
       }
-      Task t{CHT_U32, k, r, k + 1, dur[2], {s_of(k, r)}};
+      Task t{CHT_U32 | first, k, r, k + 1, dur[2], {s_of(k, r)}};
       for (int s = 4 * (k + 1); s <= std::min(4 * (k + 1) + 3, rlast); ++s)
         if (s != r) t.deps.push_back(s_of(k, s));
       if (it != last_upd.end()) t.deps.push_back(it->second);
@@ -590,12 +619,13 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   return out;
 }
 
-// chain_kernel applies to one f64 member without identity or ragged rows, on a stream that is not being
-// captured (the first call of a shape uploads its task list), up to chain_max_p rows
+// chain_kernel applies to one f64 member (or a small batch) without ragged rows -- identity extra rows
+// included (chain_eye) --, on a stream that is not being captured (the first call of a shape uploads its task
+// list), up to chain_max_p (identity rows: chain_max_p_eye) rows
 bool chain_applies(const gpk_layout* lay, bool eye, const int64_t* n_dev, const int64_t* m_dev, const Tune& tn,
                    hipStream_t s) {
-  if (!tn.chain || lay->dtype != GPK_F64 || eye || n_dev || m_dev) return false;
-  if (lay->batch == 1 ? lay->p > tn.chain_max_p
+  if (!tn.chain || lay->dtype != GPK_F64 || (eye && !tn.chain_eye) || n_dev || m_dev) return false;
+  if (lay->batch == 1 ? lay->p > (eye ? tn.chain_max_p_eye : tn.chain_max_p)
                       : (lay->batch > tn.chain_max_batch || lay->batch * lay->p > tn.chain_batch_max_rows))
     return false;
   if (tn.diag_dbg != 0 || tn.diag_version == 1) return false;
@@ -607,7 +637,8 @@ bool chain_applies(const gpk_layout* lay, bool eye, const int64_t* n_dev, const 
   return true;
 }
 
-int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, const Tune& tn, hipStream_t s) {
+int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, const Tune& tn, hipStream_t s,
+                bool eye) {
   int dev = 0, ncu = 0;
   GPK_HIP(hipGetDevice(&dev), "device");
   GPK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "device");
@@ -618,10 +649,11 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
     const int group = chain_group_for(tn.chain_group, lay->n_pad), nmem = lay->batch;
-    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq);
+    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq, eye ? 1 : 0);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
-      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq);
+      const std::vector<int32_t> ord =
+          chain_order(lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq, eye);
       ChainPlan p;
       p.ntasks = (int32_t)(ord.size() / 4);
       p.nblk = (int32_t)(lay->n_pad / NB);
@@ -704,7 +736,8 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     a.trace = grid <= 4096 ? g_chain_trace : nullptr;
   }
   const double n3 = (double)lay->n_pad;
-  GPK_HIP(timed(3, lay->batch * n3 * n3 * n3 / 3.0, 0.0, s, [&] { return launch_chain(a, grid, s); }), "chain");
+  GPK_HIP(timed(3, lay->batch * n3 * n3 * n3 / (eye ? 1.0 : 3.0), 0.0, s, [&] { return launch_chain(a, grid, s); }),
+          "chain");
   ++g_chain_launches;
   t_chain_last = true;
   return 0;
@@ -860,7 +893,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   t_chain_last = false;
   // a single evaluation: the whole factorisation as one persistent launch (no K build fused into it)
   if (!kb && chain_applies(lay, eye, n_dev, m_dev, tn, s)) {
-    const int e = chain_potrf(lay, W, Winv, info_dev, tn, s);
+    const int e = chain_potrf(lay, W, Winv, info_dev, tn, s, eye);
     if (!e) note_factorisation(s);
     return e;
   }
@@ -1812,7 +1845,7 @@ int gpk_pinv_factor(int64_t m, int32_t batch, const double* V, const double* lam
   if (batch <= 0) return fail_arg(2, "batch");
   if (!V) return fail_arg(3, "V");
   if (!lam) return fail_arg(4, "lam");
-  if (mode != 0 && mode != 1) return fail_arg(6, "mode");
+  if (mode < 0 || mode > 2) return fail_arg(6, "mode (0, 1 or 2)");
   if (!mu) return fail_arg(7, "mu");
   if (!U) return fail_arg(8, "U");
   if (!rank_dev) return fail_arg(9, "rank_dev");
@@ -1932,15 +1965,24 @@ int gpk_chain_trace(int32_t* out, int64_t n) {
 }
 
 int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_out, int64_t cap, int64_t* ntasks) {
+  return gpk_chain_plan_ex(n_pad, y_row, grid, 0, tasks_out, cap, ntasks);
+}
+
+int gpk_chain_plan_ex(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, int32_t* tasks_out, int64_t cap,
+                      int64_t* ntasks) {
   if (n_pad <= 0 || n_pad % NB != 0) return fail_arg(1, "n_pad (a positive multiple of 128)");
   if (y_row < n_pad) return fail_arg(2, "y_row (>= n_pad)");
   if (grid <= 0) return fail_arg(3, "grid");
-  if (!ntasks) return fail_arg(6, "ntasks");
-  const std::vector<int32_t> ord =
-      chain_order(n_pad, y_row, grid, chain_group_for(tune_now().chain_group, n_pad), 1, (int)tune_now().chain_uq);
+  if (flags & ~GPK_AUG_EXTRA_IDENTITY) return fail_arg(4, "flags");
+  const bool eye = (flags & GPK_AUG_EXTRA_IDENTITY) != 0;
+  if (eye && (y_row - n_pad < 1 || y_row - n_pad > n_pad))
+    return fail_arg(2, "y_row (identity extra rows: n_pad + n with 0 < n <= n_pad)");
+  if (!ntasks) return fail_arg(7, "ntasks");
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, chain_group_for(tune_now().chain_group, n_pad), 1,
+                                               (int)tune_now().chain_uq, eye);
   *ntasks = (int64_t)(ord.size() / 4);
   if (tasks_out) {
-    if (cap < *ntasks) return fail_arg(5, "cap (fewer than ntasks)");
+    if (cap < *ntasks) return fail_arg(6, "cap (fewer than ntasks)");
     memcpy(tasks_out, ord.data(), ord.size() * sizeof(int32_t));
   }
   return 0;

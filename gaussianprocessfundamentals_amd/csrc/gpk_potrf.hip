@@ -1048,8 +1048,10 @@ __device__ __forceinline__ int claim_ticket(int32_t* p) {
 }
 
 // Wave 0 (all its lanes poll the same words: no lane-divergent branch) waits until the task's inputs are
-// published; false on timeout (reported) or after another task's timeout.
-__device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, int r, int j, int g, int64_t co) {
+// published; false on timeout (reported) or after another task's timeout.  kprev: the count the previous
+// update of the task's cells published (k, or 0 when there is none: the task word's first bit)
+__device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int kprev, int k, int r, int j, int g,
+                                           int64_t co) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int32_t* dflag = a.dflag + co;
   const int32_t* sdone = a.sdone + co;
@@ -1074,7 +1076,7 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, in
     return chain_wait_set<4>(a, p, v, t0);
   } else if (ty == CH_S) {
     const int32_t* p[2] = {dflag + k, ucnt + (int64_t)r * a.nbc + k};
-    const int32_t v[2] = {1, k > 0 ? k : 0};
+    const int32_t v[2] = {1, kprev};
     return chain_wait_set<2>(a, p, v, t0);
   } else if (ty == CH_U32) {
     const int32_t* sd = sdone + (int64_t)k * a.nsl;
@@ -1091,7 +1093,7 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, in
       v[1 + i] = need ? 1 : 0;
     }
     p[5] = ucnt + (int64_t)r * a.nbc + j;
-    v[5] = k > 0 ? k : 0;
+    v[5] = kprev;
     return chain_wait_set<6>(a, p, v, t0);
   }
   // BLK over the g panels k .. k + g - 1: the last panel's solves of both blocks' slices (S(q, r) done implies
@@ -1108,7 +1110,7 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int k, in
     p[4 + i] = sd + (sj < a.nsl ? sj : 4 * j);
     v[4 + i] = sj < a.nsl ? 1 : 0;
     p[8 + i] = ucnt + (int64_t)(sr < a.nsl ? sr : 4 * r) * a.nbc + j;
-    v[8 + i] = (sr < a.nsl && k > 0) ? k : 0;
+    v[8 + i] = sr < a.nsl ? kprev : 0;
   }
   return chain_wait_set<12>(a, p, v, t0);
 }
@@ -1129,8 +1131,9 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     const int t = __builtin_amdgcn_readfirstlane(slot[0]);
     if (t >= a.ntasks) break;
     const int tyg = __builtin_amdgcn_readfirstlane(a.tasks[4 * t]);
-    // BLK: updates over g panels; U32 with g > 1: the quarter g - 2 task (UQ); member
-    const int ty = tyg & 3, g = ((tyg >> 2) & 63) + 1, mem = tyg >> 8;
+    // BLK: updates over g panels; U32 with g > 1: the quarter g - 2 task (UQ); first: the cells the task
+    // updates have no earlier update (identity-augmented lists: their counter waits are for 0); member
+    const int ty = tyg & 3, g = ((tyg >> 2) & 15) + 1, first = (tyg >> 6) & 1, mem = tyg >> 8;
     double* const Wm = a.W + (int64_t)mem * a.w_bs;
     const int64_t co = (int64_t)mem * a.ctl_stride;
     const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
@@ -1143,9 +1146,9 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     const bool shalf = GPK_CHAIN_SHALF && spref && (r >> 2) == k + 1;  // (the S tasks on the diagonal chain)
     if (wave == 0) {
       if (a.times) a.times[6 * t] = __builtin_amdgcn_s_memrealtime();
-      const bool ok = spref ? (k == 0 || chain_wait(a, a.ucnt + co + (int64_t)r * a.nbc + k, k,
-                                                    __builtin_amdgcn_s_memrealtime()))
-                            : chain_deps(a, ty, k, r, j, g, co);
+      const bool ok = spref ? (k == 0 || first || chain_wait(a, a.ucnt + co + (int64_t)r * a.nbc + k, k,
+                                                             __builtin_amdgcn_s_memrealtime()))
+                            : chain_deps(a, ty, first ? 0 : k, k, r, j, g, co);
       if (a.times) {
         a.times[6 * t + 1] = __builtin_amdgcn_s_memrealtime();
         if (ty == CH_D || ty == CH_BLK) a.times[6 * t + 4] = __builtin_amdgcn_s_memtime();  // shader clock

@@ -388,7 +388,15 @@ class InverseFactorization(AugmentedFactorization):
     def run(self, kd: nat.GpkKdesc, hyp: torch.Tensor, hyp_stride: int, noise: torch.Tensor,
             noise_stride: int, X: torch.Tensor, x_bstride: int, y: torch.Tensor, y_bstride: int,
             gradient: bool = True, **unused):
+        """Enqueue the identity-augmented factorisation (+ gradient); single evaluations take the persistent
+        launch like the value path and are verified at the first read (CHAIN_VERIFY)."""
+        args = (kd, hyp, hyp_stride, noise, noise_stride, X, x_bstride, y, y_bstride, gradient)
         self._pending = None
+        self._run_inverse(*args)
+        self._defer_verify(lambda: self._run_inverse(*args))
+        return self
+
+    def _run_inverse(self, kd, hyp, hyp_stride, noise, noise_stride, X, x_bstride, y, y_bstride, gradient):
         lay = self.layout
         B, n, d = self.batch, self.n, self.d
         dev = self.W.device
@@ -418,6 +426,7 @@ class InverseFactorization(AugmentedFactorization):
 
     def gradient(self) -> torch.Tensor:
         """[batch, n_hyp + 1] fp64: d(-LML)/d hyp (DFS order), then d(-LML)/d noise."""
+        self._settle()
         if self.grad is None:
             raise RuntimeError("run(..., gradient=True) first")
         return self.grad

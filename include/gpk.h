@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define GPK_ABI_VERSION 5
+#define GPK_ABI_VERSION 6
 
 /* arithmetic types of the factorisation */
 enum { GPK_F64 = 0, GPK_F32 = 1 };
@@ -399,7 +399,8 @@ int gpk_timing_reset(void);
  * same bits, slower -- for A/B checks), "trd_split_m" (gpk_syevd: above this m, at most 1024, the
  * tridiagonalisation's A22 v runs over the chip, three launches per column, instead of one workgroup per
  * panel; default 1024), "chain" (every f64, batch-1, non-ragged factorisation with at most
- * "chain_max_p" (12416) rows that is not being captured runs as ONE persistent launch -- "chain_grid"
+ * "chain_max_p" (12416) rows -- identity-augmented ones (gpk_potrf_aug_ex, gpk_nlml_grad) while "chain_eye" (1) and
+ * at most "chain_max_p_eye" (16640) rows -- that is not being captured runs as ONE persistent launch -- "chain_grid"
  * workgroups (0: one per CU), every wait bounded by "chain_timeout_ms": 1, the default, auto: unless a
  * factorisation this library enqueued on another stream of the device is still in flight (each
  * persistent launch claims every CU); 2 always; 0 never), with "chain_group" panels per deferred tile update
@@ -434,6 +435,13 @@ int gpk_chain_stats(int64_t* out, int32_t n);
  * j = k + 1 -= panel k; 3: 128 x 128 tile (r, j) -= panel k), k, r, j.  Host only (no device call):
  * tasks_out may be NULL to query *ntasks; cap = its capacity in tasks. */
 int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_out, int64_t cap, int64_t* ntasks);
+/* gpk_chain_plan with flags: GPK_AUG_EXTRA_IDENTITY plans the identity-augmented factorisation (gpk_potrf_aug_ex,
+ * gpk_nlml_grad; y_row = n_pad + n): tasks that would only move the structurally zero parts of E L^-T are left
+ * out, and a task word with bit 6 set updates cells no earlier task updated (its counter wait is for 0).  The
+ * type word: type (bits 0..1) | (g - 1) << 2 (type 3: an update over the g panels k .. k + g - 1; type 2 with
+ * g > 1: the 32 x 32 quarter g - 2 of slice r in diagonal block j) | bit 6. */
+int gpk_chain_plan_ex(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, int32_t* tasks_out, int64_t cap,
+                      int64_t* ntasks);
 
 #ifdef __cplusplus
 }

@@ -36,9 +36,14 @@ def shape(n, m):
 
 def decode(task):
     """(type, k, r, j, g): BLK tasks carry ty = 3 | (g - 1) << 2 for an update over panels k .. k + g - 1; a U32
-    task with g > 1 is the quarter g - 2 (UQ) of slice r in diagonal block j; bits 8.. hold the member."""
+    task with g > 1 is the quarter g - 2 (UQ) of slice r in diagonal block j; bit 6 (first(): identity-augmented
+    lists) marks a task whose cells no earlier task updated; bits 8.. hold the member."""
     tyg, k, r, j = (int(v) for v in task)
-    return tyg & 3, k, r, j, ((tyg >> 2) & 63) + 1
+    return tyg & 3, k, r, j, ((tyg >> 2) & 15) + 1
+
+
+def first(task):
+    return (int(task[0]) >> 6) & 1
 
 
 def cells(task, nsl, uq=False):
@@ -67,6 +72,7 @@ def cells(task, nsl, uq=False):
 def waits(task, nsl, uq=False):
     """The kernel's waits (chain_kernel, dependency section): (counter, index, value >= )."""
     ty, k, r, j, g = decode(task)
+    kprev = 0 if first(task) else k   # (the count the previous update of the task's cells published)
     out = []
     if ty == D:
         if k > 0 and uq:
@@ -75,22 +81,22 @@ def waits(task, nsl, uq=False):
             out += [("ucnt", (s, k), k) for s in range(4 * k, 4 * k + 4)]
     elif ty == S:
         out.append(("dflag", k, 1))
-        if k > 0:
-            out.append(("ucnt", (r, k), k))
+        if kprev > 0:
+            out.append(("ucnt", (r, k), kprev))
     elif ty == U32:
         out.append(("sdone", (k, r), 1))
         if g > 1:
             out.append(("sdone", (k, 4 * j + g - 2), 1))
         else:
             out += [("sdone", (k, s), 1) for s in range(4 * j, 4 * j + 4) if s < nsl]
-        if k > 0:
-            out.append(("ucnt", (r, j), k))
+        if kprev > 0:
+            out.append(("ucnt", (r, j), kprev))
     else:
         q = k + g - 1
         out += [("sdone", (q, s), 1) for s in range(4 * r, 4 * r + 4) if s < nsl]
         out += [("sdone", (q, s), 1) for s in range(4 * j, 4 * j + 4) if s < nsl]
-        if k > 0:
-            out += [("ucnt", (s, j), k) for s in range(4 * r, 4 * r + 4) if s < nsl]
+        if kprev > 0:
+            out += [("ucnt", (s, j), kprev) for s in range(4 * r, 4 * r + 4) if s < nsl]
     return out
 
 
@@ -190,9 +196,9 @@ def run_tasks(W, tasks, nblk):
     return W
 
 
-def plan(n_pad, y_row, grid, group, uq=1):
+def plan(n_pad, y_row, grid, group, uq=1, eye=False):
     with nat.thread_tune(chain_group=group, chain_uq=uq):
-        return nat.chain_plan(n_pad, y_row, grid)
+        return nat.chain_plan(n_pad, y_row, grid, eye)
 
 
 def applied_panels(tasks, nblk):
@@ -216,7 +222,7 @@ def test_chain_plan_waits_cover_every_dependency(n, m, group, uq):
     for grid in (1, 3, 16, 256):
         tasks = plan(n_pad, y_row, grid, group, uq)
         kinds = np.bincount(tasks[:, 0] & 3, minlength=4)
-        nq = int(np.sum(((tasks[:, 0] & 3) == U32) & (((tasks[:, 0] >> 2) & 63) > 0)))
+        nq = int(np.sum(((tasks[:, 0] & 3) == U32) & (((tasks[:, 0] >> 2) & 15) > 0)))
         assert nq == (10 * (nblk - 1) if uq else 0)   # 1 + 2 + 3 + 4 quarters per next diagonal block
         assert kinds[D] == nblk
         assert len({tuple(t) for t in tasks.tolist()}) == len(tasks)
@@ -259,3 +265,78 @@ def test_chain_plan_rejects_bad_shapes():
         nat.chain_plan(100, 100, 8)
     with pytest.raises(nat.GpkError):
         nat.chain_plan(128, 100, 8)
+
+
+# ------------------------------------------------------------------ identity-augmented lists (gradient path)
+def eye_live(i, q, nblk, yb):
+    """Block i holds a nonzero row in panel q's columns: training blocks always, the y row's block always, extra
+    block e = i - nblk from panel e on (row n_pad + t of E L^-T is zero left of column t)."""
+    return i < nblk or i == yb or i - nblk <= q
+
+
+def augmented_eye(n, rng):
+    n_pad = -(-n // NB) * NB
+    y_row = n_pad + n
+    p = -(-(y_row + 1) // NB) * NB
+    x = np.sort(rng.uniform(0, 1, n))
+    Kn = np.exp(-0.5 * (x[:, None] - x[None, :]) ** 2 / 0.1 ** 2) + 1e-2 * np.eye(n)
+    y = np.sin(6 * x) + 0.1 * rng.standard_normal(n)
+    W = np.zeros((p, p))
+    W[:n, :n] = Kn
+    W[n:n_pad, n:n_pad] = np.eye(n_pad - n)
+    W[n_pad:n_pad + n, :n] = np.eye(n)
+    W[y_row, :n] = y
+    return np.tril(W), Kn, y, n_pad, y_row
+
+
+@pytest.mark.parametrize("n", [1, 100, 128, 300, 700, 1000, 1500])
+@pytest.mark.parametrize("group,uq", [(1, 1), (4, 1), (8, 0)])
+def test_chain_plan_eye_waits_cover_every_dependency(n, group, uq):
+    """The identity-augmented list: every live (panel, tile) update exactly once, dead ones only as zero panels
+    inside a group whose last panel is live, no panel solve of a still-zero slice, and the waits -- with the
+    first-update bit -- cover every dependency under random durations."""
+    _lib_or_skip()
+    n_pad = -(-n // NB) * NB
+    y_row = n_pad + n
+    nsl = y_row // SL + 1
+    nblk, yb = n_pad // NB, y_row // NB
+    rng = np.random.default_rng(n)
+    for grid in (1, 5, 64, 256):
+        tasks = plan(n_pad, y_row, grid, group, uq, eye=True)
+        assert len({tuple(t) for t in tasks.tolist()}) == len(tasks)
+        assert np.bincount(tasks[:, 0] & 3, minlength=4)[D] == nblk
+        for t in tasks:
+            ty, k, r, j, g = decode(t)
+            if ty == S:
+                assert eye_live(r // 4, k, nblk, yb)
+            if ty == BLK:
+                assert eye_live(r, k + g - 1, nblk, yb) and eye_live(j, k + g - 1, nblk, yb)
+        upd = applied_panels(tasks, nblk)
+        assert len(upd) == len(set(upd))
+        live = {(q, i, j) for q in range(nblk) for j in range(q + 2, yb + 1) for i in range(j, yb + 1)
+                if eye_live(i, q, nblk, yb) and eye_live(j, q, nblk, yb)}
+        assert live <= set(upd)
+        for q, i, j in set(upd) - live:
+            assert j >= q + 2 and i >= j
+        for _ in range(2):
+            simulate(tasks, nsl, grid, rng)
+
+
+@pytest.mark.parametrize("n", [200, 300, 1100])
+@pytest.mark.parametrize("group,uq", [(1, 0), (4, 1)])
+def test_chain_plan_eye_reproduces_the_inverse(n, group, uq):
+    """Run in list order on the identity-augmented matrix: L, the extra rows L^-T, the corner -K^-1 and its y row
+    -alpha^T (the layout gpk_nlml_grad reads, include/gpk.h)."""
+    _lib_or_skip()
+    rng = np.random.default_rng(11)
+    W0, Kn, y, n_pad, y_row = augmented_eye(n, rng)
+    tasks = plan(n_pad, y_row, 64, group, uq, eye=True)
+    W = run_tasks(W0.copy(), tasks, n_pad // NB)
+    L = np.linalg.cholesky(Kn)
+    np.testing.assert_allclose(np.tril(W[:n, :n]), L, rtol=0, atol=1e-12)
+    Linv = np.linalg.inv(L)
+    np.testing.assert_allclose(W[n_pad:n_pad + n, :n], Linv.T, rtol=0, atol=1e-9 * np.abs(Linv).max())
+    Kinv = np.linalg.inv(Kn)
+    got = np.tril(W[n_pad:n_pad + n, n_pad:n_pad + n])
+    np.testing.assert_allclose(got, -np.tril(Kinv), rtol=0, atol=1e-9 * np.abs(Kinv).max())
+    np.testing.assert_allclose(-W[y_row, n_pad:n_pad + n], Kinv @ y, rtol=0, atol=1e-8 * np.abs(Kinv @ y).max())

@@ -354,3 +354,68 @@ def test_run_is_asynchronous_and_verified_at_the_first_read():
     got = float(f.nlml().cpu()[0])
     assert f._pending is None
     assert got == pytest.approx(o.nlml(SE, [0.1], 1e-2, x, y), rel=1e-9)
+
+
+# ------------------------------------------------------------------ identity-augmented (gradient / inverse) path
+def _run_eye(n, chain, batch=1, seed=5, noise=1e-2):
+    x, y = o.make_inputs("C1", n=n, seed=seed)
+    dev = engine.device()
+    kd = engine.kernel_descriptor(make_kernel(SE, 1), 1)
+    H = torch.linspace(0.08, 0.12, batch, dtype=torch.float64, device=dev).reshape(batch, 1).contiguous()
+    NZ = torch.tensor([noise], dtype=torch.float64, device=dev)
+    X = torch.tensor(x, dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+    Y = torch.tensor(y, dtype=torch.float64, device=dev).reshape(1, -1).contiguous()
+    before = engine.nat.chain_stats()["launches"]
+    with engine.nat.thread_tune(chain=2 if chain else 0, chain_max_batch=8):
+        f = engine.InverseFactorization(n, 1, batch)
+        f.W.zero_()
+        f.run(kd, H, 1, NZ, 0, X, 0, Y, 0)
+        torch.cuda.synchronize()
+    assert (engine.nat.chain_stats()["launches"] > before) == bool(chain)
+    return f, (x, y)
+
+
+@pytest.mark.parametrize("n,batch", [(1, 1), (257, 1), (1000, 1), (2048, 1), (2048, 2), (4096, 1), (6144, 1),
+                                     (8192, 1)])
+def test_chain_eye_bitwise_vs_launch_path(n, batch):
+    """The identity-augmented factorisation (the value + gradient call, include/gpk.h gpk_nlml_grad) as one
+    persistent launch: its list leaves out the structurally zero tasks of E L^-T (gpk_chain_plan_ex), keeps the
+    launch path's per-tile MFMA k-order, and reproduces the launch path bit for bit -- L, L^-T, -K^-1, -alpha, the
+    -LML and the gradient."""
+    fc, _ = _run_eye(n, 1, batch)
+    fl, _ = _run_eye(n, 0, batch)
+    for b in range(batch):
+        a, c = _lower_b(fc, b), _lower_b(fl, b)
+        diff = int(np.count_nonzero(a.view(np.uint64) != c.view(np.uint64)))
+        assert diff == 0, "member %d: %d of %d lower-triangle words differ" % (b, diff, a.size)
+    assert torch.equal(fc.out.cpu(), fl.out.cpu())
+    assert torch.equal(fc.gradient().cpu(), fl.gradient().cpu())
+
+
+def test_chain_eye_matches_the_oracle():
+    from oracle import gp_autodiff as ad
+    f, (x, y) = _run_eye(3000, 1, seed=9)
+    nl, g, gn = ad.nlml_and_grad(SE, [0.08], 1e-2, x.reshape(-1, 1), y)
+    assert float(f.nlml().cpu()[0]) == pytest.approx(nl, rel=1e-9)
+    got = f.gradient()[0].cpu().numpy()
+    exp = np.array([float(np.asarray(g[0]).reshape(-1)[0]), gn])
+    assert np.max(np.abs(got - exp)) <= 1e-7 * max(1.0, np.max(np.abs(exp)))
+    Kn = o.k_noised(SE, [0.08], 1e-2, x.reshape(-1, 1))
+    Ki = np.linalg.inv(Kn)
+    assert np.linalg.norm(f.k_inv(0).cpu().numpy() - Ki) / np.linalg.norm(Ki) < 1e-8
+
+
+def test_chain_eye_timeout_falls_back():
+    """A forced timeout in the identity-augmented persistent launch: the first read (the gradient) re-runs the
+    value + gradient call on the launch path."""
+    before = engine.CHAIN_FALLBACKS
+    engine.nat.tune("chain_force_timeout", 1)
+    try:
+        f, (x, y) = _run_eye(1500, 1, seed=4)
+    finally:
+        engine.nat.tune("chain_force_timeout", 0)
+    g = f.gradient()[0].cpu().numpy()
+    assert engine.CHAIN_FALLBACKS == before + 1
+    fl, _ = _run_eye(1500, 0, seed=4)
+    assert np.array_equal(g, fl.gradient()[0].cpu().numpy())
+    assert float(f.nlml().cpu()[0]) == float(fl.nlml().cpu()[0])

@@ -3,6 +3,8 @@
 Oracle: oracle/gp_autodiff.py (torch reverse mode of the restated reference op sequence, the
 gradient tf.GradientTape takes in gpbasics/Optimizer/Fitter.py:104-158), itself pinned by finite
 differences in tests/test_grad_oracle.py.
+The oracle tests run through both single-evaluation paths (the launch path and the persistent launch, fixture
+factor_path); the schedule tests below are launch-path only (tests/conftest.py).
 Tolerances (fp64): -LML rel <= 1e-9; gradient |g - g_ref| <= 1e-7 * max(1, |g_ref|_max) per
 hyperparameter set; K^-1 / L^-1 normwise relative error <= 1e-8 (noise >= 1e-2).
 """
@@ -39,7 +41,9 @@ def _check_grad(got, exp, tol=1e-7):
 
 @pytest.mark.parametrize("case", range(len(GRAD_CASES)))
 @pytest.mark.parametrize("n", [70, 333])
-def test_gradient_matches_autodiff_oracle(case, n):
+def test_gradient_matches_autodiff_oracle(case, n, factor_path):
+    """Through both factorisation paths of a single evaluation (fixture factor_path): the launch path and the
+    persistent launch of the identity-augmented factorisation (gpk_tune chain_eye)."""
     tree, hyp, d, scaled, expanded = GRAD_CASES[case]
     set_flags(scaled=scaled, expanded=expanded)
     x, y = _inputs(n, d, 100 + case)
@@ -51,7 +55,7 @@ def test_gradient_matches_autodiff_oracle(case, n):
     _check_grad([g.cpu().numpy() for g in grads] + [float(gn)], list(g_ref) + [gn_ref])
 
 
-def test_autograd_backward_uses_device_gradient():
+def test_autograd_backward_uses_device_gradient(factor_path):
     tree, hyp = ("ADD", [("SE", {}), ("PER", {})]), [0.3, 0.9, 0.5]
     x, y = _inputs(257, 1, 7)
     h = [torch.tensor(v, dtype=torch.float64, requires_grad=True) for v in hyp]
