@@ -462,8 +462,9 @@ constexpr int kChainFirst = 1 << 6;
 std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group, int nmem, int chain_uq,
                                  bool eye = false) {
   const int nblk = (int)(n_pad / NB), yb = (int)(y_row / NB), rlast = (int)(y_row / 32);
-  // block i holds a nonzero row in the columns of panel q (monotone in q)
-  auto live = [&](int i, int q) { return !eye || i < nblk || i == yb || i - nblk <= q; };
+  // block i holds a nonzero row in the columns of panel q (monotone in q): from panel live_from(i) on
+  auto live_from = [&](int i) { return (!eye || i < nblk || i == yb) ? 0 : i - nblk; };
+  auto live = [&](int i, int q) { return live_from(i) <= q; };
   struct Task {
     int ty, k, r, j;
     float dur;
@@ -486,6 +487,8 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   // the group's last panel solve; the columns nearer the diagonal take each panel on its own (depth 128),
   // so the diagonal chain never waits for a deep update.  G = 1 disables it.
   const int G = std::max(1, std::min(group, 16));
+  const int Gc = std::max(1, std::min<int>((int)env_i64("GPK_CHAIN_GROUP_CORNER", 16), 16));
+  const int tail_c = (int)std::max<int64_t>(0, env_i64("GPK_CHAIN_CORNER_TAIL", 8));
   const int LA = (int)std::max<int64_t>(1, env_i64("GPK_CHAIN_GROUP_LA", 2));
   auto add = [&](Task t) {
     T.push_back(std::move(t));
@@ -495,6 +498,13 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   auto blk = [&](int q0, int g, int i, int jj) {
     const int ql = q0 + g - 1;  // (S(ql, r) done implies S(q, r) done for every q < ql that has an S task)
     if (!live(i, ql) || !live(jj, ql)) return;  // (identity rows: zero in every panel of the group)
+    // (identity rows: the group's leading panels in which either block is still zero are left out -- their
+    // products are exact zeros, so the tile's bits are those of the launch path, which includes or skips them)
+    const int f = std::max(live_from(i), live_from(jj));
+    if (f > q0) {
+      g -= f - q0;
+      q0 = f;
+    }
     Task t{CHT_BLK | ((g - 1) << 2), q0, i, jj, dur[3] * (0.25f + 0.75f * (float)g), {}};
     for (int s = 4 * i; s <= std::min(4 * i + 3, rlast); ++s) t.deps.push_back(s_of(ql, s));
     if (jj != i)
@@ -551,9 +561,22 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
       if (it != last_upd.end()) t.deps.push_back(it->second);
       U[(size_t)k * nr + r] = add(t);
     }
-    const int q0 = k / G * G, q1 = std::min(q0 + G, nblk);
     for (int jj = k + 2; jj <= yb; ++jj) {
-      const bool grouped = G > 1 && jj >= q1 + LA;
+      // identity-augmented lists: the corner's columns (jj >= nblk) are read by no later task -- only the
+      // read-out and the gradient use -K^-1 -- so their tiles take deeper groups (chain_group_corner)
+      // (the corner's last updates wait for the last panel solves and form the factorisation's tail: the last
+      // tail_c panels keep depth G)
+      const bool corner = eye && jj >= nblk;
+      const int qlim = corner ? std::max(0, nblk - tail_c) : 0;
+      int q0, q1;
+      if (corner && k < qlim) {
+        q0 = k / Gc * Gc;
+        q1 = std::min(q0 + Gc, qlim);
+      } else {
+        q0 = qlim + (k - qlim) / G * G;
+        q1 = std::min(q0 + G, nblk);
+      }
+      const bool grouped = q1 - q0 > 1 && jj >= q1 + LA;
       if (grouped && k != q1 - 1) continue;  // the group's one task comes with its last panel
       for (int i = jj; i <= yb; ++i) {
         if (grouped)
