@@ -452,6 +452,9 @@ int chain_group_for(int64_t knob, int64_t n_pad) {
 // kChainFirst (bit 6: the (slice, block column) cells the task updates have no earlier update -- its counter
 // wait is for 0, not for the task's first panel; identity-augmented lists only) | member << 8.
 constexpr int kChainFirst = 1 << 6;
+// bit 7 on an S task (chain_uq 2): SQ -- the panel solve of a slice of the next diagonal block followed by the
+// slice's lower quarters of that block's update (chain_sq); it publishes sdone after the solve, qdone = 1 at the end
+constexpr int kChainSq = 1 << 7;
 
 // eye: identity extra rows (m = n, gpk_potrf_aug_ex GPK_AUG_EXTRA_IDENTITY).  Extra row t (row n_pad + t) of
 // E L^-T is zero left of column t, so block i >= nblk (extra block e = i - nblk) is zero in every panel q < e
@@ -519,7 +522,7 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   // the next diagonal block's update by panel k, split by 32-column quarter (UQ: U32 with the quarter + 1 in
   // the type word's bits 2..7): 10 tasks of 32 x 32 x 128 on the chain to D(k + 1) instead of 4 of 32 x 128 x
   // 128, each loading 64 KB of panel instead of 160 (chain_uq; 0: one U32 per slice)
-  const bool uq = chain_uq != 0;
+  const bool uq = chain_uq != 0, sq = chain_uq == 2;
   std::map<int, std::vector<int>> uq_of;  // slice s of diagonal block k + 1 -> its UQ tasks (panel k)
   for (int k = 0; k < nblk; ++k) {
     Task d{CHT_D, k, 0, k, dur[0], {}};
@@ -533,15 +536,28 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
     D[k] = add(d);
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
       if (!live(r / 4, k)) continue;
-      Task t{CHT_S, k, r, 0, dur[1], {D[k]}};
+      // chain_uq 2: the next diagonal block's slices take SQ tasks -- the panel solve followed by the slice's lower
+      // quarters of that block (chain_sq), which need the siblings' solved rows (claimed before: lower slices first)
+      const bool sqt = sq && k + 1 < nblk && r < 4 * (k + 2);
+      Task t{CHT_S | (sqt ? kChainSq : 0), k, r, 0, dur[1] + (sqt ? dur[2] * 0.5f : 0.f), {D[k]}};
       if (k > 0 && live(r / 4, k - 1))
         t.deps.push_back(u_of(k - 1, r));
       else if (k > 0)
         t.ty |= kChainFirst;  // (the slice's first live panel: nothing updated it before)
+      if (sqt) {
+        auto it = last_upd.find({k + 1, k + 1});
+        if (it != last_upd.end()) t.deps.push_back(it->second);
+        for (int q = 4 * (k + 1); q < r; ++q) t.deps.push_back(s_of(k, q));
+      }
       S[(size_t)k * nr + r] = add(t);
+      if (sqt) {
+        uq_of[r].push_back(S[(size_t)k * nr + r]);
+        U[(size_t)k * nr + r] = S[(size_t)k * nr + r];
+      }
     }
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
       if (!live(r / 4, k)) continue;
+      if (sq && k + 1 < nblk && r < 4 * (k + 2)) continue;  // (done by the slice's SQ task)
       auto it = last_upd.find({r / 4, k + 1});
       const int first = (it == last_upd.end() && k > 0) ? kChainFirst : 0;
       if (uq && k + 1 < nblk && r < 4 * (k + 2)) {
@@ -724,7 +740,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.w_bs = lay->w_batch_stride;
   a.inv_bs = lay->inv_batch_stride;
   a.ctl_stride = 2 * (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
-  a.uq = tn.chain_uq != 0 ? 1 : 0;
+  a.uq = (int32_t)std::max<int64_t>(0, std::min<int64_t>(2, tn.chain_uq));
   // rows of L_kk^-1 behind D's early flag: later (more of the panel solve early) for short chains, where the
   // diagonal chain is all there is; earlier for long ones, where the S tasks' waiting CUs cost tile-update time
   // (N = 4096: 112 rows 1.501 vs 96 rows 1.515 ms; 6144 / 8192 2.42 / 4.44 vs 2.37 / 4.39, profiles/r04ab_*)

@@ -736,7 +736,9 @@ __device__ __forceinline__ void slab_stage_a(const double* A, int64_t ld, char* 
     glds16a<kLdAux>(A + (int64_t)row * ld + 2 * lane, smem + row * SLAB_LDS_ROW);
   }
 }
-template <bool SUB, bool STAGED = false, bool HALF = false>
+// KEEP (the SQ task): the result also replaces the staged A rows in LDS (C/D layout -> row-major rows of
+// SLAB_LDS_ROW bytes), behind a barrier that lets every wave finish reading A first
+template <bool SUB, bool STAGED = false, bool HALF = false, bool KEEP = false>
 __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int64_t ldb, double* C, int64_t ld,
                                           int diag_off, uint64_t* st, char* smem, HalfWait hw = HalfWait{}) {
   typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -802,6 +804,15 @@ __device__ __forceinline__ void slab_gemm(const double* A, const double* B, int6
     if (live0) sts<true>(Cr + 4 * i * ld, acc0[i]);
     if (live1) sts<true>(Cr + (16 + 4 * i) * ld, acc1[i]);
   }
+  if (KEEP) {
+    wg_sync<true>();  // (every wave's A reads done; the global stores stay in flight)
+    double* xr = reinterpret_cast<double*>(smem + q * SLAB_LDS_ROW) + cb * 16 + lr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<double*>(reinterpret_cast<char*>(xr) + 4 * i * SLAB_LDS_ROW) = acc0[i];
+      *reinterpret_cast<double*>(reinterpret_cast<char*>(xr) + (16 + 4 * i) * SLAB_LDS_ROW) = acc1[i];
+    }
+  }
 }
 
 // UQ: the 32 x 32 quarter q of slice r in the next diagonal block, C -= A B^T with A = X(r) [32 x 128] and
@@ -856,6 +867,77 @@ __device__ __forceinline__ void slab_q(const double* A, const double* B, int64_t
     double* Cr = C + (int64_t)(rb * 16 + q) * ld + cbl * 16 + lr;
 #pragma unroll
     for (int i = 0; i < 4; ++i) sts<true>(Cr + 4 * i * ld, acc[i]);
+  }
+}
+
+// SQ (chain_uq = 2), second half: slice r = 4 (k + 1) + rl of the next diagonal block, its panel-k rows X(r) in
+// LDS rows 0..31 (slab_gemm KEEP), applies panel k to its lower quarters of that block,
+//   C(r, q) -= X(r) X(4 (k + 1) + q)^T,  q = 0 .. rl   (32 x 32 x 128 each, on the diagonal one the lower half),
+// the siblings' rows X(4 (k + 1) + q), q < rl, published by the SQ tasks claimed before this one, staged by LDS-DMA
+// into LDS rows 32 (q + 1) ..  Every 16 x 16 accumulator runs slab_q's k-steps in its order (the same bits as the
+// quarter tasks UQ, the per-slice U32 and the launch path).  The 4 rl + 3 live 16 x 16 blocks are dealt to the 8
+// waves (block b to wave b % 8).  sib_ok: the siblings' rows were published (false after a timeout: no work).
+__device__ __forceinline__ void sq_quarters(double* W, int64_t ld, int k, int r, int rl, bool sib_ok, char* smem) {
+  typedef double dbl2 __attribute__((ext_vector_type(2)));
+  const int tid = opaque_tid();
+  const int lane = tid & 63;
+  const int w = wave_uniform(tid >> 6);
+  const int lr = lane & 15, lq = lane >> 4;
+  if (sib_ok) {
+    // siblings: 32 rows each, 4 rows per wave (1 KB per instruction)
+    for (int q = 0; q < rl; ++q) {
+      const double* X = W + (int64_t)(32 * (4 * (k + 1) + q)) * ld + (int64_t)k * NB;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 4 * w + i;
+        glds16a<kLdAux>(X + (int64_t)row * ld + 2 * lane, smem + (32 * (q + 1) + row) * SLAB_LDS_ROW);
+      }
+    }
+  }
+  const int nblk16 = 4 * rl + 3;
+  double* const Cq = W + (int64_t)(32 * r) * ld + (int64_t)(k + 1) * NB;
+  const __amdgpu_buffer_rsrc_t crs = uniform_rsrc(Cq);
+  const int ldc4 = __builtin_amdgcn_readfirstlane((int)(4 * ld * 8));
+  d4 acc[2];
+  int qq[2], rb[2], cbl[2];
+  bool act[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int b = w + 8 * u;
+    act[u] = sib_ok && b < nblk16;
+    // block b: quarter b / 4, position b % 4 = (rb, cbl) in (0,0), (1,0), (0,1), (1,1); the diagonal quarter
+    // (q = rl) has the three blocks (0,0), (1,0), (1,1)
+    const int q = b < 4 * rl ? b / 4 : rl;
+    const int pos = b < 4 * rl ? b % 4 : (b - 4 * rl == 2 ? 3 : b - 4 * rl);
+    qq[u] = q;
+    rb[u] = pos & 1;
+    cbl[u] = pos >> 1;
+    const int cvo = (int)(((int64_t)(rb[u] * 16 + lq) * ld + 32 * q + cbl[u] * 16 + lr) * 8);
+    acc[u] = d4{0.0, 0.0, 0.0, 0.0};
+    if (act[u]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[u][i] = ld8_buf(crs, cvo, i * ldc4);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA writes are not tracked by hipcc)
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (act[u]) {
+      const char* a0 = smem + (rb[u] * 16 + lr) * SLAB_LDS_ROW + lq * 16;
+      const int brow = (qq[u] == rl ? 0 : 32 * (qq[u] + 1)) + cbl[u] * 16 + lr;
+      const char* b0 = smem + brow * SLAB_LDS_ROW + lq * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const dbl2 x = *reinterpret_cast<const dbl2*>(a0 + j * 64);
+        const dbl2 y = *reinterpret_cast<const dbl2*>(b0 + j * 64);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[e], y[e], acc[u], 0, 0, 1);
+      }
+      double* Cr = Cq + (int64_t)(rb[u] * 16 + lq) * ld + 32 * qq[u] + cbl[u] * 16 + lr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sts<true>(Cr + 4 * i * ld, acc[u][i]);
+    }
   }
 }
 
@@ -1005,6 +1087,33 @@ GPK_CHAIN_FN void chain_s_half(double* W, int64_t ld, const double* Winv, int k,
   double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
   slab_gemm<false, true, true>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem, hw);
 }
+// SQ: the diagonal chain's panel solve S(k, r) of slice r = 4 (k + 1) + rl, whose rows stay in LDS, then -- after
+// publishing sdone[k][r] (sd_k = sdone + k nsl) and waiting for its siblings' -- its lower quarters of block k + 1
+// (sq_quarters).  hw.full etc.: the panel solve's wait for all of L_kk^-1; slot: an LDS word for the siblings' ok.
+GPK_CHAIN_FN void chain_sq(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem,
+                           HalfWait hw, int32_t* sd_k, int32_t* slot) {
+  double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
+  slab_gemm<false, true, true, true>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem, hw);
+  const int rl = r - 4 * (k + 1);
+  const int wave = wave_uniform(opaque_tid() >> 6);
+  // publish the rows (every storing wave drains its stores first), then wait for the siblings' rows
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wave == 0) {
+    st_flag(sd_k + r, 1);
+    bool ok = true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int q = 0; q < rl && ok; ++q)
+      ok = chain_wait_v(sd_k + 4 * (k + 1) + q, 1, hw.ctl, hw.info, hw.nmem, hw.timeout, hw.force_abort, t0);
+    if (ok && !kChainSc1Ld && rl > 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    slot[2] = ok ? 1 : 0;
+  }
+  __syncthreads();
+  sq_quarters(W, ld, k, r, rl, __builtin_amdgcn_readfirstlane(slot[2]) != 0, smem);
+}
 GPK_CHAIN_FN void chain_s_stage(double* W, int64_t ld, int k, int r, char* smem) {
   slab_stage_a(W + (int64_t)r * 32 * ld + (int64_t)k * NB, ld, smem);
 }
@@ -1065,9 +1174,10 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int kprev
     for (int i = 0; i < 4; ++i) {
       const int s = 4 * k + i;
       if (a.uq) {
-        // every quarter update of panel k - 1 on the block's slices (slice s has s - 4 k + 1 of them)
+        // every quarter update of panel k - 1 on the block's slices (slice s has s - 4 k + 1 of them; uq 2: one
+        // SQ task per slice sets 1 once all of its quarters are stored)
         p[i] = a.qdone + co + (int64_t)(k - 1) * a.nsl + (s < a.nsl ? s : 4 * k);
-        v[i] = s < a.nsl ? i + 1 : 0;
+        v[i] = s < a.nsl ? (a.uq == 2 ? 1 : i + 1) : 0;
       } else {
         p[i] = ucnt + (int64_t)s * a.nbc + k;
         v[i] = k;
@@ -1134,6 +1244,7 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     // BLK: updates over g panels; U32 with g > 1: the quarter g - 2 task (UQ); first: the cells the task
     // updates have no earlier update (identity-augmented lists: their counter waits are for 0); member
     const int ty = tyg & 3, g = ((tyg >> 2) & 15) + 1, first = (tyg >> 6) & 1, mem = tyg >> 8;
+    const bool sq = ty == CH_S && ((tyg >> 7) & 1);  // (chain_uq 2: S + the next block's quarters, chain_sq)
     double* const Wm = a.W + (int64_t)mem * a.w_bs;
     const int64_t co = (int64_t)mem * a.ctl_stride;
     const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
@@ -1146,9 +1257,17 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     const bool shalf = GPK_CHAIN_SHALF && spref && (r >> 2) == k + 1;  // (the S tasks on the diagonal chain)
     if (wave == 0) {
       if (a.times) a.times[6 * t] = __builtin_amdgcn_s_memrealtime();
-      const bool ok = spref ? (k == 0 || first || chain_wait(a, a.ucnt + co + (int64_t)r * a.nbc + k, k,
-                                                             __builtin_amdgcn_s_memrealtime()))
-                            : chain_deps(a, ty, first ? 0 : k, k, r, j, g, co);
+      bool ok;
+      if (sq && k > 0) {
+        // SQ: the slice's panel-k columns and its quarters' block column k + 1, both updated through panel k - 1
+        const int32_t* p[2] = {a.ucnt + co + (int64_t)r * a.nbc + k, a.ucnt + co + (int64_t)r * a.nbc + k + 1};
+        const int32_t v[2] = {k, k};
+        ok = chain_wait_set<2>(a, p, v, __builtin_amdgcn_s_memrealtime());
+      } else {
+        ok = spref ? (k == 0 || first || chain_wait(a, a.ucnt + co + (int64_t)r * a.nbc + k, k,
+                                                    __builtin_amdgcn_s_memrealtime()))
+                   : chain_deps(a, ty, first ? 0 : k, k, r, j, g, co);
+      }
       if (a.times) {
         a.times[6 * t + 1] = __builtin_amdgcn_s_memrealtime();
         if (ty == CH_D || ty == CH_BLK) a.times[6 * t + 4] = __builtin_amdgcn_s_memtime();  // shader clock
@@ -1184,6 +1303,12 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     if (ty == CH_D) {
       chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, a.dprof,
               GPK_CHAIN_SHALF ? a.hflag + co + k : nullptr, a.half_step, sm);
+    } else if (sq) {
+      chain_sq(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
+               reinterpret_cast<char*>(sm),
+               HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort,
+                        GPK_CHAIN_SHALF ? a.half_step : 0},
+               a.sdone + co + (int64_t)k * a.nsl, slot);
     } else if (shalf) {
       chain_s_half(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
                    reinterpret_cast<char*>(sm),
@@ -1214,6 +1339,8 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       if (a.times) a.times[6 * t + 3] = __builtin_amdgcn_s_memrealtime();
       if (ty == CH_D) {
         st_flag(a.dflag + co + k, 1);
+      } else if (sq) {
+        st_flag(a.qdone + co + (int64_t)k * a.nsl + r, 1);  // (its sdone went out before the quarters)
       } else if (ty == CH_S) {
         st_flag(a.sdone + co + (int64_t)k * a.nsl + r, 1);
       } else if (ty == CH_U32 && g > 1) {

@@ -46,6 +46,12 @@ def first(task):
     return (int(task[0]) >> 6) & 1
 
 
+def is_sq(task):
+    """chain_uq 2: an S task with bit 7 -- the panel solve of slice r of diagonal block k + 1 followed by the slice's
+    lower quarters of that block (publishes sdone after the solve, qdone = 1 at the end)."""
+    return (int(task[0]) & 3) == S and (int(task[0]) >> 7) & 1 == 1
+
+
 def cells(task, nsl, uq=False):
     """(reads, writes) of a task as sets of (slice, block column) cells plus ('inv', k) and, for the quarter
     updates (UQ), ('q', slice, block column, quarter)."""
@@ -58,6 +64,10 @@ def cells(task, nsl, uq=False):
         c = {(s, k) for s in sl(k)}
         qc = {("q", s, k, q) for s in sl(k) for q in range(s - 4 * k + 1)} if (uq and k > 0) else set()
         return c | qc, c | {("inv", k)}
+    if ty == S and is_sq(task):
+        rl = r - 4 * (k + 1)
+        rd = {(r, k), ("inv", k), (r, k + 1)} | {(s, k) for s in range(4 * (k + 1), r)}
+        return rd, {(r, k)} | {("q", r, k + 1, q) for q in range(rl + 1)}
     if ty == S:
         return {(r, k), ("inv", k)}, {(r, k)}
     if ty == U32 and g > 1:
@@ -75,7 +85,9 @@ def waits(task, nsl, uq=False):
     kprev = 0 if first(task) else k   # (the count the previous update of the task's cells published)
     out = []
     if ty == D:
-        if k > 0 and uq:
+        if k > 0 and uq == 2:
+            out += [("qdone", (k - 1, s), 1) for s in range(4 * k, 4 * k + 4) if s < nsl]
+        elif k > 0 and uq:
             out += [("qdone", (k - 1, s), s - 4 * k + 1) for s in range(4 * k, 4 * k + 4) if s < nsl]
         elif k > 0:
             out += [("ucnt", (s, k), k) for s in range(4 * k, 4 * k + 4)]
@@ -83,6 +95,10 @@ def waits(task, nsl, uq=False):
         out.append(("dflag", k, 1))
         if kprev > 0:
             out.append(("ucnt", (r, k), kprev))
+        if is_sq(task):
+            if k > 0:
+                out.append(("ucnt", (r, k + 1), k))
+            out += [("sdone", (k, s), 1) for s in range(4 * (k + 1), r)]
     elif ty == U32:
         out.append(("sdone", (k, r), 1))
         if g > 1:
@@ -104,6 +120,8 @@ def publishes(task, nsl):
     ty, k, r, j, g = decode(task)
     if ty == D:
         return [("dflag", k, 1)]
+    if ty == S and is_sq(task):
+        return [("sdone", (k, r), 1), ("qdone", (k, r), 1)]
     if ty == S:
         return [("sdone", (k, r), 1)]
     if ty == U32 and g > 1:
@@ -115,7 +133,7 @@ def publishes(task, nsl):
 
 def simulate(tasks, nsl, workers, rng):
     """Claim in list order; start = max(worker free, every wait's publish time); check cell versions."""
-    uq = any(decode(t)[0] == U32 and decode(t)[4] > 1 for t in tasks)
+    uq = 2 if any(is_sq(t) for t in tasks) else any(decode(t)[0] == U32 and decode(t)[4] > 1 for t in tasks)
     pub = {}           # (counter, index) -> list of (value, time); counters added to: value = "+1"
     last_w = {}        # cell -> finish time of the last earlier-claimed writer
     readers = {}       # cell -> finish times of earlier-claimed readers since that writer
@@ -183,6 +201,10 @@ def run_tasks(W, tasks, nblk):
         elif ty == S:
             R = slice(SL * r, SL * r + SL)
             W[R, K] = W[R, K] @ inv[k].T
+            if is_sq(task):
+                for q in range(r - 4 * (k + 1) + 1):
+                    Q = slice(NB * (k + 1) + SL * q, NB * (k + 1) + SL * q + SL)
+                    W[R, Q] -= W[R, K] @ W[Q, K].T
         elif ty == U32 and g > 1:
             q = g - 2
             R, Q = slice(SL * r, SL * r + SL), slice(NB * j + SL * q, NB * j + SL * q + SL)
@@ -212,7 +234,7 @@ def applied_panels(tasks, nblk):
 
 
 @pytest.mark.parametrize("n,m", [(1, 0), (128, 0), (300, 0), (700, 37), (1000, 200), (2048, 0), (3000, 0)])
-@pytest.mark.parametrize("group,uq", [(1, 1), (4, 1), (8, 1), (4, 0)])
+@pytest.mark.parametrize("group,uq", [(1, 1), (4, 1), (8, 1), (4, 0), (4, 2), (1, 2)])
 def test_chain_plan_waits_cover_every_dependency(n, m, group, uq):
     _lib_or_skip()
     n_pad, y_row, p = shape(n, m)
@@ -223,7 +245,8 @@ def test_chain_plan_waits_cover_every_dependency(n, m, group, uq):
         tasks = plan(n_pad, y_row, grid, group, uq)
         kinds = np.bincount(tasks[:, 0] & 3, minlength=4)
         nq = int(np.sum(((tasks[:, 0] & 3) == U32) & (((tasks[:, 0] >> 2) & 15) > 0)))
-        assert nq == (10 * (nblk - 1) if uq else 0)   # 1 + 2 + 3 + 4 quarters per next diagonal block
+        assert nq == (10 * (nblk - 1) if uq == 1 else 0)   # 1 + 2 + 3 + 4 quarters per next diagonal block
+        assert sum(is_sq(t) for t in tasks) == (4 * (nblk - 1) if uq == 2 else 0)
         assert kinds[D] == nblk
         assert len({tuple(t) for t in tasks.tolist()}) == len(tasks)
         upd = applied_panels(tasks, nblk)
@@ -236,7 +259,7 @@ def test_chain_plan_waits_cover_every_dependency(n, m, group, uq):
 
 
 @pytest.mark.parametrize("n,m", [(200, 0), (600, 50), (1100, 0), (2100, 40)])
-@pytest.mark.parametrize("group,uq", [(1, 0), (4, 1)])
+@pytest.mark.parametrize("group,uq", [(1, 0), (4, 1), (4, 2)])
 def test_chain_plan_reproduces_the_blocked_factorisation(n, m, group, uq):
     _lib_or_skip()
     rng = np.random.default_rng(7)
@@ -290,7 +313,7 @@ def augmented_eye(n, rng):
 
 
 @pytest.mark.parametrize("n", [1, 100, 128, 300, 700, 1000, 1500])
-@pytest.mark.parametrize("group,uq", [(1, 1), (4, 1), (8, 0)])
+@pytest.mark.parametrize("group,uq", [(1, 1), (4, 1), (8, 0), (4, 2)])
 def test_chain_plan_eye_waits_cover_every_dependency(n, group, uq):
     """The identity-augmented list: every live (panel, tile) update exactly once, dead ones only as zero panels
     inside a group whose last panel is live, no panel solve of a still-zero slice, and the waits -- with the
@@ -323,7 +346,7 @@ def test_chain_plan_eye_waits_cover_every_dependency(n, group, uq):
 
 
 @pytest.mark.parametrize("n", [200, 300, 1100])
-@pytest.mark.parametrize("group,uq", [(1, 0), (4, 1)])
+@pytest.mark.parametrize("group,uq", [(1, 0), (4, 1), (4, 2)])
 def test_chain_plan_eye_reproduces_the_inverse(n, group, uq):
     """Run in list order on the identity-augmented matrix: L, the extra rows L^-T, the corner -K^-1 and its y row
     -alpha^T (the layout gpk_nlml_grad reads, include/gpk.h)."""

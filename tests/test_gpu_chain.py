@@ -82,11 +82,12 @@ def test_chain_bitwise_vs_launch_path(n, m):
     assert fc.out.cpu()[0].item() == fl.out.cpu()[0].item()
 
 
-@pytest.mark.parametrize("group,uq", [(1, 0), (1, 1), (4, 0), (8, 1)])
+@pytest.mark.parametrize("group,uq", [(1, 0), (1, 1), (4, 0), (8, 1), (4, 2), (1, 2)])
 @pytest.mark.parametrize("n,m", [(2100, 40), (5000, 0)])
 def test_chain_plan_variants_bitwise_vs_launch_path(n, m, group, uq):
-    """Every planner variant (deferred-update depth chain_group, the next diagonal block's update as quarter tasks or
-    one task per slice) reproduces the launch path bit for bit: the same per-tile MFMA k-order in every variant."""
+    """Every planner variant (deferred-update depth chain_group, the next diagonal block's update as quarter tasks,
+    one task per slice, or inside the slices' panel-solve tasks (SQ, chain_uq 2)) reproduces the launch path bit for
+    bit: the same per-tile MFMA k-order in every variant."""
     with engine.nat.thread_tune(chain_group=group, chain_uq=uq):
         before = engine.nat.chain_stats()["launches"]
         fc, _ = _run(n, m, 1)
@@ -419,3 +420,23 @@ def test_chain_eye_timeout_falls_back():
     fl, _ = _run_eye(1500, 0, seed=4)
     assert np.array_equal(g, fl.gradient()[0].cpu().numpy())
     assert float(f.nlml().cpu()[0]) == float(fl.nlml().cpu()[0])
+
+
+@pytest.mark.parametrize("n", [700, 4096, 8192])
+def test_chain_sq_eye_and_timeout(n):
+    """SQ tasks (chain_uq 2) in the identity-augmented list, bitwise against the launch path; and a forced timeout of
+    an SQ launch recovers on the launch path."""
+    with engine.nat.thread_tune(chain_uq=2):
+        fc, _ = _run_eye(n, 1)
+    fl, _ = _run_eye(n, 0)
+    a, c = _lower_b(fc, 0), _lower_b(fl, 0)
+    assert int(np.count_nonzero(a.view(np.uint64) != c.view(np.uint64))) == 0
+    assert torch.equal(fc.gradient().cpu(), fl.gradient().cpu())
+    if n == 700:
+        engine.nat.tune("chain_force_timeout", 1)
+        try:
+            with engine.nat.thread_tune(chain_uq=2):
+                f, (x, y) = _run(n, 0, 1)
+        finally:
+            engine.nat.tune("chain_force_timeout", 0)
+        assert float(f.nlml().cpu()[0]) == pytest.approx(o.nlml(SE, [0.1], 1e-2, x, y), rel=1e-9)

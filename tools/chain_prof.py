@@ -33,7 +33,8 @@ for _ in range(3):
 torch.cuda.synchronize()
 lay = f.layout
 tasks = nat.chain_plan(lay.n_pad, lay.y_row, grid if grid > 0 else torch.cuda.get_device_properties(0).multi_processor_count)
-gsz = (tasks[:, 0] >> 2) + 1   # BLK over g panels
+tyraw = tasks[:, 0].copy()
+gsz = ((tyraw >> 2) & 15) + 1   # BLK over g panels
 tasks = tasks.copy()
 tasks[:, 0] &= 3
 nt = len(tasks)
@@ -117,3 +118,19 @@ if rows:
     r = np.array(rows).mean(axis=0)
     print("mean over %d steps: D %.1f | ->S %.1f (late claim %.1f) | S %.1f | ->U %.1f (late %.1f) | U %.1f | "
           "->D %.1f (late %.1f) | step %.1f us" % ((len(rows),) + tuple(r)), flush=True)
+
+# chain_uq 2 (SQ tasks: S type with bit 7): D(k) | -> SQ ready | SQ run | -> D(k + 1) ready
+sqm = ((tyraw & 3) == 1) & (((tyraw >> 7) & 1) == 1)
+if sqm.any():
+    rows = []
+    for k in range(1, len(d) - 1):
+        i_d, i_d1 = d[k], d[k + 1]
+        sl = np.where(sqm & (tasks[:, 1] == k))[0]
+        if len(sl) == 0:
+            continue
+        s_rdy, s_done = max(T[sl, 1]), max(T[sl, 3])
+        rows.append((T[i_d, 3] - T[i_d, 1], s_rdy - T[i_d, 3], s_done - s_rdy, T[i_d1, 1] - s_done,
+                     max(0.0, T[i_d1, 0] - s_done), T[i_d1, 1] - T[i_d, 1]))
+    r = np.array(rows).mean(axis=0)
+    print("SQ mean over %d steps: D %.1f | ->SQ %.1f | SQ %.1f | ->D %.1f (late %.1f) | step %.1f us" % (
+        (len(rows),) + tuple(r)), flush=True)
