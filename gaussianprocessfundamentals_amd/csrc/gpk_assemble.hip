@@ -86,6 +86,9 @@ __device__ __forceinline__ void stage_points(const gpk_kdesc& kd, const AsmArgs&
 #ifndef GPK_ASM_INTERIOR_TREE
 #define GPK_ASM_INTERIOR_TREE 1  // trees of base nodes on the interior path too
 #endif
+#ifndef GPK_ASM_PAIR_MFMA
+#define GPK_ASM_PAIR_MFMA 1  // two-leaf SE + periodic trees on f64 MFMA (pair_mfma_tile; 0: the VALU form, A/B)
+#endif
 #ifndef GPK_ASM_INTERIOR
 #define GPK_ASM_INTERIOR 1  // 0: every tile through the generic loop (A/B)
 #endif
@@ -255,6 +258,121 @@ __device__ __forceinline__ void interior_pair(const gpk_kdesc& kd, const FastNod
   }
 }
 
+// ------------------------------------------------------------------ two-leaf SE + periodic trees on f64 MFMA
+// SURVEY C5's ADD(SE-ARD, PER standard): the per-dimension sums of both leaves are dot products of per-point
+// features, so a tile's 64 x 64 of them are f64 MFMA tiles and only the two exps and a few FMAs per element
+// stay on the VALU (the VALU form: 150 instructions per element, VALU-issue-bound at 0.94 ms for C5):
+//   SE   ||u_a - u_b||^2 = |u_a|^2 + |u_b|^2 - 2 u_a . u_b                 (u: the leaf's ARD slot or raw points;
+//        the reference's expanded norm, Auxiliary/Distances.py:4-7, clamped at 0 as the direct sum never goes
+//        negative)
+//   PER  sum_k sin^2(pi (u_ak - u_bk)) = D / 2 - 1/2 sum_k (C_ak C_bk + S_ak S_bk),  C = cos 2 pi f, S = sin 2 pi f,
+//        from the staged sin(pi f), cos(pi f) (f = u - rint(u), u = x / p): C = 1 - 2 s^2, S = 2 s c
+// A point's value against itself (i == j in one point set) takes distance 0 exactly (k(x, x) = sg).  Both forms
+// cancel for close points: |d(r^2)| <~ 4 eps (|u_a|^2 + |u_b|^2) and |d(sn)| <~ 2 D eps, relative errors in K of
+// half and 2 / l^2 times that.  A tile takes this path only where those stay <~ 1e-13 (kernel-matrix tests: rel
+// 1e-12): max |u|^2 of its rows + of its columns <= 512, and D / l_per^2 <= 128, D >= 4 (pair_mfma_ok); other tiles
+// keep the VALU form (per tile, like the sin / cos form itself; the decision is symmetric in rows and columns).
+constexpr double PAIR_MFMA_MAX_NORM = 512.0;
+constexpr double PAIR_MFMA_MAX_DIL2 = 128.0;
+
+// per-point feature k of the periodic leaf: C_k (k < D), S_{k - D} (k < 2 D), else 0
+__device__ __forceinline__ double per_feature(const double* pts, int pt, int k, int D, int dp, int sc_sin, int sc_cos) {
+#pragma clang fp contract(on)
+  if (k < D) {
+    const double sv = pts[sc_sin + pt * dp + k];
+    return fma(-2.0 * sv, sv, 1.0);
+  }
+  if (k < 2 * D) {
+    const double sv = pts[sc_sin + pt * dp + k - D], cv = pts[sc_cos + pt * dp + k - D];
+    return 2.0 * (sv * cv);
+  }
+  return 0.0;
+}
+
+// wave w: rows 16 w .. 16 w + 15 of the tile against its 64 columns (four 16 x 16 MFMA blocks), then the per-element
+// read-out with the generic loop's classes (so edge tiles, test rows and ragged members take the same values).
+template <typename TOut>
+__device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArgs& a, const FastNode* fns, int se_leaf,
+                                               const double* prow, const double* pcol, int sc_sin, int sc_cos,
+                                               const double* na_r, const double* na_c, int64_t gi0, int64_t gj0,
+                                               int b, TOut* W) {
+#pragma clang fp contract(on)
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, kq = lane >> 4;
+  const int D = a.d, dp = a.dp;
+  const FastNode fs = fns[se_leaf], fq = fns[1 - se_leaf];
+  d4 dse[4], dpe[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    dse[cb] = d4{0.0, 0.0, 0.0, 0.0};
+    dpe[cb] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  for (int s = 0; 4 * s < D; ++s) {
+    const int k = 4 * s + kq;
+    const double av = k < D ? prow[fs.off + (16 * w + lr) * dp + k] : 0.0;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const double bv = k < D ? pcol[fs.off + (16 * cb + lr) * dp + k] : 0.0;
+      dse[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, dse[cb], 0, 0, 0);
+    }
+  }
+  for (int s = 0; 4 * s < 2 * D; ++s) {
+    const int k = 4 * s + kq;
+    const double av = per_feature(prow, 16 * w + lr, k, D, dp, sc_sin, sc_cos);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const double bv = per_feature(pcol, 16 * cb + lr, k, D, dp, sc_sin, sc_cos);
+      dpe[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, dpe[cb], 0, 0, 0);
+    }
+  }
+  const bool mul = kd.nodes[2].op == GPK_OP_MUL;
+  const bool same_set = !a.plain || a.X == a.Xs;  // (row i and column i are one point)
+  const double halfd = 0.5 * (double)D;
+  const double noise = a.plain ? 0.0 : a.noise[(int64_t)b * a.noise_stride];
+  const int64_t nm = a.plain ? a.n : member_n(a, b), mm = a.plain ? a.m : member_m(a, b);
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int col = 16 * cb + lr;
+    const int64_t gj = gj0 + col;
+    const int ccls = a.plain ? CLS_TRAIN : classify(a, gj, nm, mm);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 16 * w + kq + 4 * i;
+      const int64_t gi = gi0 + row;
+      const bool same = same_set && gi == gj;
+      double r2 = fma(-2.0, dse[cb][i], na_r[row] + na_c[col]);
+      double sn = fma(-0.5, dpe[cb][i], halfd);
+      r2 = same ? 0.0 : fmax(r2, 0.0);
+      sn = same ? 0.0 : fmax(sn, 0.0);
+      const double vse = fs.sg * exp(-0.5 * (r2 * fs.il2));
+      const double vper = fq.sg * exp((-2.0 * sn) * fq.il2);
+      const double v0 = se_leaf == 0 ? vse : vper, v1 = se_leaf == 0 ? vper : vse;
+      double v = mul ? v0 * v1 : v0 + v1;
+      if (a.plain) {
+        if (gi >= a.n || gj >= a.m || (a.uplo && gj > gi)) continue;
+        if (gi == gj) v += a.diag_add;
+      } else {
+        const int rcls = classify(a, gi, nm, mm);
+        if (rcls == CLS_PAD || ccls == CLS_PAD) {
+          v = (gi == gj) ? 1.0 : 0.0;
+        } else if (a.eye && rcls == CLS_TEST) {
+          v = (ccls == CLS_TRAIN && gj == gi - a.n_pad) ? 1.0 : 0.0;
+        } else if (a.E != nullptr && rcls == CLS_TEST) {
+          v = (ccls == CLS_TRAIN) ? a.E[(int64_t)b * a.e_bs + (gi - a.n_pad) * a.n + gj] : 0.0;
+        } else if ((rcls == CLS_TRAIN || rcls == CLS_TEST) && (ccls == CLS_TRAIN || ccls == CLS_TEST)) {
+          if (rcls == CLS_TRAIN && ccls == CLS_TRAIN && gi == gj) v += noise;
+        } else if (rcls == CLS_Y && ccls == CLS_TRAIN) {
+          v = a.y[(int64_t)b * a.y_bs + gj];
+        } else {
+          v = 0.0;
+        }
+      }
+      W[gi * a.ld + gj] = (TOut)v;
+    }
+  }
+}
+
 // TREE: 0 single base node, 1 general tree, 2 two-leaf tree (interior_pair)
 template <typename TOut, int D, int TREE>
 __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& fn, const FastNode* fns, bool fast,
@@ -290,6 +408,7 @@ template <typename TOut, int TREE>
 __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int sc_flag;
+  __shared__ unsigned long long pair_max[2];  // (TREE 2) max |u|^2 of the tile's row / column points, as bits
   const int slot_stride = ATILE * a.dp;
   // slots per tile edge: raw points, one per ARD node, and (periodic node through sin / cos) sin, cos
   const int scq = a.A == nullptr ? sc_node(kd) : -1;
@@ -325,7 +444,10 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   const int tid = threadIdx.x;
   const double* hyp_g = a.hyp + (int64_t)b * a.hyp_stride;
   for (int e = tid; e < kd.n_hyp; e += 256) hyp_s[e] = hyp_g[e];
-  if (tid == 0) sc_flag = 1;
+  if (tid == 0) {
+    sc_flag = 1;
+    pair_max[0] = pair_max[1] = 0ull;
+  }
   __syncthreads();
   // per-node constants of a tree (reciprocals of the hyperparameters; single nodes keep theirs in
   // registers below)
@@ -353,6 +475,37 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   __syncthreads();
   // the sin / cos form for this tile: every staged point within |x / p| <= SC_MAX_U (workgroup-uniform)
   const bool sc_on = scq >= 0 && sc_flag != 0;
+  if (TREE == 2 && GPK_ASM_PAIR_MFMA && sc_on && a.A == nullptr && a.d >= 4 && !GPK_ASM_ABLATE) {
+    // two-leaf SE + periodic tree: the tile on f64 MFMA (pair_mfma_tile) when its error bounds hold
+    const gpk_node n0 = kd.nodes[0], n1 = kd.nodes[1];
+    const bool se0 = n0.op == GPK_OP_SE && !(n0.flags & GPK_NODE_SE_EXPANDED);
+    const bool se1 = n1.op == GPK_OP_SE && !(n1.flags & GPK_NODE_SE_EXPANDED);
+    const int se_leaf = (se0 && n1.op == GPK_OP_PER) ? 0 : ((se1 && n0.op == GPK_OP_PER) ? 1 : -1);
+    if (se_leaf >= 0 && fns[1 - se_leaf].sc && (double)a.d * fns[1 - se_leaf].il2 <= PAIR_MFMA_MAX_DIL2) {
+      double* na_r = reinterpret_cast<double*>(fns + GPK_MAX_NODES);
+      double* na_c = na_r + ATILE;
+      const FastNode fs = fns[se_leaf];
+      if (tid < 2 * ATILE) {
+        const double* pts = tid < ATILE ? prow : pcol;
+        const int pt = tid & (ATILE - 1);
+        double nrm = 0.0;
+        for (int k = 0; k < a.d; ++k) {
+          const double u = pts[fs.off + pt * a.dp + k];
+          nrm = fma(u, u, nrm);
+        }
+        (tid < ATILE ? na_r : na_c)[pt] = nrm;
+        atomicMax(&pair_max[tid < ATILE ? 0 : 1], (unsigned long long)__double_as_longlong(nrm));
+      }
+      __syncthreads();
+      const double bound = (__longlong_as_double((long long)pair_max[0]) + __longlong_as_double((long long)pair_max[1])) *
+                           fs.il2;
+      if (bound <= PAIR_MFMA_MAX_NORM) {
+        pair_mfma_tile<TOut>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b,
+                             reinterpret_cast<TOut*>(a.W) + (int64_t)b * a.w_bs);
+        return;
+      }
+    }
+  }
 
   const int c = tid & 63;
   const int r0 = tid >> 6;
@@ -997,7 +1150,7 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
                            hipStream_t s) {
   const int nslot = 1 + kd.n_ard + ((a.A == nullptr && sc_node(kd) >= 0) ? 2 : 0);
   const size_t lds = sizeof(double) * (GPK_MAX_HYP + 2 * (size_t)nslot * ATILE * a.dp) +
-                     sizeof(FastNode) * GPK_MAX_NODES;
+                     sizeof(FastNode) * GPK_MAX_NODES + sizeof(double) * 2 * ATILE;  // (+ pair_mfma_tile's norms)
   dim3 grid;
   if (a.plain) {
     const int64_t tr = (a.n + ATILE - 1) / ATILE, tc = (a.m + ATILE - 1) / ATILE;
