@@ -289,8 +289,10 @@ __device__ __forceinline__ double per_feature(const double* pts, int pt, int k, 
   return 0.0;
 }
 
-// wave w: rows 16 w .. 16 w + 15 of the tile against its 64 columns (four 16 x 16 MFMA blocks), then the per-element
-// read-out with the generic loop's classes (so edge tiles, test rows and ragged members take the same values).
+// wave w: rows 16 w .. 16 w + 15 of the tile against its 64 columns, one 16 x 16 MFMA block at a time (two f64
+// accumulators live: the path must not raise the kernel's VGPR count -- its VALU form shares the instantiation),
+// then the per-element read-out; interior tiles (every row and column a training point) skip the generic loop's
+// classes, edge tiles, test rows and ragged members take them (same values as the generic loop).
 template <typename TOut>
 __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArgs& a, const FastNode* fns, int se_leaf,
                                                const double* prow, const double* pcol, int sc_sin, int sc_cos,
@@ -302,54 +304,51 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
   const int lr = lane & 15, kq = lane >> 4;
   const int D = a.d, dp = a.dp;
   const FastNode fs = fns[se_leaf], fq = fns[1 - se_leaf];
-  d4 dse[4], dpe[4];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    dse[cb] = d4{0.0, 0.0, 0.0, 0.0};
-    dpe[cb] = d4{0.0, 0.0, 0.0, 0.0};
-  }
-  for (int s = 0; 4 * s < D; ++s) {
-    const int k = 4 * s + kq;
-    const double av = k < D ? prow[fs.off + (16 * w + lr) * dp + k] : 0.0;
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const double bv = k < D ? pcol[fs.off + (16 * cb + lr) * dp + k] : 0.0;
-      dse[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, dse[cb], 0, 0, 0);
-    }
-  }
-  for (int s = 0; 4 * s < 2 * D; ++s) {
-    const int k = 4 * s + kq;
-    const double av = per_feature(prow, 16 * w + lr, k, D, dp, sc_sin, sc_cos);
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const double bv = per_feature(pcol, 16 * cb + lr, k, D, dp, sc_sin, sc_cos);
-      dpe[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, dpe[cb], 0, 0, 0);
-    }
-  }
   const bool mul = kd.nodes[2].op == GPK_OP_MUL;
   const bool same_set = !a.plain || a.X == a.Xs;  // (row i and column i are one point)
   const double halfd = 0.5 * (double)D;
   const double noise = a.plain ? 0.0 : a.noise[(int64_t)b * a.noise_stride];
   const int64_t nm = a.plain ? a.n : member_n(a, b), mm = a.plain ? a.m : member_m(a, b);
+  const bool interior = !a.plain && gi0 + ATILE <= nm && gj0 + ATILE <= nm;
+  TOut* const Wt = W + gi0 * a.ld + gj0;
+  double nrow[4];
 #pragma unroll
+  for (int i = 0; i < 4; ++i) nrow[i] = na_r[16 * w + kq + 4 * i];
+#pragma unroll 1
   for (int cb = 0; cb < 4; ++cb) {
+    d4 dse = {0.0, 0.0, 0.0, 0.0}, dpe = {0.0, 0.0, 0.0, 0.0};
+    for (int s = 0; 4 * s < D; ++s) {
+      const int k = 4 * s + kq;
+      const double av = k < D ? prow[fs.off + (16 * w + lr) * dp + k] : 0.0;
+      const double bv = k < D ? pcol[fs.off + (16 * cb + lr) * dp + k] : 0.0;
+      dse = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, dse, 0, 0, 0);
+    }
+    for (int s = 0; 4 * s < 2 * D; ++s) {
+      const int k = 4 * s + kq;
+      const double av = per_feature(prow, 16 * w + lr, k, D, dp, sc_sin, sc_cos);
+      const double bv = per_feature(pcol, 16 * cb + lr, k, D, dp, sc_sin, sc_cos);
+      dpe = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, dpe, 0, 0, 0);
+    }
     const int col = 16 * cb + lr;
     const int64_t gj = gj0 + col;
-    const int ccls = a.plain ? CLS_TRAIN : classify(a, gj, nm, mm);
+    const double ncol = na_c[col];
+    const int ccls = (a.plain || interior) ? CLS_TRAIN : classify(a, gj, nm, mm);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = 16 * w + kq + 4 * i;
       const int64_t gi = gi0 + row;
       const bool same = same_set && gi == gj;
-      double r2 = fma(-2.0, dse[cb][i], na_r[row] + na_c[col]);
-      double sn = fma(-0.5, dpe[cb][i], halfd);
+      double r2 = fma(-2.0, dse[i], nrow[i] + ncol);
+      double sn = fma(-0.5, dpe[i], halfd);
       r2 = same ? 0.0 : fmax(r2, 0.0);
       sn = same ? 0.0 : fmax(sn, 0.0);
       const double vse = fs.sg * exp(-0.5 * (r2 * fs.il2));
       const double vper = fq.sg * exp((-2.0 * sn) * fq.il2);
       const double v0 = se_leaf == 0 ? vse : vper, v1 = se_leaf == 0 ? vper : vse;
       double v = mul ? v0 * v1 : v0 + v1;
-      if (a.plain) {
+      if (interior) {
+        if (gi == gj) v += noise;
+      } else if (a.plain) {
         if (gi >= a.n || gj >= a.m || (a.uplo && gj > gi)) continue;
         if (gi == gj) v += a.diag_add;
       } else {
@@ -368,7 +367,7 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
           v = 0.0;
         }
       }
-      W[gi * a.ld + gj] = (TOut)v;
+      Wt[(int64_t)row * a.ld + col] = (TOut)v;
     }
   }
 }
@@ -403,7 +402,9 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
 
 
 // TREE: the instantiation for kernel trees (its interior loop holds two column points in registers;
-// single-node kernels get the lighter instantiation and keep four waves per SIMD)
+// single-node kernels get the lighter instantiation and keep four waves per SIMD); 3: two-leaf SE + periodic trees
+// on MFMA (pair_mfma_tile), tiles outside its error bounds through the generic loop -- an instantiation of its own,
+// so that neither path's registers limit the other's occupancy
 template <typename TOut, int TREE>
 __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -475,7 +476,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   __syncthreads();
   // the sin / cos form for this tile: every staged point within |x / p| <= SC_MAX_U (workgroup-uniform)
   const bool sc_on = scq >= 0 && sc_flag != 0;
-  if (TREE == 2 && GPK_ASM_PAIR_MFMA && sc_on && a.A == nullptr && a.d >= 4 && !GPK_ASM_ABLATE) {
+  if (TREE == 3 && sc_on && a.A == nullptr && a.d >= 4 && !GPK_ASM_ABLATE) {
     // two-leaf SE + periodic tree: the tile on f64 MFMA (pair_mfma_tile) when its error bounds hold
     const gpk_node n0 = kd.nodes[0], n1 = kd.nodes[1];
     const bool se0 = n0.op == GPK_OP_SE && !(n0.flags & GPK_NODE_SE_EXPANDED);
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
   fn.sc = scq == 0 ? 1 : 0;
   fn.sc_sin = sc_sin;
   fn.sc_cos = sc_cos;
-  if (GPK_ASM_INTERIOR && !a.generic && a.A == nullptr && gi0 + ATILE <= nm) {  // lower tiles: gj0 <= gi0
+  if (TREE != 3 && GPK_ASM_INTERIOR && !a.generic && a.A == nullptr && gi0 + ATILE <= nm) {  // lower tiles: gj0 <= gi0
     bool done = false;
     switch (a.d) {
       case 1: done = interior_d<TOut, 1, TREE>(kd, fn, fns, fast, prow, pcol, slot_stride, a.dp, c, r0, gi0, gj, noise, W, a.ld, sc_sin, sc_cos, sc_on); break;
@@ -1161,14 +1162,21 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
   } else {
     grid = dim3((unsigned)(a.ntile * (a.ntile + 1) / 2), (unsigned)batch, 1);
   }
-  // instantiation: 0 single base node, 2 two leaves under one ADD / MUL, 1 any other tree
+  // instantiation: 0 single base node, 2 two leaves under one ADD / MUL, 3 the two leaves SE (direct norm) and a
+  // separable periodic node at D >= 4 (pair_mfma_tile), 1 any other tree
   const bool pair = kd.n_nodes == 3 && (kd.nodes[2].op == GPK_OP_ADD || kd.nodes[2].op == GPK_OP_MUL);
-  const int tree = kd.n_nodes == 1 ? 0 : (pair && !tune_pair_off() ? 2 : 1);
+  int tree = kd.n_nodes == 1 ? 0 : (pair && !tune_pair_off() ? 2 : 1);
+  if (tree == 2 && GPK_ASM_PAIR_MFMA && a.A == nullptr && a.d >= 4 && dtype == GPK_F64) {
+    const int q = sc_node(kd);
+    const gpk_node se = kd.nodes[q == 0 ? 1 : 0];
+    if ((q == 0 || q == 1) && se.op == GPK_OP_SE && !(se.flags & GPK_NODE_SE_EXPANDED)) tree = 3;
+  }
   // (above 64 KB -- e.g. an ARD node beside a standard PER node, whose per-point sin / cos take two more point
   // slots, at d = 16: 71 KB; two ARD nodes: 87 KB -- the kernel's dynamic-LDS limit must be raised first)
   {
     const void* fn = dtype == GPK_F64
-                         ? (tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<double, 2>)
+                         ? (tree == 3 ? reinterpret_cast<const void*>(assemble_kernel<double, 3>)
+                            : tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<double, 2>)
                                       : tree == 1 ? reinterpret_cast<const void*>(assemble_kernel<double, 1>)
                                                   : reinterpret_cast<const void*>(assemble_kernel<double, 0>))
                          : (tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<float, 2>)
@@ -1178,7 +1186,9 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
     if (e != hipSuccess) return e;
   }
   if (dtype == GPK_F64) {
-    if (tree == 2)
+    if (tree == 3)
+      hipLaunchKernelGGL((assemble_kernel<double, 3>), grid, dim3(256), lds, s, kd, a);
+    else if (tree == 2)
       hipLaunchKernelGGL((assemble_kernel<double, 2>), grid, dim3(256), lds, s, kd, a);
     else if (tree == 1)
       hipLaunchKernelGGL((assemble_kernel<double, 1>), grid, dim3(256), lds, s, kd, a);
