@@ -270,43 +270,52 @@ __device__ __forceinline__ void interior_pair(const gpk_kdesc& kd, const FastNod
 // A point's value against itself (i == j in one point set) takes distance 0 exactly (k(x, x) = sg).  Both forms
 // cancel for close points: |d(r^2)| <~ 4 eps (|u_a|^2 + |u_b|^2) and |d(sn)| <~ 2 D eps, relative errors in K of
 // half and 2 / l^2 times that.  A tile takes this path only where those stay <~ 1e-13 (kernel-matrix tests: rel
-// 1e-12): max |u|^2 of its rows + of its columns <= 512, and D / l_per^2 <= 128, D >= 4 (pair_mfma_ok); other tiles
+// 1e-12): max |u|^2 of its rows + of its columns <= 512, and D / l_per^2 <= 128, D in {4, 8, 12, 16}; other tiles
 // keep the VALU form (per tile, like the sin / cos form itself; the decision is symmetric in rows and columns).
 constexpr double PAIR_MFMA_MAX_NORM = 512.0;
 constexpr double PAIR_MFMA_MAX_DIL2 = 128.0;
 
-// per-point feature k of the periodic leaf: C_k (k < D), S_{k - D} (k < 2 D), else 0
-__device__ __forceinline__ double per_feature(const double* pts, int pt, int k, int D, int dp, int sc_sin, int sc_cos) {
+// per-point feature k0 + kq of the periodic leaf: C_k (k < D), S_{k - D} (k < 2 D); k0 a multiple of 4 (inside the
+// unrolled k-step loops a constant, so the branch folds)
+template <int D>
+__device__ __forceinline__ double per_feature(const double* pts, int pt, int k0, int kq, int dp, int sc_sin, int sc_cos) {
 #pragma clang fp contract(on)
-  if (k < D) {
-    const double sv = pts[sc_sin + pt * dp + k];
+  if (k0 < D) {
+    const double sv = pts[sc_sin + pt * dp + k0 + kq];
     return fma(-2.0 * sv, sv, 1.0);
   }
-  if (k < 2 * D) {
-    const double sv = pts[sc_sin + pt * dp + k - D], cv = pts[sc_cos + pt * dp + k - D];
-    return 2.0 * (sv * cv);
-  }
-  return 0.0;
+  const double sv = pts[sc_sin + pt * dp + k0 - D + kq], cv = pts[sc_cos + pt * dp + k0 - D + kq];
+  return 2.0 * (sv * cv);
 }
 
-// wave w: rows 16 w .. 16 w + 15 of the tile against its 64 columns, one 16 x 16 MFMA block at a time (two f64
-// accumulators live: the path must not raise the kernel's VGPR count -- its VALU form shares the instantiation),
-// then the per-element read-out; interior tiles (every row and column a training point) skip the generic loop's
-// classes, edge tiles, test rows and ragged members take them (same values as the generic loop).
-template <typename TOut>
+// wave w: rows 16 w .. 16 w + 15 of the tile against its 64 columns (four 16 x 16 MFMA blocks, their k-steps
+// interleaved: 4 independent accumulator chains per leaf), then the per-element read-out; interior tiles (every row
+// and column a training point) skip the generic loop's classes, edge tiles, test rows and ragged members take them
+// (the same values as the generic loop).  D a multiple of 4 (compile-time: the k-steps are whole).
+template <typename TOut, int D>
 __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArgs& a, const FastNode* fns, int se_leaf,
                                                const double* prow, const double* pcol, int sc_sin, int sc_cos,
                                                const double* na_r, const double* na_c, int64_t gi0, int64_t gj0,
                                                int b, TOut* W) {
 #pragma clang fp contract(on)
+  static_assert(D % 4 == 0, "whole k-steps");
+  constexpr int SS = D / 4, PS = 2 * D / 4;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, kq = lane >> 4;
-  const int D = a.d, dp = a.dp;
+  const int dp = a.dp;
   const FastNode fs = fns[se_leaf], fq = fns[1 - se_leaf];
+  // the row operands (this wave's 16 rows) once; the column operands per block
+  double ase[SS], ape[PS];
+  const int prow_pt = 16 * w + lr;
+#pragma unroll
+  for (int t = 0; t < SS; ++t) ase[t] = prow[fs.off + prow_pt * dp + 4 * t + kq];
+#pragma unroll
+  for (int t = 0; t < PS; ++t)
+    ape[t] = per_feature<D>(prow, prow_pt, 4 * t, kq, dp, sc_sin, sc_cos);
   const bool mul = kd.nodes[2].op == GPK_OP_MUL;
   const bool same_set = !a.plain || a.X == a.Xs;  // (row i and column i are one point)
-  const double halfd = 0.5 * (double)D;
+  constexpr double halfd = 0.5 * (double)D;
   const double noise = a.plain ? 0.0 : a.noise[(int64_t)b * a.noise_stride];
   const int64_t nm = a.plain ? a.n : member_n(a, b), mm = a.plain ? a.m : member_m(a, b);
   const bool interior = !a.plain && gi0 + ATILE <= nm && gj0 + ATILE <= nm;
@@ -314,22 +323,32 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
   double nrow[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) nrow[i] = na_r[16 * w + kq + 4 * i];
+  // two column blocks at a time (four accumulators and eight elements' exps live: the register count, i.e. the
+  // waves per SIMD, is set by this read-out)
 #pragma unroll 1
-  for (int cb = 0; cb < 4; ++cb) {
-    d4 dse = {0.0, 0.0, 0.0, 0.0}, dpe = {0.0, 0.0, 0.0, 0.0};
-    for (int s = 0; 4 * s < D; ++s) {
-      const int k = 4 * s + kq;
-      const double av = k < D ? prow[fs.off + (16 * w + lr) * dp + k] : 0.0;
-      const double bv = k < D ? pcol[fs.off + (16 * cb + lr) * dp + k] : 0.0;
-      dse = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, dse, 0, 0, 0);
+  for (int cp = 0; cp < 2; ++cp) {
+    d4 dse[2], dpe[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      dse[h] = d4{0.0, 0.0, 0.0, 0.0};
+      dpe[h] = d4{0.0, 0.0, 0.0, 0.0};
     }
-    for (int s = 0; 4 * s < 2 * D; ++s) {
-      const int k = 4 * s + kq;
-      const double av = per_feature(prow, 16 * w + lr, k, D, dp, sc_sin, sc_cos);
-      const double bv = per_feature(pcol, 16 * cb + lr, k, D, dp, sc_sin, sc_cos);
-      dpe = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, dpe, 0, 0, 0);
-    }
-    const int col = 16 * cb + lr;
+#pragma unroll
+    for (int t = 0; t < SS; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        dse[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ase[t], pcol[fs.off + (16 * (2 * cp + h) + lr) * dp + 4 * t + kq],
+                                                      dse[h], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < PS; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double bv = per_feature<D>(pcol, 16 * (2 * cp + h) + lr, 4 * t, kq, dp, sc_sin, sc_cos);
+        dpe[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ape[t], bv, dpe[h], 0, 0, 0);
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+    const int col = 16 * (2 * cp + h) + lr;
     const int64_t gj = gj0 + col;
     const double ncol = na_c[col];
     const int ccls = (a.plain || interior) ? CLS_TRAIN : classify(a, gj, nm, mm);
@@ -338,8 +357,8 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
       const int row = 16 * w + kq + 4 * i;
       const int64_t gi = gi0 + row;
       const bool same = same_set && gi == gj;
-      double r2 = fma(-2.0, dse[i], nrow[i] + ncol);
-      double sn = fma(-0.5, dpe[i], halfd);
+      double r2 = fma(-2.0, dse[h][i], nrow[i] + ncol);
+      double sn = fma(-0.5, dpe[h][i], halfd);
       r2 = same ? 0.0 : fmax(r2, 0.0);
       sn = same ? 0.0 : fmax(sn, 0.0);
       const double vse = fs.sg * exp(-0.5 * (r2 * fs.il2));
@@ -368,6 +387,7 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
         }
       }
       Wt[(int64_t)row * a.ld + col] = (TOut)v;
+    }
     }
   }
 }
@@ -405,8 +425,11 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
 // single-node kernels get the lighter instantiation and keep four waves per SIMD); 3: two-leaf SE + periodic trees
 // on MFMA (pair_mfma_tile), tiles outside its error bounds through the generic loop -- an instantiation of its own,
 // so that neither path's registers limit the other's occupancy
+#ifndef GPK_ASM3_MINB
+#define GPK_ASM3_MINB 1  // TREE 3: workgroups per CU the register allocation must allow (A/B)
+#endif
 template <typename TOut, int TREE>
-__global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
+__global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int sc_flag;
   __shared__ unsigned long long pair_max[2];  // (TREE 2) max |u|^2 of the tile's row / column points, as bits
@@ -501,9 +524,14 @@ __global__ __launch_bounds__(256) void assemble_kernel(gpk_kdesc kd, AsmArgs a) 
       const double bound = (__longlong_as_double((long long)pair_max[0]) + __longlong_as_double((long long)pair_max[1])) *
                            fs.il2;
       if (bound <= PAIR_MFMA_MAX_NORM) {
-        pair_mfma_tile<TOut>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b,
-                             reinterpret_cast<TOut*>(a.W) + (int64_t)b * a.w_bs);
-        return;
+        TOut* const Wb = reinterpret_cast<TOut*>(a.W) + (int64_t)b * a.w_bs;
+        switch (a.d) {
+          case 4: pair_mfma_tile<TOut, 4>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b, Wb); return;
+          case 8: pair_mfma_tile<TOut, 8>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b, Wb); return;
+          // case 12: pair_mfma_tile<TOut, 12>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b, Wb); return;
+          // case 16: pair_mfma_tile<TOut, 16>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b, Wb); return;
+          default: break;
+        }
       }
     }
   }
@@ -1166,7 +1194,7 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
   // separable periodic node at D >= 4 (pair_mfma_tile), 1 any other tree
   const bool pair = kd.n_nodes == 3 && (kd.nodes[2].op == GPK_OP_ADD || kd.nodes[2].op == GPK_OP_MUL);
   int tree = kd.n_nodes == 1 ? 0 : (pair && !tune_pair_off() ? 2 : 1);
-  if (tree == 2 && GPK_ASM_PAIR_MFMA && a.A == nullptr && a.d >= 4 && dtype == GPK_F64) {
+  if (tree == 2 && GPK_ASM_PAIR_MFMA && a.A == nullptr && a.d % 4 == 0 && dtype == GPK_F64) {
     const int q = sc_node(kd);
     const gpk_node se = kd.nodes[q == 0 ? 1 : 0];
     if ((q == 0 || q == 1) && se.op == GPK_OP_SE && !(se.flags & GPK_NODE_SE_EXPANDED)) tree = 3;
