@@ -319,10 +319,17 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
   const double noise = a.plain ? 0.0 : a.noise[(int64_t)b * a.noise_stride];
   const int64_t nm = a.plain ? a.n : member_n(a, b), mm = a.plain ? a.m : member_m(a, b);
   const bool interior = !a.plain && gi0 + ATILE <= nm && gj0 + ATILE <= nm;
+  // (workgroup-uniform; every tile of an N = 16384 matrix but the 256 diagonal and edge ones)
+  const bool fast_tile = __builtin_amdgcn_readfirstlane((int)(interior && gi0 != gj0)) != 0;
   TOut* const Wt = W + gi0 * a.ld + gj0;
   double nrow[4];
+  TOut* wrow[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) nrow[i] = na_r[16 * w + kq + 4 * i];
+  for (int i = 0; i < 4; ++i) {
+    nrow[i] = na_r[16 * w + kq + 4 * i];
+    wrow[i] = Wt + (int64_t)(16 * w + kq + 4 * i) * a.ld;
+  }
+  const double cse = -0.5 * fs.il2, cpe = -2.0 * fq.il2;  // (exp(-0.5 r^2 / l^2), exp(-2 sn / l^2))
   // two column blocks at a time (four accumulators and eight elements' exps live: the register count, i.e. the
   // waves per SIMD, is set by this read-out)
 #pragma unroll 1
@@ -346,48 +353,66 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
         const double bv = per_feature<D>(pcol, 16 * (2 * cp + h) + lr, 4 * t, kq, dp, sc_sin, sc_cos);
         dpe[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ape[t], bv, dpe[h], 0, 0, 0);
       }
+    if (fast_tile) {
+      // interior, off the diagonal: no classes, no noise, no coincident points
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-    const int col = 16 * (2 * cp + h) + lr;
-    const int64_t gj = gj0 + col;
-    const double ncol = na_c[col];
-    const int ccls = (a.plain || interior) ? CLS_TRAIN : classify(a, gj, nm, mm);
+      for (int h = 0; h < 2; ++h) {
+        const int col = 16 * (2 * cp + h) + lr;
+        const double ncol = na_c[col];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 16 * w + kq + 4 * i;
-      const int64_t gi = gi0 + row;
-      const bool same = same_set && gi == gj;
-      double r2 = fma(-2.0, dse[h][i], nrow[i] + ncol);
-      double sn = fma(-0.5, dpe[h][i], halfd);
-      r2 = same ? 0.0 : fmax(r2, 0.0);
-      sn = same ? 0.0 : fmax(sn, 0.0);
-      const double vse = fs.sg * exp(-0.5 * (r2 * fs.il2));
-      const double vper = fq.sg * exp((-2.0 * sn) * fq.il2);
-      const double v0 = se_leaf == 0 ? vse : vper, v1 = se_leaf == 0 ? vper : vse;
-      double v = mul ? v0 * v1 : v0 + v1;
-      if (interior) {
-        if (gi == gj) v += noise;
-      } else if (a.plain) {
-        if (gi >= a.n || gj >= a.m || (a.uplo && gj > gi)) continue;
-        if (gi == gj) v += a.diag_add;
-      } else {
-        const int rcls = classify(a, gi, nm, mm);
-        if (rcls == CLS_PAD || ccls == CLS_PAD) {
-          v = (gi == gj) ? 1.0 : 0.0;
-        } else if (a.eye && rcls == CLS_TEST) {
-          v = (ccls == CLS_TRAIN && gj == gi - a.n_pad) ? 1.0 : 0.0;
-        } else if (a.E != nullptr && rcls == CLS_TEST) {
-          v = (ccls == CLS_TRAIN) ? a.E[(int64_t)b * a.e_bs + (gi - a.n_pad) * a.n + gj] : 0.0;
-        } else if ((rcls == CLS_TRAIN || rcls == CLS_TEST) && (ccls == CLS_TRAIN || ccls == CLS_TEST)) {
-          if (rcls == CLS_TRAIN && ccls == CLS_TRAIN && gi == gj) v += noise;
-        } else if (rcls == CLS_Y && ccls == CLS_TRAIN) {
-          v = a.y[(int64_t)b * a.y_bs + gj];
-        } else {
-          v = 0.0;
+        for (int i = 0; i < 4; ++i) {
+          const double r2 = fmax(fma(-2.0, dse[h][i], nrow[i] + ncol), 0.0);
+          const double sn = fmax(fma(-0.5, dpe[h][i], halfd), 0.0);
+          const double vse = fs.sg * exp(r2 * cse);
+          const double vper = fq.sg * exp(sn * cpe);
+          const double v0 = se_leaf == 0 ? vse : vper, v1 = se_leaf == 0 ? vper : vse;
+          wrow[i][col] = (TOut)(mul ? v0 * v1 : v0 + v1);
         }
       }
-      Wt[(int64_t)row * a.ld + col] = (TOut)v;
+      continue;
     }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = 16 * (2 * cp + h) + lr;
+      const int64_t gj = gj0 + col;
+      const double ncol = na_c[col];
+      const int ccls = (a.plain || interior) ? CLS_TRAIN : classify(a, gj, nm, mm);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * w + kq + 4 * i;
+        const int64_t gi = gi0 + row;
+        const bool same = same_set && gi == gj;
+        double r2 = fma(-2.0, dse[h][i], nrow[i] + ncol);
+        double sn = fma(-0.5, dpe[h][i], halfd);
+        r2 = same ? 0.0 : fmax(r2, 0.0);
+        sn = same ? 0.0 : fmax(sn, 0.0);
+        const double vse = fs.sg * exp(r2 * cse);
+        const double vper = fq.sg * exp(sn * cpe);
+        const double v0 = se_leaf == 0 ? vse : vper, v1 = se_leaf == 0 ? vper : vse;
+        double v = mul ? v0 * v1 : v0 + v1;
+        if (interior) {
+          if (gi == gj) v += noise;
+        } else if (a.plain) {
+          if (gi >= a.n || gj >= a.m || (a.uplo && gj > gi)) continue;
+          if (gi == gj) v += a.diag_add;
+        } else {
+          const int rcls = classify(a, gi, nm, mm);
+          if (rcls == CLS_PAD || ccls == CLS_PAD) {
+            v = (gi == gj) ? 1.0 : 0.0;
+          } else if (a.eye && rcls == CLS_TEST) {
+            v = (ccls == CLS_TRAIN && gj == gi - a.n_pad) ? 1.0 : 0.0;
+          } else if (a.E != nullptr && rcls == CLS_TEST) {
+            v = (ccls == CLS_TRAIN) ? a.E[(int64_t)b * a.e_bs + (gi - a.n_pad) * a.n + gj] : 0.0;
+          } else if ((rcls == CLS_TRAIN || rcls == CLS_TEST) && (ccls == CLS_TRAIN || ccls == CLS_TEST)) {
+            if (rcls == CLS_TRAIN && ccls == CLS_TRAIN && gi == gj) v += noise;
+          } else if (rcls == CLS_Y && ccls == CLS_TRAIN) {
+            v = a.y[(int64_t)b * a.y_bs + gj];
+          } else {
+            v = 0.0;
+          }
+        }
+        wrow[i][col] = (TOut)v;
+      }
     }
   }
 }
@@ -426,7 +451,7 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
 // on MFMA (pair_mfma_tile), tiles outside its error bounds through the generic loop -- an instantiation of its own,
 // so that neither path's registers limit the other's occupancy
 #ifndef GPK_ASM3_MINB
-#define GPK_ASM3_MINB 1  // TREE 3: workgroups per CU the register allocation must allow (A/B)
+#define GPK_ASM3_MINB 3  // TREE 3: workgroups per CU the register allocation must allow (A/B)
 #endif
 template <typename TOut, int TREE>
 __global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
