@@ -182,6 +182,8 @@ struct Tune {
   int64_t chain_eye;      //   identity-augmented factorisations (the gradient / explicit inverse) too (1: auto as
                           //   above, 0: never)
   int64_t chain_max_p_eye;  // ... while their augmented matrix has at most this many rows
+  int64_t asm_feat;       // K build, two-leaf SE + periodic trees on MFMA: per-point features in a pre-pass
+                          // (pair_feat_kernel; 0: staged per tile, A/B -- bitwise equal)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -205,7 +207,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 0),
                          env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500),
                          env_i64("GPK_CHAIN_UQ", 1), env_i64("GPK_CHAIN_EYE", 1),
-                         env_i64("GPK_CHAIN_MAX_P_EYE", 16640)};
+                         env_i64("GPK_CHAIN_MAX_P_EYE", 16640), env_i64("GPK_ASM_FEAT", 1)};
   return t;
 }
 
@@ -231,6 +233,7 @@ const Knob kKnobs[] = {
     {"chain_group", &Tune::chain_group},     {"chain_max_batch", &Tune::chain_max_batch},
     {"chain_batch_max_rows", &Tune::chain_batch_max_rows}, {"chain_uq", &Tune::chain_uq},
     {"chain_eye", &Tune::chain_eye},         {"chain_max_p_eye", &Tune::chain_max_p_eye},
+    {"asm_feat", &Tune::asm_feat},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -251,6 +254,7 @@ Tune tune_now() {
   for (const auto& o : t_tune_over) t.*(o.first) = o.second;
   return t;
 }
+
 
 // Per host thread and device: the high-priority panel stream, the bulk-update stream (created
 // with a CU mask that leaves tune().reserve_cus CUs to the panel chain, so that the
@@ -783,6 +787,10 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
 }
 
 }  // namespace
+
+namespace gpk {
+bool tune_asm_feat() { return tune_now().asm_feat != 0; }
+}  // namespace gpk
 
 extern "C" {
 

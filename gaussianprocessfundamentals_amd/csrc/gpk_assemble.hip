@@ -20,6 +20,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <map>
+#include <mutex>
+
 #include "gpk_internal.h"
 #include "gpk_kernels.h"
 
@@ -275,6 +279,61 @@ __device__ __forceinline__ void interior_pair(const gpk_kdesc& kd, const FastNod
 constexpr double PAIR_MFMA_MAX_NORM = 512.0;
 constexpr double PAIR_MFMA_MAX_DIL2 = 128.0;
 
+// exp(x) for x <= 0 (the kernel values' exponents): 2^(k / 32) from a 32-entry table in LDS (tab) times a degree-6
+// Taylor polynomial on |r| <= ln2 / 64 (truncation <= 4e-18), k = rint(32 x / ln2), r = x - k ln2 / 32 by a two-part
+// Cody-Waite reduction (k L1 exact for |k| < 2^21); x clamped at -746 (2^-1076: 0).  <= 1.5 ulp against the correctly
+// rounded exp (checked in numpy over [-745, 0]); ~16 VALU operations and one conflict-free LDS read (distinct table
+// entries sit on distinct bank pairs) against ~25 for the library exp with its overflow / NaN guards.  NaN input:
+// never reaches it (the pair path's tile bounds reject NaN points and hyperparameters).
+__device__ const double kExp2Tab32[32] = {
+    1.0, 1.0218971486541166, 1.0442737824274138, 1.0671404006768237, 1.0905077326652577, 1.1143867425958924,
+    1.1387886347566916, 1.1637248587775775, 1.189207115002721, 1.215247359980469, 1.241857812073484,
+    1.2690509571917332, 1.2968395546510096, 1.3252366431597413, 1.3542555469368927, 1.383909881963832,
+    1.4142135623730951, 1.4451808069770467, 1.4768261459394993, 1.5091644275934228, 1.5422108254079407,
+    1.5759808451078865, 1.6104903319492543, 1.645755478153965, 1.681792830507429, 1.718619298122478,
+    1.7562521603732995, 1.7947090750031072, 1.8340080864093424, 1.8741676341103, 1.9152065613971474,
+    1.9571441241754002};
+#ifndef GPK_ASM_TAB_EXP
+#define GPK_ASM_TAB_EXP 1
+#endif
+__device__ __forceinline__ double exp_neg(double x, const double* tab) {
+#pragma clang fp contract(on)
+  if (!GPK_ASM_TAB_EXP) return exp(x);
+  x = fmax(x, -746.0);
+  const double k = rint(x * 46.16624130844683);             // 32 / ln2
+  double r = fma(-k, 0.02166084938653512, x);               // L1: ln2 / 32 to 32 significant bits
+  r = fma(-k, 5.9631716539705866e-12, r);                   // L2
+  double p = 1.0 / 720.0;
+  p = fma(p, r, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const int ki = (int)k;
+  return ldexp(tab[ki & 31] * p, ki >> 5);
+}
+
+// 2^(t / 32) = exp(t ln2 / 32) for the pair tile's fast read-out, whose exponents come out in these units (the
+// scale folded into its per-tile constants): k = rint(t), s = t - k (exact), 2^(k / 32) from the table times the
+// degree-6 Taylor polynomial of exp(s ln2 / 32) with the powers of ln2 / 32 folded into its coefficients -- no
+// reduction step.  <= 1.5 ulp against the correctly rounded exp of t ln2 / 32 (numpy / mpmath over [-24000, 80]);
+// t >= -2^26 (every exponent the pair bounds admit is >= -512 ln 2 ... -25000 units).  14 VALU operations.
+__device__ __forceinline__ double exp2_32(double t, const double* tab) {
+#pragma clang fp contract(on)
+  const double k = rint(t);
+  const double sr = t - k;
+  double p = 1.4345655584131934e-13;
+  p = fma(p, sr, 3.973709984549416e-11);
+  p = fma(p, sr, 9.172562701824643e-09);
+  p = fma(p, sr, 1.693850972437182e-06);
+  p = fma(p, sr, 0.0002345961982022468);
+  p = fma(p, sr, 0.02166084939249829);
+  p = fma(p, sr, 1.0);
+  const int ki = (int)k;
+  return ldexp(tab[ki & 31] * p, ki >> 5);
+}
+
 // per-point feature k0 + kq of the periodic leaf: C_k (k < D), S_{k - D} (k < 2 D); k0 a multiple of 4 (inside the
 // unrolled k-step loops a constant, so the branch folds)
 template <int D>
@@ -295,8 +354,8 @@ __device__ __forceinline__ double per_feature(const double* pts, int pt, int k0,
 template <typename TOut, int D>
 __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArgs& a, const FastNode* fns, int se_leaf,
                                                const double* prow, const double* pcol, int sc_sin, int sc_cos,
-                                               const double* na_r, const double* na_c, int64_t gi0, int64_t gj0,
-                                               int b, TOut* W) {
+                                               const double* na_r, const double* na_c, const double* tab,
+                                               int64_t gi0, int64_t gj0, int b, TOut* W) {
 #pragma clang fp contract(on)
   static_assert(D % 4 == 0, "whole k-steps");
   constexpr int SS = D / 4, PS = 2 * D / 4;
@@ -305,14 +364,15 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
   const int lr = lane & 15, kq = lane >> 4;
   const int dp = a.dp;
   const FastNode fs = fns[se_leaf], fq = fns[1 - se_leaf];
+  auto se_op = [&](const double* P, int pt, int k) { return P[fs.off + pt * dp + k]; };
+  auto per_op = [&](const double* P, int pt, int k0) { return per_feature<D>(P, pt, k0, kq, dp, sc_sin, sc_cos); };
   // the row operands (this wave's 16 rows) once; the column operands per block
   double ase[SS], ape[PS];
   const int prow_pt = 16 * w + lr;
 #pragma unroll
-  for (int t = 0; t < SS; ++t) ase[t] = prow[fs.off + prow_pt * dp + 4 * t + kq];
+  for (int t = 0; t < SS; ++t) ase[t] = se_op(prow, prow_pt, 4 * t + kq);
 #pragma unroll
-  for (int t = 0; t < PS; ++t)
-    ape[t] = per_feature<D>(prow, prow_pt, 4 * t, kq, dp, sc_sin, sc_cos);
+  for (int t = 0; t < PS; ++t) ape[t] = per_op(prow, prow_pt, 4 * t);
   const bool mul = kd.nodes[2].op == GPK_OP_MUL;
   const bool same_set = !a.plain || a.X == a.Xs;  // (row i and column i are one point)
   constexpr double halfd = 0.5 * (double)D;
@@ -320,7 +380,10 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
   const int64_t nm = a.plain ? a.n : member_n(a, b), mm = a.plain ? a.m : member_m(a, b);
   const bool interior = !a.plain && gi0 + ATILE <= nm && gj0 + ATILE <= nm;
   // (workgroup-uniform; every tile of an N = 16384 matrix but the 256 diagonal and edge ones)
-  const bool fast_tile = __builtin_amdgcn_readfirstlane((int)(interior && gi0 != gj0)) != 0;
+  const bool fast_tile =
+      __builtin_amdgcn_readfirstlane((int)(interior && fs.sg > 0.0 && fq.sg > 0.0)) != 0;
+  const bool diag = gi0 == gj0;
+  const double kself = (mul ? fs.sg * fq.sg : fs.sg + fq.sg) + noise;  // (diagonal of K + noise I)
   TOut* const Wt = W + gi0 * a.ld + gj0;
   double nrow[4];
   TOut* wrow[4];
@@ -330,6 +393,17 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
     wrow[i] = Wt + (int64_t)(16 * w + kq + 4 * i) * a.ld;
   }
   const double cse = -0.5 * fs.il2, cpe = -2.0 * fq.il2;  // (exp(-0.5 r^2 / l^2), exp(-2 sn / l^2))
+  // the fast read-out's exponents in units of ln2 / 32 (exp2_32), the scales sg inside them:
+  //   SE   sg exp(-0.5 il2 (|u_i|^2 + |u_j|^2 - 2 u_i.u_j)) = 2^(ts / 32),  ts = min(a_s dse + hr_i + hc_j, lsg_s)
+  //   PER  sg exp(-2 il2 (D / 2 - dpe / 2))                 = 2^(tp / 32),  tp = min(a_p dpe + c_p, lsg_p)
+  // (the min: the reference's clamp-free direct forms never exceed sg; neither may the expanded ones)
+  constexpr double kU = 46.16624130844683;  // 32 / ln2
+  const double lsg_s = fast_tile ? log(fs.sg) * kU : 0.0, lsg_p = fast_tile ? log(fq.sg) * kU : 0.0;
+  const double a_s = fs.il2 * kU, a_p = fq.il2 * kU;
+  const double c_p = fma(-(double)D, a_p, lsg_p);
+  double hr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) hr[i] = fma(-0.5 * a_s, nrow[i], lsg_s);
   // two column blocks at a time (four accumulators and eight elements' exps live: the register count, i.e. the
   // waves per SIMD, is set by this read-out)
 #pragma unroll 1
@@ -344,29 +418,32 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
     for (int t = 0; t < SS; ++t)
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        dse[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ase[t], pcol[fs.off + (16 * (2 * cp + h) + lr) * dp + 4 * t + kq],
+        dse[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ase[t], se_op(pcol, 16 * (2 * cp + h) + lr, 4 * t + kq),
                                                       dse[h], 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < PS; ++t)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const double bv = per_feature<D>(pcol, 16 * (2 * cp + h) + lr, 4 * t, kq, dp, sc_sin, sc_cos);
+        const double bv = per_op(pcol, 16 * (2 * cp + h) + lr, 4 * t);
         dpe[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ape[t], bv, dpe[h], 0, 0, 0);
       }
     if (fast_tile) {
-      // interior, off the diagonal: no classes, no noise, no coincident points
+      // interior: no classes; MUL: one exp of the summed exponents.  Diagonal tiles: the symmetric form of the SE
+      // exponent (K bitwise symmetric there) and k(x, x) + noise exactly on the diagonal.  pair_fast_kernel's values
+      // bit for bit (IEEE addition commutes, so the leaf order is moot).
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int col = 16 * (2 * cp + h) + lr;
         const double ncol = na_c[col];
+        const double hc = -0.5 * a_s * ncol;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const double r2 = fmax(fma(-2.0, dse[h][i], nrow[i] + ncol), 0.0);
-          const double sn = fmax(fma(-0.5, dpe[h][i], halfd), 0.0);
-          const double vse = fs.sg * exp(r2 * cse);
-          const double vper = fq.sg * exp(sn * cpe);
-          const double v0 = se_leaf == 0 ? vse : vper, v1 = se_leaf == 0 ? vper : vse;
-          wrow[i][col] = (TOut)(mul ? v0 * v1 : v0 + v1);
+          const double hs = diag ? fma(-0.5 * a_s, nrow[i] + ncol, lsg_s) : hr[i] + hc;
+          const double ts = fmin(fma(dse[h][i], a_s, hs), lsg_s);
+          const double tp = fmin(fma(dpe[h][i], a_p, c_p), lsg_p);
+          const double e1 = exp2_32(mul ? ts + tp : ts, tab);
+          const double v = mul ? e1 : e1 + exp2_32(tp, tab);
+          wrow[i][col] = (TOut)((diag && 16 * w + kq + 4 * i == col) ? kself : v);
         }
       }
       continue;
@@ -386,8 +463,8 @@ __device__ __forceinline__ void pair_mfma_tile(const gpk_kdesc& kd, const AsmArg
         double sn = fma(-0.5, dpe[h][i], halfd);
         r2 = same ? 0.0 : fmax(r2, 0.0);
         sn = same ? 0.0 : fmax(sn, 0.0);
-        const double vse = fs.sg * exp(r2 * cse);
-        const double vper = fq.sg * exp(sn * cpe);
+        const double vse = fs.sg * exp_neg(r2 * cse, tab);
+        const double vper = fq.sg * exp_neg(sn * cpe, tab);
         const double v0 = se_leaf == 0 ? vse : vper, v1 = se_leaf == 0 ? vper : vse;
         double v = mul ? v0 * v1 : v0 + v1;
         if (interior) {
@@ -446,6 +523,222 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
 }
 
 
+// Lower-triangular tile t of an augmented build, row-major; with tcol_hi > 0 only the tile columns [0, tcol_hi):
+// their triangle, then the full rows below it.
+__device__ __forceinline__ void lower_tile(const AsmArgs& a, int64_t t, int64_t& ti, int64_t& tj) {
+  const int64_t w = a.tcol_hi;
+  if (w > 0 && t >= w * (w + 1) / 2) {
+    const int64_t u = t - w * (w + 1) / 2;
+    ti = w + u / w;
+    tj = u % w;
+  } else {
+    int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while (r * (r + 1) / 2 > t) --r;
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    ti = r;
+    tj = t - r * (r + 1) / 2;
+  }
+}
+
+// Per-point features of the two-leaf SE + periodic MFMA path, once per point instead of once per tile (a point's
+// sin / cos and ARD quotients were recomputed by each of the ~N / 64 tiles it borders: ~20 of the ~110 VALU
+// operations per matrix element at N = 16384, D = 8).  One wave per 64-point block of member b: the feature row
+// [u_1..u_D | C_1..C_D | S_1..S_D | |u|^2 | 0] of each point -- u the SE leaf's (ARD-rescaled) coordinates, C_k =
+// 1 - 2 sin^2(pi f_k), S_k = 2 sin(pi f_k) cos(pi f_k) of the periodic leaf's f_k = x_k / p - rint(x_k / p), the
+// same operations, in the same order, as stage_points + per_feature + the per-tile norm loop -- and the block's
+// (max |u|^2, every |x_k / p| <= SC_MAX_U) for the tile kernel's bounds.  Points are classified as in
+// stage_points (training rows of X, test rows of Xs, zeros elsewhere).
+template <int D>
+__global__ __launch_bounds__(64) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a, int se_node, int per_node) {
+#pragma clang fp contract(on)
+  constexpr int FS = 3 * D + 2;
+  const int b = blockIdx.y;
+  const int64_t g = (int64_t)blockIdx.x * ATILE + threadIdx.x;
+  const double* hyp = a.hyp + (int64_t)b * a.hyp_stride;
+  const gpk_node se = kd.nodes[se_node], pq = kd.nodes[per_node];
+  const bool ard = (se.flags & GPK_NODE_ARD) != 0;
+  const double iper = 1.0 / hyp[pq.hyp_offset + 1];
+  const int c = classify(a, g, member_n(a, b), member_m(a, b));
+  const double* src = nullptr;
+  if (c == CLS_TRAIN) src = a.X + (int64_t)b * a.x_bs + g * a.d;
+  else if (c == CLS_TEST && a.E == nullptr && !a.eye) src = a.Xs + (int64_t)b * a.xs_bs + (g - a.n_pad) * a.d;
+  double* f = const_cast<double*>(a.feat) + (int64_t)b * a.feat_bs + g * FS;
+  double nrm = 0.0;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const double v = src ? src[k] : 0.0;
+    const double u = ard ? v / hyp[se.hyp_offset + k] : v;
+    nrm = fma(u, u, nrm);
+    f[k] = u;
+    const double t = v * iper;
+    ok = ok && fabs(t) <= SC_MAX_U;
+    double sv, cv;
+    sincospi(t - rint(t), &sv, &cv);
+    f[D + k] = fma(-2.0 * sv, sv, 1.0);
+    f[2 * D + k] = 2.0 * (sv * cv);
+  }
+  f[3 * D] = nrm;
+  f[3 * D + 1] = 0.0;
+  double mx = nrm;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  const bool all_ok = __all(ok);
+  if (threadIdx.x == 0) {
+    double* x = const_cast<double*>(a.faux) + 2 * ((int64_t)b * gridDim.x + blockIdx.x);
+    x[0] = mx;
+    x[1] = all_ok ? 1.0 : 0.0;
+    if (blockIdx.x == 0) {
+      // the member's read-out constants (pair_fast_kernel; the same operations as pair_mfma_tile's): exponents in
+      // units of ln2 / 32, the scales inside them; [5] the node-level bounds, [6] the SE leaf's 1 / l^2
+      const FastNode fsn = make_fast_node(se, hyp, a.d), fqn = make_fast_node(pq, hyp, a.d);
+      const bool node_ok = (double)a.d * fqn.il2 <= PAIR_MFMA_MAX_DIL2 && fsn.sg > 0.0 && fqn.sg > 0.0;
+      constexpr double kU = 46.16624130844683;
+      double* mc = const_cast<double*>(a.faux) + 2 * (int64_t)gridDim.y * gridDim.x + 8 * b;
+      mc[0] = fsn.il2 * kU;
+      mc[1] = node_ok ? log(fsn.sg) * kU : 0.0;
+      mc[2] = fqn.il2 * kU;
+      mc[4] = node_ok ? log(fqn.sg) * kU : 0.0;
+      mc[3] = fma(-(double)D, mc[2], mc[4]);
+      mc[5] = node_ok ? 1.0 : 0.0;
+      mc[6] = fsn.il2;
+      mc[7] = kd.nodes[2].op == GPK_OP_MUL ? fsn.sg * fqn.sg : fsn.sg + fqn.sg;  // k(x, x)
+      if (b == 0) const_cast<int32_t*>(a.tlist)[0] = 0;
+    }
+  }
+}
+
+// The interior off-diagonal tiles of a two-leaf SE + periodic tree whose bounds hold, from pair_feat_kernel's
+// features: one 256-thread workgroup per lower tile (the assemble grid).  The tile's 2 x 64 feature rows (contiguous
+// in HBM, L2-resident) go to LDS -- row stride 3 D + 2 doubles, so that the 16 points x 2 k-lanes of an MFMA operand
+// read hit 32 distinct bank pairs -- then wave w takes rows 16 w .. 16 w + 15 against the 64 columns: per 16 x 16
+// block D / 4 MFMAs (u_i . u_j) and D / 2 (sum_k C_ik C_jk + S_ik S_jk), then per element
+//   ADD  2^(ts / 32) + 2^(tp / 32),  MUL  2^((ts + tp) / 32),
+//   ts = min(a_s dse + hr_i + hc_j, lsg_s), tp = min(a_p dpe + c_p, lsg_p)   (pair_feat_kernel's member constants)
+// Every other tile (the diagonal, edge tiles, tiles outside the bounds) is appended to the tile list for the general
+// instantiation.  No class logic, no staging, no sin / cos: ~31 VALU operations per element with ADD (two exps of
+// 14), ~17 with MUL -- a kernel of its own, so that none of the general path's registers weigh on it.
+template <int D, bool MUL>
+__global__ __launch_bounds__(256, 3) void pair_fast_kernel(gpk_kdesc kd, AsmArgs a) {
+#pragma clang fp contract(on)
+  constexpr int FS = 3 * D + 2, SS = D / 4, PS = 2 * D / 4;
+  __shared__ __attribute__((aligned(16))) double fr[ATILE * FS];
+  __shared__ __attribute__((aligned(16))) double fc[ATILE * FS];
+  __shared__ double tab[32];
+  const int b = blockIdx.y;
+  int64_t ti, tj;
+  lower_tile(a, blockIdx.x, ti, tj);
+  const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
+  const int64_t nm = member_n(a, b), mm = member_m(a, b);
+  const int tid = threadIdx.x;
+  if (gi0 >= a.n_pad + mm) {
+    // tail tiles (the y row and the zero rows below it): y^T on the y row, zeros elsewhere -- the general loop's
+    // values (CLS_Y / CLS_ZERO rows), without its staging
+    const int c = tid & 63;
+    const int64_t gj = gj0 + c;
+    const double yv = gj < nm ? a.y[(int64_t)b * a.y_bs + gj] : 0.0;
+    double* const Wc = reinterpret_cast<double*>(a.W) + (int64_t)b * a.w_bs + gj;
+    for (int rr = tid >> 6; rr < ATILE; rr += 4) Wc[(gi0 + rr) * a.ld] = gi0 + rr == a.y_row ? yv : 0.0;
+    return;
+  }
+  const double* xr = a.faux + 2 * ((int64_t)b * a.ntile + ti);
+  const double* xc = a.faux + 2 * ((int64_t)b * a.ntile + tj);
+  const double* mc = a.faux + 2 * (int64_t)gridDim.y * a.ntile + 8 * b;
+  const bool fast = gi0 + ATILE <= nm && gj0 + ATILE <= nm && mc[5] != 0.0 && xr[1] != 0.0 && xc[1] != 0.0 &&
+                    (xr[0] + xc[0]) * mc[6] <= PAIR_MFMA_MAX_NORM;
+  if (!fast) {
+    if (tid == 0) {
+      int32_t* tl = const_cast<int32_t*>(a.tlist);
+      const int k = atomicAdd(tl, 1);
+      tl[1 + 3 * k] = b;
+      tl[2 + 3 * k] = (int32_t)ti;
+      tl[3 + 3 * k] = (int32_t)tj;
+    }
+    return;
+  }
+  const double* fb = a.feat + (int64_t)b * a.feat_bs;
+  {
+    const double2* sr = reinterpret_cast<const double2*>(fb + gi0 * FS);
+    const double2* sc = reinterpret_cast<const double2*>(fb + gj0 * FS);
+    double2* dr = reinterpret_cast<double2*>(fr);
+    double2* dc = reinterpret_cast<double2*>(fc);
+    for (int e = tid; e < ATILE * FS / 2; e += 256) {
+      dr[e] = sr[e];
+      dc[e] = sc[e];
+    }
+    if (tid < 32) tab[tid] = kExp2Tab32[tid];
+  }
+  const double a_s = mc[0], lsg_s = mc[1], a_p = mc[2], c_p = mc[3], lsg_p = mc[4];
+  const bool diag = ti == tj;
+  const double kself = mc[7] + (diag ? a.noise[(int64_t)b * a.noise_stride] : 0.0);
+  __syncthreads();
+  const int lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, kq = lane >> 4;
+  double ase[SS], ape[PS];
+  const int prow_pt = 16 * w + lr;
+#pragma unroll
+  for (int t = 0; t < SS; ++t) ase[t] = fr[prow_pt * FS + 4 * t + kq];
+#pragma unroll
+  for (int t = 0; t < PS; ++t) ape[t] = fr[prow_pt * FS + D + 4 * t + kq];
+  double hr[4];
+  double* wrow[4];
+  double* const Wt = reinterpret_cast<double*>(a.W) + (int64_t)b * a.w_bs + gi0 * a.ld + gj0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    hr[i] = fma(-0.5 * a_s, fr[(16 * w + kq + 4 * i) * FS + 3 * D], lsg_s);
+    wrow[i] = Wt + (int64_t)(16 * w + kq + 4 * i) * a.ld;
+  }
+#pragma unroll 1
+  for (int cp = 0; cp < 2; ++cp) {
+    d4 dse[2], dpe[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      dse[h] = d4{0.0, 0.0, 0.0, 0.0};
+      dpe[h] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+#pragma unroll
+    for (int t = 0; t < SS; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        dse[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ase[t], fc[(16 * (2 * cp + h) + lr) * FS + 4 * t + kq], dse[h],
+                                                      0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < PS; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        dpe[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ape[t], fc[(16 * (2 * cp + h) + lr) * FS + D + 4 * t + kq],
+                                                      dpe[h], 0, 0, 0);
+    if (!diag) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int col = 16 * (2 * cp + h) + lr;
+        const double hc = -0.5 * a_s * fc[col * FS + 3 * D];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const double ts = fmin(fma(dse[h][i], a_s, hr[i] + hc), lsg_s);
+          const double tp = fmin(fma(dpe[h][i], a_p, c_p), lsg_p);
+          wrow[i][col] = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
+        }
+      }
+    } else {
+      // the diagonal tile: the symmetric form of the SE exponent (K bitwise symmetric), k(x, x) + noise exactly
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int col = 16 * (2 * cp + h) + lr;
+        const double ncol = fc[col * FS + 3 * D];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 16 * w + kq + 4 * i;
+          const double ts = fmin(fma(dse[h][i], a_s, fma(-0.5 * a_s, fr[row * FS + 3 * D] + ncol, lsg_s)), lsg_s);
+          const double tp = fmin(fma(dpe[h][i], a_p, c_p), lsg_p);
+          const double v = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
+          wrow[i][col] = row == col ? kself : v;
+        }
+      }
+    }
+  }
+}
+
 // TREE: the instantiation for kernel trees (its interior loop holds two column points in registers;
 // single-node kernels get the lighter instantiation and keep four waves per SIMD); 3: two-leaf SE + periodic trees
 // on MFMA (pair_mfma_tile), tiles outside its error bounds through the generic loop -- an instantiation of its own,
@@ -454,10 +747,8 @@ __device__ __forceinline__ bool interior_d(const gpk_kdesc& kd, const FastNode& 
 #define GPK_ASM3_MINB 3  // TREE 3: workgroups per CU the register allocation must allow (A/B)
 #endif
 template <typename TOut, int TREE>
-__global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int sc_flag;
-  __shared__ unsigned long long pair_max[2];  // (TREE 2) max |u|^2 of the tile's row / column points, as bits
+__device__ __forceinline__ void assemble_tile(const gpk_kdesc& kd, const AsmArgs& a, int64_t ti, int64_t tj, int b,
+                                              double* smem, int& sc_flag, unsigned long long* pair_max) {
   const int slot_stride = ATILE * a.dp;
   // slots per tile edge: raw points, one per ARD node, and (periodic node through sin / cos) sin, cos
   const int scq = a.A == nullptr ? sc_node(kd) : -1;
@@ -466,30 +757,6 @@ __global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_k
   double* hyp_s = smem;                                  // GPK_MAX_HYP
   double* prow = smem + GPK_MAX_HYP;                     // nslot * slot_stride
   double* pcol = prow + nslot * slot_stride;
-
-  const int b = blockIdx.y;
-  int64_t ti, tj;
-  if (a.plain) {
-    ti = blockIdx.x / ((a.m + ATILE - 1) / ATILE);
-    tj = blockIdx.x - ti * ((a.m + ATILE - 1) / ATILE);
-    if (a.uplo && tj > ti) return;
-  } else {
-    // lower-triangular tile enumeration, row-major; with tcol_hi > 0 only the tile columns
-    // [0, tcol_hi): their triangle, then the full rows below it
-    const int64_t t = blockIdx.x;
-    const int64_t w = a.tcol_hi;
-    if (w > 0 && t >= w * (w + 1) / 2) {
-      const int64_t u = t - w * (w + 1) / 2;
-      ti = w + u / w;
-      tj = u % w;
-    } else {
-      int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-      while (r * (r + 1) / 2 > t) --r;
-      while ((r + 1) * (r + 2) / 2 <= t) ++r;
-      ti = r;
-      tj = t - r * (r + 1) / 2;
-    }
-  }
   const int tid = threadIdx.x;
   const double* hyp_g = a.hyp + (int64_t)b * a.hyp_stride;
   for (int e = tid; e < kd.n_hyp; e += 256) hyp_s[e] = hyp_g[e];
@@ -533,6 +800,8 @@ __global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_k
     if (se_leaf >= 0 && fns[1 - se_leaf].sc && (double)a.d * fns[1 - se_leaf].il2 <= PAIR_MFMA_MAX_DIL2) {
       double* na_r = reinterpret_cast<double*>(fns + GPK_MAX_NODES);
       double* na_c = na_r + ATILE;
+      double* tab = na_c + ATILE;  // exp_neg's 2^(j / 32)
+      if (tid < 32) tab[tid] = kExp2Tab32[tid];
       const FastNode fs = fns[se_leaf];
       if (tid < 2 * ATILE) {
         const double* pts = tid < ATILE ? prow : pcol;
@@ -551,10 +820,10 @@ __global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_k
       if (bound <= PAIR_MFMA_MAX_NORM) {
         TOut* const Wb = reinterpret_cast<TOut*>(a.W) + (int64_t)b * a.w_bs;
         switch (a.d) {
-          case 4: pair_mfma_tile<TOut, 4>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b, Wb); return;
-          case 8: pair_mfma_tile<TOut, 8>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b, Wb); return;
-          // case 12: pair_mfma_tile<TOut, 12>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b, Wb); return;
-          // case 16: pair_mfma_tile<TOut, 16>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, ti * ATILE, tj * ATILE, b, Wb); return;
+          case 4: pair_mfma_tile<TOut, 4>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, tab, ti * ATILE, tj * ATILE, b, Wb); return;
+          case 8: pair_mfma_tile<TOut, 8>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, tab, ti * ATILE, tj * ATILE, b, Wb); return;
+          // case 12: pair_mfma_tile<TOut, 12>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, tab, ti * ATILE, tj * ATILE, b, Wb); return;
+          // case 16: pair_mfma_tile<TOut, 16>(kd, a, fns, se_leaf, prow, pcol, sc_sin, sc_cos, na_r, na_c, tab, ti * ATILE, tj * ATILE, b, Wb); return;
           default: break;
         }
       }
@@ -637,6 +906,39 @@ __global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_k
       v = yv;
     }
     W[gi * a.ld + gj] = (TOut)v;
+  }
+}
+
+template <typename TOut, int TREE>
+__global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_kernel(gpk_kdesc kd, AsmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int sc_flag;
+  __shared__ unsigned long long pair_max[2];  // (TREE 3) max |u|^2 of the tile's row / column points, as bits
+  // (TREE 4: TREE 3's body over the tile list -- the tiles pair_fast_kernel left: diagonal, edge, outside its
+  // bounds -- in a persistent loop; an instantiation of its own without the register bound of TREE 3's, whose
+  // occupancy its few tiles do not need)
+  constexpr int TB = TREE == 4 ? 3 : TREE;
+  const bool list = TREE == 4;
+  const int cnt = list ? a.tlist[0] : 1;
+  for (int e = list ? (int)blockIdx.x : 0; e < cnt; e += list ? (int)gridDim.x : 1) {
+    int b;
+    int64_t ti, tj;
+    if (list) {
+      const int32_t* t = a.tlist + 1 + 3 * e;
+      b = t[0];
+      ti = t[1];
+      tj = t[2];
+      __syncthreads();  // (the previous tile's LDS reads)
+    } else if (a.plain) {
+      b = blockIdx.y;
+      ti = blockIdx.x / ((a.m + ATILE - 1) / ATILE);
+      tj = blockIdx.x - ti * ((a.m + ATILE - 1) / ATILE);
+      if (a.uplo && tj > ti) return;
+    } else {
+      b = blockIdx.y;
+      lower_tile(a, blockIdx.x, ti, tj);
+    }
+    assemble_tile<TOut, TB>(kd, a, ti, tj, b, smem, sc_flag, pair_max);
   }
 }
 
@@ -1192,6 +1494,33 @@ hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_
   return hipGetLastError();
 }
 
+// The K build's stream-ordered scratch (the per-point features of pair_feat_kernel): one pool per device, created
+// on first use, that keeps its memory between builds (release threshold: never).
+static hipMemPool_t feat_pool() {
+  static std::mutex mu;
+  static std::map<int, hipMemPool_t> pools;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = pools.find(dev);
+  if (it != pools.end()) return it->second;
+  hipMemPoolProps props;
+  memset(&props, 0, sizeof(props));
+  props.allocType = hipMemAllocationTypePinned;
+  props.location.type = hipMemLocationTypeDevice;
+  props.location.id = dev;
+  hipMemPool_t p = nullptr;
+  if (hipMemPoolCreate(&p, &props) != hipSuccess) {
+    (void)hipGetLastError();
+    p = nullptr;
+  } else {
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+  pools[dev] = p;
+  return p;
+}
+
 static bool tune_pair_off() {  // GPK_ASM_PAIR=0: two-leaf trees through the general tree instantiation (A/B)
   static const bool off = [] {
     const char* v = getenv("GPK_ASM_PAIR");
@@ -1204,7 +1533,7 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
                            hipStream_t s) {
   const int nslot = 1 + kd.n_ard + ((a.A == nullptr && sc_node(kd) >= 0) ? 2 : 0);
   const size_t lds = sizeof(double) * (GPK_MAX_HYP + 2 * (size_t)nslot * ATILE * a.dp) +
-                     sizeof(FastNode) * GPK_MAX_NODES + sizeof(double) * 2 * ATILE;  // (+ pair_mfma_tile's norms)
+                     sizeof(FastNode) * GPK_MAX_NODES + sizeof(double) * (2 * ATILE + 32);  // (+ pair_mfma_tile's)
   dim3 grid;
   if (a.plain) {
     const int64_t tr = (a.n + ATILE - 1) / ATILE, tc = (a.m + ATILE - 1) / ATILE;
@@ -1224,11 +1553,63 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
     const gpk_node se = kd.nodes[q == 0 ? 1 : 0];
     if ((q == 0 || q == 1) && se.op == GPK_OP_SE && !(se.flags & GPK_NODE_SE_EXPANDED)) tree = 3;
   }
+  // tree 3 on an augmented matrix: the per-point features first (pair_feat_kernel), into stream-ordered scratch of
+  // the library's pool (freed on the stream after the build; the pool keeps its memory, so after the first call
+  // this is a host-side bookkeeping step), then pair_fast_kernel over the grid, then the general instantiation over
+  // the tiles it left.  Without the scratch (or with gpk_tune("asm_feat", 0)) the general instantiation takes the
+  // grid and stages every tile's points itself (the same values, bit for bit).
+  AsmArgs af = a;
+  af.feat = nullptr;
+  af.faux = nullptr;
+  af.tlist = nullptr;
+  void* scratch = nullptr;
+  if (tree == 3 && !a.plain && (a.d == 4 || a.d == 8) && a.ntile > 0 && tune_asm_feat()) {
+    const int fsz = 3 * a.d + 2;
+    const int64_t rows = a.ntile * ATILE;
+    const size_t ntl = (size_t)grid.x * batch;
+    const size_t fdoubles = (size_t)batch * rows * fsz + 2 * (size_t)batch * a.ntile + 8 * (size_t)batch;
+    const size_t fbytes = sizeof(double) * fdoubles + sizeof(int32_t) * (1 + 3 * ntl);
+    hipMemPool_t pool = feat_pool();
+    if (pool && hipMallocFromPoolAsync(&scratch, fbytes, pool, s) == hipSuccess) {
+      af.feat = static_cast<const double*>(scratch);
+      af.faux = af.feat + (size_t)batch * rows * fsz;
+      af.feat_bs = rows * fsz;
+      af.feat_fs = fsz;
+      af.tlist = reinterpret_cast<const int32_t*>(af.feat + fdoubles);
+      const int q = sc_node(kd);
+      const bool mul = kd.nodes[2].op == GPK_OP_MUL;
+      const dim3 fgrid((unsigned)a.ntile, (unsigned)batch, 1);
+      if (a.d == 8) {
+        hipLaunchKernelGGL((pair_feat_kernel<8>), fgrid, dim3(64), 0, s, kd, af, 1 - q, q);
+        if (mul)
+          hipLaunchKernelGGL((pair_fast_kernel<8, true>), grid, dim3(256), 0, s, kd, af);
+        else
+          hipLaunchKernelGGL((pair_fast_kernel<8, false>), grid, dim3(256), 0, s, kd, af);
+      } else {
+        hipLaunchKernelGGL((pair_feat_kernel<4>), fgrid, dim3(64), 0, s, kd, af, 1 - q, q);
+        if (mul)
+          hipLaunchKernelGGL((pair_fast_kernel<4, true>), grid, dim3(256), 0, s, kd, af);
+        else
+          hipLaunchKernelGGL((pair_fast_kernel<4, false>), grid, dim3(256), 0, s, kd, af);
+      }
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        (void)hipFreeAsync(scratch, s);
+        return e;
+      }
+      // the leftover tiles: ~ one per tile row of the matrix normally (diagonal + edge), all of them at worst
+      grid = dim3((unsigned)std::min<size_t>(ntl, 2048), 1, 1);
+    } else {
+      (void)hipGetLastError();
+      scratch = nullptr;
+    }
+  }
   // (above 64 KB -- e.g. an ARD node beside a standard PER node, whose per-point sin / cos take two more point
   // slots, at d = 16: 71 KB; two ARD nodes: 87 KB -- the kernel's dynamic-LDS limit must be raised first)
   {
     const void* fn = dtype == GPK_F64
-                         ? (tree == 3 ? reinterpret_cast<const void*>(assemble_kernel<double, 3>)
+                         ? (af.tlist != nullptr ? reinterpret_cast<const void*>(assemble_kernel<double, 4>)
+                            : tree == 3 ? reinterpret_cast<const void*>(assemble_kernel<double, 3>)
                             : tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<double, 2>)
                                       : tree == 1 ? reinterpret_cast<const void*>(assemble_kernel<double, 1>)
                                                   : reinterpret_cast<const void*>(assemble_kernel<double, 0>))
@@ -1238,9 +1619,12 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
     hipError_t e = ensure_dyn_lds(fn, lds);
     if (e != hipSuccess) return e;
   }
+  if (af.tlist != nullptr) tree = 4;
   if (dtype == GPK_F64) {
-    if (tree == 3)
-      hipLaunchKernelGGL((assemble_kernel<double, 3>), grid, dim3(256), lds, s, kd, a);
+    if (tree == 4)
+      hipLaunchKernelGGL((assemble_kernel<double, 4>), grid, dim3(256), lds, s, kd, af);
+    else if (tree == 3)
+      hipLaunchKernelGGL((assemble_kernel<double, 3>), grid, dim3(256), lds, s, kd, af);
     else if (tree == 2)
       hipLaunchKernelGGL((assemble_kernel<double, 2>), grid, dim3(256), lds, s, kd, a);
     else if (tree == 1)
@@ -1255,7 +1639,12 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
     else
       hipLaunchKernelGGL((assemble_kernel<float, 0>), grid, dim3(256), lds, s, kd, a);
   }
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (scratch) {
+    const hipError_t ef = hipFreeAsync(scratch, s);
+    if (e == hipSuccess) e = ef;
+  }
+  return e;
 }
 
 }  // namespace gpk

@@ -72,6 +72,16 @@ struct AsmArgs {
   const double* A;
   int64_t a_ld;
   int64_t a_bs;
+  // set by launch_assemble only (callers leave them): the two-leaf SE + periodic MFMA path's per-point features
+  // (pair_feat_kernel: rows of feat_fs doubles [u_1..u_D | C_1..C_D | S_1..S_D | |u|^2 | 0], member stride feat_bs)
+  // and per 64-point block (max |u|^2, sin / cos form allowed) in faux; NULL: features staged per tile
+  const double* feat;
+  const double* faux;
+  int64_t feat_bs;
+  int32_t feat_fs;
+  // set by launch_assemble only: tiles the MFMA fast kernel left (count, then (member, ti, tj) triples); the
+  // general instantiation then loops over this list instead of the grid
+  const int32_t* tlist;
 };
 
 struct GemmArgs {
@@ -245,6 +255,7 @@ struct TrsvArgs {
 };
 
 // ----------------------------------------------------------------------------------- launchers
+bool tune_asm_feat();  // gpk_tune("asm_feat") in effect on this thread
 hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
                            hipStream_t s);
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s);

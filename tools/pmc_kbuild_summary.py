@@ -2,6 +2,10 @@
 dispatch, the VALU / SALU / LDS instruction counts per matrix element, the VALU issue utilisation, and HBM bytes
 (2 x FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction) against the algorithmic bytes and 8 TB/s.
 
+The K build of the C5 tree is three launches since round 5 (pair_feat_kernel, pair_fast_kernel, the leftover
+assemble_kernel): the counters are summed over every K-build kernel of one build (dispatches grouped per launch of
+the build), and the duration is the sum of their median durations.
+
 usage: python tools/pmc_kbuild_summary.py [dir] [n] [d]"""
 import collections
 import csv
@@ -18,21 +22,41 @@ alg_bytes = 8 * p * (p + 64) / 2 + 8 * n * d
 tot = collections.defaultdict(float)
 cnt = collections.Counter()
 dur = []
+KB = ("assemble_kernel", "pair_fast_kernel", "pair_feat_kernel")
+
+
+def fam(name):
+    return next((k for k in KB if k in name), None)
+
+
 for f in sorted(glob.glob(root + "/p*/run_counter_collection.csv")):
     per = collections.defaultdict(dict)
     for r in csv.DictReader(open(f)):
-        if "assemble" in r["Kernel_Name"]:
-            per[r["Dispatch_Id"]][r["Counter_Name"]] = per[r["Dispatch_Id"]].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    for dd in per.values():
-        for k, v in dd.items():
-            tot[k] += v
-            cnt[k] += 1
+        k = fam(r["Kernel_Name"])
+        if k:
+            key = (k, r["Dispatch_Id"])
+            per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    for (k, _), dd in per.items():
+        for c, v in dd.items():
+            tot[(k, c)] += v
+            cnt[(k, c)] += 1
+durs = collections.defaultdict(list)
 for f in sorted(glob.glob(root + "/p*/run_kernel_trace.csv"))[:1]:
-    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(open(f)) if "assemble" in r["Kernel_Name"]]
-avg = {k: tot[k] / cnt[k] for k in tot}
-us = sorted(dur)[len(dur) // 2] if dur else float("nan")
+    for r in csv.DictReader(open(f)):
+        k = fam(r["Kernel_Name"])
+        if k:
+            durs[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+med = {k: sorted(v)[len(v) // 2] for k, v in durs.items()}
+for k in KB:
+    if k in med:
+        print("  %-17s median %.1f us over %d dispatches" % (k, med[k], len(durs[k])))
+avg = collections.defaultdict(float)
+for (k, c), v in tot.items():
+    avg[c] += v / cnt[(k, c)]        # per build: the sum over its kernels of each one's per-dispatch mean
+dur = [d for v in durs.values() for d in v]
+us = sum(med.values()) if med else float("nan")
 we = elements / 64.0   # wave-elements (one element per lane)
-print("assemble_kernel, N = %d, D = %d: %d dispatches, median %.1f us, %.3g elements" % (n, d, len(dur), us, elements))
+print("K build (all its kernels), N = %d, D = %d: %.1f us (sum of medians), %.3g elements" % (n, d, us, elements))
 for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
     if k in avg:
         print("  %-14s %.4g per dispatch = %.1f per element (per lane)" % (k, avg[k], avg[k] / we))

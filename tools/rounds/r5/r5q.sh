@@ -1,0 +1,21 @@
+# round 5: fast kernel takes diagonal and tail tiles too -- tests, A/B (GPK_ASM_FEAT=0), PMC
+set -o pipefail
+O=gpurun_out/r5q; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -q --timeout 150 --timeout-method thread tests/test_gpu_kbuild_pair.py \
+  tests/test_gpu_kbuild.py tests/test_gpu_parity.py tests/test_gpu_properties.py -m gpu > $O/tests.log 2>&1
+rc=$?; grep -E "passed|failed|FAILED|pair MFMA" $O/tests.log | tail -25
+[ $rc -eq 124 ] || [ $rc -eq 134 ] || [ $rc -eq 137 ] || [ $rc -eq 139 ] && exit $rc
+for f in 1 0 1 0; do
+  echo "feat=$f $(GPK_ASM_FEAT=$f timeout -k 10 200 python tools/bench_kbuild.py C5 2>&1 | grep '^{' | cut -c1-140)" | tee -a $O/ab.txt
+done
+export TMPDIR=/tmp
+KB=$O/pmc; mkdir -p $KB; i=0
+while read -r grp; do
+  [ -z "$grp" ] && continue
+  i=$((i+1))
+  [ $i -eq 3 ] && continue
+  timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$(pwd)/$KB/p$i" -o run -- python tools/bench_kbuild.py C5 > $KB/p$i.log 2>&1 || exit 1
+done < tools/pmc_kbuild.txt
+python tools/pmc_kbuild_summary.py $KB 16384 8 > $KB/summary.txt 2>&1; cat $KB/summary.txt
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$(pwd)/$O/stats" -o run -- python tools/bench_kbuild.py C5 > $O/stats.log 2>&1 || exit 1
+exit $rc
