@@ -547,13 +547,16 @@ __device__ __forceinline__ void lower_tile(const AsmArgs& a, int64_t t, int64_t&
 // 1 - 2 sin^2(pi f_k), S_k = 2 sin(pi f_k) cos(pi f_k) of the periodic leaf's f_k = x_k / p - rint(x_k / p), the
 // same operations, in the same order, as stage_points + per_feature + the per-tile norm loop -- and the block's
 // (max |u|^2, every |x_k / p| <= SC_MAX_U) for the tile kernel's bounds.  Points are classified as in
-// stage_points (training rows of X, test rows of Xs, zeros elsewhere).
+// stage_points (training rows of X, test rows of Xs, zeros elsewhere).  256 threads per block: the four waves
+// split the dimensions (the sin / cos and the ARD quotients), wave 0 then sums the norms in dimension order.
 template <int D>
-__global__ __launch_bounds__(64) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a, int se_node, int per_node) {
+__global__ __launch_bounds__(256) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a, int se_node, int per_node) {
 #pragma clang fp contract(on)
   constexpr int FS = 3 * D + 2;
+  __shared__ double us[ATILE][D + 1];
   const int b = blockIdx.y;
-  const int64_t g = (int64_t)blockIdx.x * ATILE + threadIdx.x;
+  const int pt = threadIdx.x & (ATILE - 1), grp = threadIdx.x >> 6;  // point, dimensions grp, grp + 4, ...
+  const int64_t g = (int64_t)blockIdx.x * ATILE + pt;
   const double* hyp = a.hyp + (int64_t)b * a.hyp_stride;
   const gpk_node se = kd.nodes[se_node], pq = kd.nodes[per_node];
   const bool ard = (se.flags & GPK_NODE_ARD) != 0;
@@ -563,13 +566,12 @@ __global__ __launch_bounds__(64) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a, 
   if (c == CLS_TRAIN) src = a.X + (int64_t)b * a.x_bs + g * a.d;
   else if (c == CLS_TEST && a.E == nullptr && !a.eye) src = a.Xs + (int64_t)b * a.xs_bs + (g - a.n_pad) * a.d;
   double* f = const_cast<double*>(a.feat) + (int64_t)b * a.feat_bs + g * FS;
-  double nrm = 0.0;
   bool ok = true;
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
+  for (int k = grp; k < D; k += 4) {
     const double v = src ? src[k] : 0.0;
     const double u = ard ? v / hyp[se.hyp_offset + k] : v;
-    nrm = fma(u, u, nrm);
+    us[pt][k] = u;
     f[k] = u;
     const double t = v * iper;
     ok = ok && fabs(t) <= SC_MAX_U;
@@ -578,12 +580,16 @@ __global__ __launch_bounds__(64) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a, 
     f[D + k] = fma(-2.0 * sv, sv, 1.0);
     f[2 * D + k] = 2.0 * (sv * cv);
   }
+  const bool all_ok = __syncthreads_and(ok) != 0;
+  if (threadIdx.x >= ATILE) return;
+  double nrm = 0.0;  // (in dimension order: the staged path's norm bit for bit)
+#pragma unroll
+  for (int k = 0; k < D; ++k) nrm = fma(us[pt][k], us[pt][k], nrm);
   f[3 * D] = nrm;
   f[3 * D + 1] = 0.0;
   double mx = nrm;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-  const bool all_ok = __all(ok);
   if (threadIdx.x == 0) {
     double* x = const_cast<double*>(a.faux) + 2 * ((int64_t)b * gridDim.x + blockIdx.x);
     x[0] = mx;
@@ -618,8 +624,11 @@ __global__ __launch_bounds__(64) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a, 
 // Every other tile (the diagonal, edge tiles, tiles outside the bounds) is appended to the tile list for the general
 // instantiation.  No class logic, no staging, no sin / cos: ~31 VALU operations per element with ADD (two exps of
 // 14), ~17 with MUL -- a kernel of its own, so that none of the general path's registers weigh on it.
+#ifndef GPK_FAST_MINB
+#define GPK_FAST_MINB 4  // pair_fast_kernel: workgroups per CU the register allocation must allow (A/B)
+#endif
 template <int D, bool MUL>
-__global__ __launch_bounds__(256, 3) void pair_fast_kernel(gpk_kdesc kd, AsmArgs a) {
+__global__ __launch_bounds__(256, GPK_FAST_MINB) void pair_fast_kernel(gpk_kdesc kd, AsmArgs a) {
 #pragma clang fp contract(on)
   constexpr int FS = 3 * D + 2, SS = D / 4, PS = 2 * D / 4;
   __shared__ __attribute__((aligned(16))) double fr[ATILE * FS];
@@ -1580,13 +1589,13 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
       const bool mul = kd.nodes[2].op == GPK_OP_MUL;
       const dim3 fgrid((unsigned)a.ntile, (unsigned)batch, 1);
       if (a.d == 8) {
-        hipLaunchKernelGGL((pair_feat_kernel<8>), fgrid, dim3(64), 0, s, kd, af, 1 - q, q);
+        hipLaunchKernelGGL((pair_feat_kernel<8>), fgrid, dim3(256), 0, s, kd, af, 1 - q, q);
         if (mul)
           hipLaunchKernelGGL((pair_fast_kernel<8, true>), grid, dim3(256), 0, s, kd, af);
         else
           hipLaunchKernelGGL((pair_fast_kernel<8, false>), grid, dim3(256), 0, s, kd, af);
       } else {
-        hipLaunchKernelGGL((pair_feat_kernel<4>), fgrid, dim3(64), 0, s, kd, af, 1 - q, q);
+        hipLaunchKernelGGL((pair_feat_kernel<4>), fgrid, dim3(256), 0, s, kd, af, 1 - q, q);
         if (mul)
           hipLaunchKernelGGL((pair_fast_kernel<4, true>), grid, dim3(256), 0, s, kd, af);
         else
