@@ -41,6 +41,14 @@ DEFAULT_PIPELINE_METRIC = 2
 # C5 38.2 -> 38.7 evals/s against 3, C4 flat; 5, 6 and 8 measured slower than 4 on C2 (785, 924, 1135) with 4, 8
 # or 16 hardware queues alike
 DEFAULT_PIPELINE_OTHER = 4
+# one f64 candidate per step where the persistent factorisation applies (C2, N <= 12288): 8 persistent launches in
+# flight, each on 3/16 of the CUs (chain_grid 48 of 256) -- 1594-1619 evals/s against 1343-1347 for the launch path
+# at 4 in flight; 6 x 42 1510, 4 x 64 1549, 8 x 32 / 40 1595-1605, 10 / 12 / 16 in flight collapse to ~850 (more
+# streams than the 8 hardware queues), profiles/r05u_c2_concurrent_persistent.txt, r05v_c2_persistent_sweep.txt.
+# (Before round 5 every persistent run was verified with a host synchronisation inside run(), which serialised
+# them: r04ae measured no overlap.)
+PERSIST_PIPELINE = 8
+PERSIST_CU_SHARE = 3.0 / 16.0
 
 CONFIGS = {
     # name: (kernel, d, n, noise, dtype, hyp)
@@ -426,8 +434,11 @@ def main():
     # --pipeline P: P factorisation buffers on P streams, consecutive steps round-robin over them,
     # so that one batch's exposed panel chain (start and tail of the factorisation) overlaps the
     # trailing updates of the next (the batches are independent candidate sets of the sweep)
+    persist = (args.pipeline is None and args.chain is None and not grad_mode and not sweep and batch == 1 and
+               dtn == "f64" and n <= 12288)
     P = max(1, args.pipeline if args.pipeline is not None else
-            (DEFAULT_PIPELINE_METRIC if args.config == "metric" else DEFAULT_PIPELINE_OTHER))
+            (DEFAULT_PIPELINE_METRIC if args.config == "metric" else
+             PERSIST_PIPELINE if persist else DEFAULT_PIPELINE_OTHER))
     la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 2)
     nat.tune("lookahead", la)
     # batches overlapping on P > 1 streams: the panel solve stays a separate launch (fused, its redundant
@@ -436,7 +447,15 @@ def main():
         nat.tune("fuse_trsm", args.fuse_trsm if args.fuse_trsm is not None else 0)
     # the persistent factorisation keeps one workgroup per CU for the whole evaluation: with P > 1
     # batches in flight the launch path's kernels share the chip better
-    if args.chain is not None or P > 1:
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    chain_grid = 0
+    if persist:
+        # P persistent launches side by side, each claiming its share of the CUs (no launch waits for another's
+        # workgroups: each one's tasks only ever wait for tasks claimed earlier in its own list)
+        chain_grid = max(1, int(round(ncu * PERSIST_CU_SHARE)))
+        nat.tune("chain", 2)
+        nat.tune("chain_grid", chain_grid)
+    elif args.chain is not None or P > 1:
         nat.tune("chain", args.chain if args.chain is not None else 0)
     if grad_mode:
         facts = [engine.InverseFactorization(n, d, batch, dt) for _ in range(P)]
@@ -550,6 +569,21 @@ def main():
                     "algorithmic_gflop_per_launch": round(up["flops"] / max(1, up["launches"]) / 1e9, 4),
                     "algorithmic_bytes_per_launch": round(up["bytes"] / max(1, up["launches"])),
                     "overlapped_achieved": round(ov["flops"] / (ov["ms"] * 1e-3) / 1e12, 3) if ov["ms"] > 0 else None}
+            if persist and ov["launches"] > 0 and ov["ms"] > 0:
+                # the persistent launches (timing class "update": the whole factorisation is one chain_kernel
+                # launch) as they run in the timed schedule, P side by side: each launch's algorithmic flops /
+                # its own HIP-event span, against the fp64 MFMA peak of the CUs it holds
+                ach_l = ov["flops"] / (ov["ms"] * 1e-3) / 1e12
+                peak_l = PEAK[dtn] * chain_grid / ncu
+                roof.update({"achieved": round(ach_l, 3), "peak": round(peak_l, 3), "frac": round(ach_l / peak_l, 4),
+                             "kernel": "chain_kernel (persistent factorisation, %d workgroups = %d of %d CUs, f64 "
+                                       "MFMA tiles)" % (chain_grid, chain_grid, ncu),
+                             "measured_in": "%d-step events pass of the timed schedule (%d launches in flight); peak "
+                                            "scaled to the launch's CU share" % (args.roofline_steps, P),
+                             "launches_per_step": ov["launches"] // args.roofline_steps,
+                             "avg_launch_us": round(ov["ms"] * 1e3 / ov["launches"], 2),
+                             "algorithmic_gflop_per_launch": round(ov["flops"] / ov["launches"] / 1e9, 4),
+                             "isolated_achieved": round(ach, 3), "chip_achieved": round(f_lml * value / 1e12, 3)})
             asm = timing["assemble"]
             ia = iso["assemble"]
             if ia["launches"] > 0 and ia["ms"] > 0:
@@ -604,9 +638,12 @@ def main():
                                     % (args.config, kname, d, n, noise, batch)),
                        "candidates_per_rank_step": batch,
                        "batches_in_flight": P,
-                       "schedule": ("consecutive steps rotate over %d factorisation buffers on %d HIP streams (one "
-                                    "batch's panel chain overlaps the next batch's trailing updates), panel "
-                                    "look-ahead %s" % (P, P, {0: "off", 1: "on"}.get(la, "auto"))),
+                       "schedule": (("consecutive steps rotate over %d factorisation buffers on %d HIP streams, "
+                                     "each factorisation ONE persistent launch on %d of the %d CUs (%d in flight side "
+                                     "by side)" % (P, P, chain_grid, ncu, P)) if persist else
+                                    ("consecutive steps rotate over %d factorisation buffers on %d HIP streams (one "
+                                     "batch's panel chain overlaps the next batch's trailing updates), panel "
+                                     "look-ahead %s" % (P, P, {0: "off", 1: "on"}.get(la, "auto")))),
                        "n": n, "d": d, "kernel": kname, "panel": int(lay.nb), "parallelism": "dp%d (independent candidates)" % world},
             "roofline": roof,
             "kbuild_roofline": roof_k,

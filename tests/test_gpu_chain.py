@@ -155,6 +155,28 @@ def test_chain_on_concurrent_streams():
         assert np.array_equal(_lower(out[n]).view(np.uint64), ref[n].view(np.uint64))
 
 
+def test_persistent_launches_side_by_side_on_cu_shares():
+    """bench.py's C2 schedule: 8 persistent launches in flight on 8 streams, each with 3/16 of the CUs as its grid
+    (chain_grid), the runs not verified until read (no synchronisation between them).  Each reproduces the launch
+    path bit for bit, whatever the others do meanwhile."""
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    n, hyps = 2600, [0.05 + 0.01 * i for i in range(8)]
+    ref = [_lower(_run(n, 0, 0, hyp=h)[0]) for h in hyps]
+    streams = [torch.cuda.Stream() for _ in hyps]
+    runs = []
+    with engine.nat.thread_tune(chain_grid=max(1, ncu * 3 // 16)):
+        before = engine.nat.chain_stats()["launches"]
+        for rep in range(2):
+            for s, h in zip(streams, hyps):
+                with torch.cuda.stream(s):
+                    runs.append(_run(n, 0, 1, hyp=h, sync=False)[0])
+        assert engine.nat.chain_stats()["launches"] - before == 2 * len(hyps)
+    torch.cuda.synchronize()
+    for i, f in enumerate(runs):
+        assert int(f.info.cpu()[0]) == 0
+        assert np.array_equal(_lower(f).view(np.uint64), ref[i % len(hyps)].view(np.uint64)), i
+
+
 def test_timed_out_wait_falls_back_to_the_launch_path():
     """gpk_tune("chain_force_timeout", 1): the next persistent launch reports a timeout at its first wait
     (info = -1, W left half factored).  The same run() call re-assembles and factors on the launch path and
