@@ -405,8 +405,13 @@ int gpk_timing_reset(void);
  * factorisation this library enqueued on another stream of the device is still in flight (each
  * persistent launch claims every CU); 2 always; 0 never), with "chain_group" panels per deferred tile update
  * (0, the default: 4 below 80 diagonal blocks, 8 from there), "chain_uq" (1: the next diagonal block's update by each panel as 32-column quarter tasks; 0: one task
- * per 32-row slice) and, for batches, "chain_max_batch" members (8) while batch x p <= "chain_batch_max_rows"
- * (17500).
+ * per 32-row slice; 2: slice r's panel solve and the next diagonal block's quarter updates as one task) and, for
+ * batches, "chain_max_batch" members (8) while batch x p <= "chain_batch_max_rows" (17500).  Several persistent
+ * launches may run side by side on different streams, each with "chain_grid" workgroups (a CU share): no launch
+ * waits for another's workgroups (bench.py's C2 schedule: 8 in flight at 3/16 of the CUs each).
+ * "asm_feat" (1: the K build of a two-leaf SE + periodic tree at D = 4 or 8 computes the per-point features in a
+ * pre-pass and runs its interior tiles on the f64 MFMA fast-tile kernel; 0: every tile stages its points itself
+ * -- the same bits, slower; A/B).
  * A persistent launch whose wait timed out
  * sets info = -1 -- an infrastructure failure, not a non-positive pivot: the factorisation is
  * incomplete and W undefined; re-assemble and re-run it with "chain" 0 (the Python layer does,
@@ -438,8 +443,9 @@ int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_ou
 /* gpk_chain_plan with flags: GPK_AUG_EXTRA_IDENTITY plans the identity-augmented factorisation (gpk_potrf_aug_ex,
  * gpk_nlml_grad; y_row = n_pad + n): tasks that would only move the structurally zero parts of E L^-T are left
  * out, and a task word with bit 6 set updates cells no earlier task updated (its counter wait is for 0).  The
- * type word: type (bits 0..1) | (g - 1) << 2 (type 3: an update over the g panels k .. k + g - 1; type 2 with
- * g > 1: the 32 x 32 quarter g - 2 of slice r in diagonal block j) | bit 6. */
+ * type word: type (bits 0..1) | (g - 1) << 2 (bits 2..5; type 3: an update over the g panels k .. k + g - 1;
+ * type 2 with g > 1: the 32 x 32 quarter g - 2 of slice r in diagonal block j) | bit 6 | bit 7 (an SQ task of
+ * "chain_uq" 2: the slice's panel solve, then the next diagonal block's quarter updates) | member << 8. */
 int gpk_chain_plan_ex(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, int32_t* tasks_out, int64_t cap,
                       int64_t* ntasks);
 
