@@ -478,8 +478,11 @@ def main():
             else:
                 f.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
             if use_dist:
-                mine[i][:batch] = f.nlml()
-                mine[i][chunk:chunk + batch] = f.info.to(torch.float64)
+                # (device views, no settle: a persistent run is not waited for here; a timed-out one would
+                # arrive as info = -1 and fail the all-gather check)
+                nl_dev, info_dev = f.unsettled_results()
+                mine[i][:batch] = nl_dev
+                mine[i][chunk:chunk + batch] = info_dev.to(torch.float64)
                 dist.all_gather_into_tensor(gathered[i], mine[i])
 
     for _ in range(args.warmup):

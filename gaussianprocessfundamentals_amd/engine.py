@@ -308,6 +308,12 @@ class AugmentedFactorization:
     def nlml(self) -> torch.Tensor:
         return self.out.view(self.batch, 4)[:, 0]
 
+    def unsettled_results(self):
+        """(-LML, info) device views WITHOUT settling a pending persistent run (no host synchronisation): for callers
+        that pipeline runs and only forward the values on the device -- a wait that timed out shows as info = -1
+        there, and the run is not re-done.  Everyone else reads nlml() / info."""
+        return self._out.view(self.batch, 4)[:, 0], self._info
+
     def fit(self) -> torch.Tensor:
         return self.out.view(self.batch, 4)[:, 1]
 

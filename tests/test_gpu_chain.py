@@ -177,6 +177,16 @@ def test_persistent_launches_side_by_side_on_cu_shares():
         assert np.array_equal(_lower(f).view(np.uint64), ref[i % len(hyps)].view(np.uint64)), i
 
 
+def test_unsettled_results_are_the_settled_ones():
+    """unsettled_results() (bench.py's per-step all-gather) reads the device buffers without waiting for the run:
+    after the stream drains they hold what nlml() / info return once settled."""
+    f, _ = _run(3000, 0, 1, sync=False)
+    nl, info = f.unsettled_results()
+    nl, info = nl.clone(), info.clone()   # (stream-ordered copies)
+    torch.cuda.synchronize()
+    assert torch.equal(nl, f.nlml()) and torch.equal(info, f.info)
+
+
 def test_timed_out_wait_falls_back_to_the_launch_path():
     """gpk_tune("chain_force_timeout", 1): the next persistent launch reports a timeout at its first wait
     (info = -1, W left half factored).  The same run() call re-assembles and factors on the launch path and
