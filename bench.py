@@ -42,13 +42,14 @@ DEFAULT_PIPELINE_METRIC = 2
 # or 16 hardware queues alike
 DEFAULT_PIPELINE_OTHER = 4
 # one f64 candidate per step where the persistent factorisation applies (C2, N <= 12288): 8 persistent launches in
-# flight, each on 3/16 of the CUs (chain_grid 48 of 256) -- 1594-1619 evals/s against 1343-1347 for the launch path
-# at 4 in flight; 6 x 42 1510, 4 x 64 1549, 8 x 32 / 40 1595-1605, 10 / 12 / 16 in flight collapse to ~850 (more
-# streams than the 8 hardware queues), profiles/r05u_c2_concurrent_persistent.txt, r05v_c2_persistent_sweep.txt.
-# (Before round 5 every persistent run was verified with a host synchronisation inside run(), which serialised
-# them: r04ae measured no overlap.)
+# flight, each with a quarter of the CUs as its grid (chain_grid 64 of 256: four run at a time, the next ones start
+# as CUs free up) -- 1695-1714 evals/s against 1343-1347 for the launch path at 4 in flight; 8 x 48 1594-1619,
+# 8 x 56 / 80 / 96 / 128 1582 / 1614 / 1623 / 1562, 6 x 64 1707, 4 x 64 1549, 10 / 12 / 16 in flight collapse to
+# ~850 (more streams than the 8 hardware queues), profiles/r05u_*, r05v_*, r05ac_*, r05ad_*.  (Before round 5
+# every persistent run was verified with a host synchronisation inside run(), which serialised them: r04ae
+# measured no overlap.)
 PERSIST_PIPELINE = 8
-PERSIST_CU_SHARE = 3.0 / 16.0
+PERSIST_CU_SHARE = 1.0 / 4.0
 
 CONFIGS = {
     # name: (kernel, d, n, noise, dtype, hyp)
