@@ -41,8 +41,9 @@ def _noise_float(noise) -> float:
 
 def noise_vector(noise) -> torch.Tensor:
     """Rank-0 noise as a 1-element fp64 device vector (no host round trip for device tensors)."""
-    t = noise if isinstance(noise, torch.Tensor) else torch.tensor(float(noise), dtype=torch.float64)
-    return t.detach().to(device=engine.device(), dtype=torch.float64).reshape(1)
+    if not isinstance(noise, torch.Tensor) or (noise.device.type == "cpu" and not noise.requires_grad):
+        return engine.host_f64_to_device([float(noise)])
+    return noise.detach().to(device=engine.device(), dtype=torch.float64).reshape(1)
 
 
 class CovarianceMatrix:

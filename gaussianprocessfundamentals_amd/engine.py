@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -91,6 +92,21 @@ def kernel_descriptor(kernel, dim: Optional[int] = None) -> nat.GpkKdesc:
     return kd
 
 
+# small host values (hyperparameters, noise) reach the device through one asynchronous copy from pinned memory
+# (torch's caching host allocator keeps the block until the copy is done) instead of a synchronous pageable copy
+# per tensor; GPK_PINNED_H2D=0 restores the plain copy (A/B)
+PINNED_H2D = os.environ.get("GPK_PINNED_H2D", "1") != "0"
+
+
+def host_f64_to_device(values) -> torch.Tensor:
+    """fp64 device vector of a short list of host floats (asynchronous, stream-ordered on the current stream)."""
+    t = torch.tensor(values, dtype=torch.float64)
+    dev = device()
+    if PINNED_H2D and dev.type == "cuda":
+        return t.pin_memory().to(dev, non_blocking=True)
+    return t.to(dev)
+
+
 def pack_hyper_parameter(hyper_parameter: Sequence, n_expected: Optional[int] = None) -> torch.Tensor:
     """Flat fp64 device vector of a hyperparameter list (each entry reshaped to [-1], concatenated;
     BasicGPComponent.serialize_hyper_parameter, gpbasics/Auxiliary/BasicGPComponent.py:16-23)."""
@@ -114,7 +130,7 @@ def pack_hyper_parameter(hyper_parameter: Sequence, n_expected: Optional[int] = 
                         host_vals.extend(float(v) for v in h)
                     except TypeError:
                         host_vals.append(float(h))
-            flat = torch.tensor(host_vals, dtype=torch.float64, device=dev)
+            flat = host_f64_to_device(host_vals)
         else:
             for h in hyper_parameter:
                 parts.append(torch.as_tensor(h).to(device=dev, dtype=torch.float64).reshape(-1))
