@@ -472,15 +472,35 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   // block i holds a nonzero row in the columns of panel q (monotone in q): from panel live_from(i) on
   auto live_from = [&](int i) { return (!eye || i < nblk || i == yb) ? 0 : i - nblk; };
   auto live = [&](int i, int q) { return live_from(i) <= q; };
+  // (flat storage: the lists reach 70 000+ tasks for the identity-augmented N = 8192 -- a vector per task's
+  // dependencies and a map per tile made the first call of a shape cost ~30 ms of host time there)
+  constexpr int MAXDEP = 16;  // D: up to 10 quarter tasks; BLK: 4 + 4 slices + the tile's last update
   struct Task {
     int ty, k, r, j;
     float dur;
-    std::vector<int> deps;
+    int nd;
+    int deps[MAXDEP];
+    void dep(int d) {
+      if (nd < MAXDEP) deps[nd] = d;
+      ++nd;
+    }
   };
   std::vector<Task> T;
+  T.reserve(4096);
   const int nr = rlast + 1;
   std::vector<int> D(nblk, -1), S((size_t)nblk * nr, -1), U((size_t)nblk * nr, -1);
-  std::map<std::pair<int, int>, int> last_upd;  // tile (i, j) -> its latest update task so far
+  const int nbt = yb + 1;
+  std::vector<int> last_upd((size_t)nbt * nbt, -1);  // tile (i, j) -> its latest update task so far
+  auto mk = [](int ty, int k, int r, int j, float du) {
+    Task t;
+    t.ty = ty;
+    t.k = k;
+    t.r = r;
+    t.j = j;
+    t.dur = du;
+    t.nd = 0;
+    return t;
+  };
   auto s_of = [&](int k, int r) { return S[(size_t)k * nr + r]; };
   auto u_of = [&](int k, int r) { return U[(size_t)k * nr + r]; };
   // list-scheduling durations (us) of D / S / U32 / BLK: the measured per-task run times
@@ -497,8 +517,12 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   const int Gc = std::max(1, std::min<int>((int)env_i64("GPK_CHAIN_GROUP_CORNER", 16), 16));
   const int tail_c = (int)std::max<int64_t>(0, env_i64("GPK_CHAIN_CORNER_TAIL", 8));
   const int LA = (int)std::max<int64_t>(1, env_i64("GPK_CHAIN_GROUP_LA", 2));
-  auto add = [&](Task t) {
-    T.push_back(std::move(t));
+  auto add = [&](const Task& t) {
+    if (t.nd > MAXDEP) {  // (unreachable: the graph's in-degrees are bounded by construction)
+      fprintf(stderr, "libgpk: chain_order: a task with %d dependencies (at most %d)\n", t.nd, MAXDEP);
+      abort();
+    }
+    T.push_back(t);
     return (int)T.size() - 1;
   };
   // BLK tasks carry ty = 3 | (g - 1) << 2 for an update over the g panels k .. k + g - 1
@@ -512,30 +536,30 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
       g -= f - q0;
       q0 = f;
     }
-    Task t{CHT_BLK | ((g - 1) << 2), q0, i, jj, dur[3] * (0.25f + 0.75f * (float)g), {}};
-    for (int s = 4 * i; s <= std::min(4 * i + 3, rlast); ++s) t.deps.push_back(s_of(ql, s));
+    Task t = mk(CHT_BLK | ((g - 1) << 2), q0, i, jj, dur[3] * (0.25f + 0.75f * (float)g));
+    for (int s = 4 * i; s <= std::min(4 * i + 3, rlast); ++s) t.dep(s_of(ql, s));
     if (jj != i)
-      for (int s = 4 * jj; s <= std::min(4 * jj + 3, rlast); ++s) t.deps.push_back(s_of(ql, s));
-    auto it = last_upd.find({i, jj});
-    if (it != last_upd.end())
-      t.deps.push_back(it->second);
+      for (int s = 4 * jj; s <= std::min(4 * jj + 3, rlast); ++s) t.dep(s_of(ql, s));
+    int& lu = last_upd[(size_t)i * nbt + jj];
+    if (lu >= 0)
+      t.dep(lu);
     else if (q0 > 0)
       t.ty |= kChainFirst;
-    last_upd[{i, jj}] = add(t);
+    lu = add(t);
   };
   // the next diagonal block's update by panel k, split by 32-column quarter (UQ: U32 with the quarter + 1 in
   // the type word's bits 2..7): 10 tasks of 32 x 32 x 128 on the chain to D(k + 1) instead of 4 of 32 x 128 x
   // 128, each loading 64 KB of panel instead of 160 (chain_uq; 0: one U32 per slice)
   const bool uq = chain_uq != 0, sq = chain_uq == 2;
-  std::map<int, std::vector<int>> uq_of;  // slice s of diagonal block k + 1 -> its UQ tasks (panel k)
+  std::vector<std::vector<int>> uq_of(nr);  // slice s of diagonal block k + 1 -> its UQ tasks (panel k)
   for (int k = 0; k < nblk; ++k) {
-    Task d{CHT_D, k, 0, k, dur[0], {}};
+    Task d = mk(CHT_D, k, 0, k, dur[0]);
     if (k > 0)
       for (int s = 4 * k; s <= std::min(4 * k + 3, rlast); ++s) {
         if (uq)
-          for (int t : uq_of[s]) d.deps.push_back(t);
+          for (int t : uq_of[s]) d.dep(t);
         else
-          d.deps.push_back(u_of(k - 1, s));
+          d.dep(u_of(k - 1, s));
       }
     D[k] = add(d);
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
@@ -543,15 +567,16 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
       // chain_uq 2: the next diagonal block's slices take SQ tasks -- the panel solve followed by the slice's lower
       // quarters of that block (chain_sq), which need the siblings' solved rows (claimed before: lower slices first)
       const bool sqt = sq && k + 1 < nblk && r < 4 * (k + 2);
-      Task t{CHT_S | (sqt ? kChainSq : 0), k, r, 0, dur[1] + (sqt ? dur[2] * 0.5f : 0.f), {D[k]}};
+      Task t = mk(CHT_S | (sqt ? kChainSq : 0), k, r, 0, dur[1] + (sqt ? dur[2] * 0.5f : 0.f));
+      t.dep(D[k]);
       if (k > 0 && live(r / 4, k - 1))
-        t.deps.push_back(u_of(k - 1, r));
+        t.dep(u_of(k - 1, r));
       else if (k > 0)
         t.ty |= kChainFirst;  // (the slice's first live panel: nothing updated it before)
       if (sqt) {
-        auto it = last_upd.find({k + 1, k + 1});
-        if (it != last_upd.end()) t.deps.push_back(it->second);
-        for (int q = 4 * (k + 1); q < r; ++q) t.deps.push_back(s_of(k, q));
+        const int lu = last_upd[(size_t)(k + 1) * nbt + (k + 1)];
+        if (lu >= 0) t.dep(lu);
+        for (int q = 4 * (k + 1); q < r; ++q) t.dep(s_of(k, q));
       }
       S[(size_t)k * nr + r] = add(t);
       if (sqt) {
@@ -562,23 +587,25 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
       if (!live(r / 4, k)) continue;
       if (sq && k + 1 < nblk && r < 4 * (k + 2)) continue;  // (done by the slice's SQ task)
-      auto it = last_upd.find({r / 4, k + 1});
-      const int first = (it == last_upd.end() && k > 0) ? kChainFirst : 0;
+      const int lu = last_upd[(size_t)(r / 4) * nbt + (k + 1)];
+      const int first = (lu < 0 && k > 0) ? kChainFirst : 0;
       if (uq && k + 1 < nblk && r < 4 * (k + 2)) {
         const int rl = r - 4 * (k + 1);
         for (int q = 0; q <= rl; ++q) {  // lower quarters of the diagonal block's slice r
-          Task t{CHT_U32 | ((q + 1) << 2) | first, k, r, k + 1, dur[2] * 0.5f, {s_of(k, r)}};
-          if (q != rl) t.deps.push_back(s_of(k, 4 * (k + 1) + q));
-          if (it != last_upd.end()) t.deps.push_back(it->second);
+          Task t = mk(CHT_U32 | ((q + 1) << 2) | first, k, r, k + 1, dur[2] * 0.5f);
+          t.dep(s_of(k, r));
+          if (q != rl) t.dep(s_of(k, 4 * (k + 1) + q));
+          if (lu >= 0) t.dep(lu);
           uq_of[r].push_back(add(t));
         }
         U[(size_t)k * nr + r] = uq_of[r].back();  // (not read: D(k + 1) waits for every quarter)
         continue;
       }
-      Task t{CHT_U32 | first, k, r, k + 1, dur[2], {s_of(k, r)}};
+      Task t = mk(CHT_U32 | first, k, r, k + 1, dur[2]);
+      t.dep(s_of(k, r));
       for (int s = 4 * (k + 1); s <= std::min(4 * (k + 1) + 3, rlast); ++s)
-        if (s != r) t.deps.push_back(s_of(k, s));
-      if (it != last_upd.end()) t.deps.push_back(it->second);
+        if (s != r) t.dep(s_of(k, s));
+      if (lu >= 0) t.dep(lu);
       U[(size_t)k * nr + r] = add(t);
     }
     for (int jj = k + 2; jj <= yb; ++jj) {
@@ -616,22 +643,26 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
       for (int t = 0; t < n1; ++t) {
         Task c = T[t];
         c.ty |= m << 8;
-        for (int& dd : c.deps) dd += m * n1;
-        T.push_back(std::move(c));
+        for (int e = 0; e < c.nd; ++e) c.deps[e] += m * n1;
+        T.push_back(c);
       }
   }
   const int n = (int)T.size();
-  std::vector<std::vector<int>> succ(n);
-  std::vector<int> indeg(n, 0);
+  // successors in CSR form, each task's in the order its dependants were built
+  std::vector<int> indeg(n, 0), soff(n + 1, 0);
   for (int t = 0; t < n; ++t)
-    for (int d : T[t].deps) {
-      succ[d].push_back(t);
+    for (int e = 0; e < T[t].nd; ++e) ++soff[T[t].deps[e] + 1];
+  for (int t = 0; t < n; ++t) soff[t + 1] += soff[t];
+  std::vector<int> succ(soff[n]), fill(soff.begin(), soff.end() - 1);
+  for (int t = 0; t < n; ++t)
+    for (int e = 0; e < T[t].nd; ++e) {
+      succ[fill[T[t].deps[e]]++] = t;
       ++indeg[t];
     }
   std::vector<float> bl(n, 0.f);
   for (int t = n - 1; t >= 0; --t) {  // the construction order is topological
     float m = 0.f;
-    for (int s : succ[t]) m = std::max(m, bl[s]);
+    for (int e = soff[t]; e < soff[t + 1]; ++e) m = std::max(m, bl[succ[e]]);
     bl[t] = T[t].dur + m;
   }
   auto cmp = [&](int a, int b) { return bl[a] != bl[b] ? bl[a] < bl[b] : a > b; };
@@ -656,8 +687,8 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
     ev.pop();
     now = e.first;
     ++free;
-    for (int s : succ[e.second])
-      if (--indeg[s] == 0) ready.push(s);
+    for (int x = soff[e.second]; x < soff[e.second + 1]; ++x)
+      if (--indeg[succ[x]] == 0) ready.push(succ[x]);
   }
   return out;
 }
