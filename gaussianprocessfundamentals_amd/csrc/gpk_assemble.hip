@@ -7,6 +7,11 @@
 // layout only lower-triangular tiles are launched (the factorisation never reads the upper
 // triangle), so the bytes written are p(p+64)/2 elements per batch member.
 //
+// Two-leaf SE + periodic trees at D = 4 / 8 (the C5 kernel) take three launches instead (launch_assemble):
+// pair_feat_kernel (per-point MFMA operands and norms, once per point), pair_fast_kernel (interior tiles whose
+// error bounds hold: the dot products on the f64 MFMA, a table exp in ln2 / 32 units; y-row / zero tail tiles
+// written directly; every other tile appended to a device list) and the general instantiation over that list.
+//
 // Reference semantics (paths relative to gpbasics/):
 //   SE     KernelBasics/BaseKernels.py:277-294   exp(-0.5 * (dist^2 / l^2)), sg * (..) if scaled
 //   PER    KernelBasics/BaseKernels.py:440-457   exp((-2 sin^2(pi * (d1 / p))) / l^2)
