@@ -184,6 +184,11 @@ struct Tune {
   int64_t chain_max_p_eye;  // ... while their augmented matrix has at most this many rows
   int64_t asm_feat;       // K build, two-leaf SE + periodic trees on MFMA: per-point features in a pre-pass
                           // (pair_feat_kernel; 0: staged per tile, A/B -- bitwise equal)
+  int64_t chain_min_p;    // chain = 1 (auto): the launch path below this many rows (a handful of panels: the
+                          // launch path's few launches win -- get_metric N = 128 / 256 / 384 0.119 / 0.165 / 0.216
+                          // vs 0.145 / 0.187 / 0.224 ms, equal at 512, the persistent launch ahead from 768,
+                          // profiles/r05ak_api_small_n_chain_vs_launch.jsonl)
+  int64_t chain_min_p_eye;  // ... and for identity-augmented factorisations (value + gradient)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -207,7 +212,8 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_TIMEOUT_MS", 1000), env_i64("GPK_CHAIN_GROUP", 0),
                          env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500),
                          env_i64("GPK_CHAIN_UQ", 1), env_i64("GPK_CHAIN_EYE", 1),
-                         env_i64("GPK_CHAIN_MAX_P_EYE", 16640), env_i64("GPK_ASM_FEAT", 1)};
+                         env_i64("GPK_CHAIN_MAX_P_EYE", 16640), env_i64("GPK_ASM_FEAT", 1),
+                         env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 2304)};
   return t;
 }
 
@@ -233,7 +239,8 @@ const Knob kKnobs[] = {
     {"chain_group", &Tune::chain_group},     {"chain_max_batch", &Tune::chain_max_batch},
     {"chain_batch_max_rows", &Tune::chain_batch_max_rows}, {"chain_uq", &Tune::chain_uq},
     {"chain_eye", &Tune::chain_eye},         {"chain_max_p_eye", &Tune::chain_max_p_eye},
-    {"asm_feat", &Tune::asm_feat},
+    {"asm_feat", &Tune::asm_feat},           {"chain_min_p", &Tune::chain_min_p},
+    {"chain_min_p_eye", &Tune::chain_min_p_eye},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -704,6 +711,7 @@ bool chain_applies(const gpk_layout* lay, bool eye, const int64_t* n_dev, const 
     return false;
   if (tn.diag_dbg != 0 || tn.diag_version == 1) return false;
   if (!plain_stream(s)) return false;
+  if (tn.chain == 1 && lay->p < (eye ? tn.chain_min_p_eye : tn.chain_min_p)) return false;
   if (tn.chain == 1 && other_stream_busy(s)) {
     ++g_chain_declined;
     return false;
