@@ -188,7 +188,9 @@ struct Tune {
                           // launch path's few launches win -- get_metric N = 128 / 256 / 384 0.119 / 0.165 / 0.216
                           // vs 0.145 / 0.187 / 0.224 ms, equal at 512, the persistent launch ahead from 768,
                           // profiles/r05ak_api_small_n_chain_vs_launch.jsonl)
-  int64_t chain_min_p_eye;  // ... and for identity-augmented factorisations (value + gradient)
+  int64_t chain_min_p_eye;  // ... and for identity-augmented factorisations (value + gradient): N = 1024 / 1280
+                            // 0.554 / 0.657 ms on the launch path vs 0.590 / 0.683, N = 1536 0.809 vs 0.786
+                            // (profiles/r05al_api_crossover.jsonl)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -213,7 +215,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500),
                          env_i64("GPK_CHAIN_UQ", 1), env_i64("GPK_CHAIN_EYE", 1),
                          env_i64("GPK_CHAIN_MAX_P_EYE", 16640), env_i64("GPK_ASM_FEAT", 1),
-                         env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 2304)};
+                         env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 3072)};
   return t;
 }
 

@@ -410,7 +410,7 @@ int gpk_timing_reset(void);
  * launches may run side by side on different streams, each with "chain_grid" workgroups (a CU share): no launch
  * waits for another's workgroups (bench.py's C2 schedule: 8 in flight, 64 workgroups each on 256 CUs).
  * With "chain" 1 (auto) factorisations of fewer than "chain_min_p" (768) rows -- identity-augmented ones:
- * "chain_min_p_eye" (2304) -- keep the launch path (a handful of panels: its few launches are faster).
+ * "chain_min_p_eye" (3072) -- keep the launch path (a handful of panels: its few launches are faster).
  * "asm_feat" (1: the K build of a two-leaf SE + periodic tree at D = 4 or 8 computes the per-point features in a
  * pre-pass and runs its interior tiles on the f64 MFMA fast-tile kernel; 0: every tile stages its points itself
  * -- the same bits, slower; A/B).
