@@ -298,6 +298,9 @@ __device__ const double kExp2Tab32[32] = {
     1.5759808451078865, 1.6104903319492543, 1.645755478153965, 1.681792830507429, 1.718619298122478,
     1.7562521603732995, 1.7947090750031072, 1.8340080864093424, 1.8741676341103, 1.9152065613971474,
     1.9571441241754002};
+#ifndef GPK_FAST_ABLATE
+#define GPK_FAST_ABLATE 0  // timing-only ablations of the fast read-out (A/B builds; wrong values)
+#endif
 #ifndef GPK_ASM_TAB_EXP
 #define GPK_ASM_TAB_EXP 1
 #endif
@@ -336,6 +339,9 @@ __device__ __forceinline__ double exp2_32(double t, const double* tab) {
   p = fma(p, sr, 0.02166084939249829);
   p = fma(p, sr, 1.0);
   const int ki = (int)k;
+#if GPK_FAST_ABLATE == 1
+  return ldexp(p, ki >> 5);  // (timing-only ablation: no table read)
+#endif
   return ldexp(tab[ki & 31] * p, ki >> 5);
 }
 
@@ -731,7 +737,14 @@ __global__ __launch_bounds__(256, GPK_FAST_MINB) void pair_fast_kernel(gpk_kdesc
         for (int i = 0; i < 4; ++i) {
           const double ts = fmin(fma(dse[h][i], a_s, hr[i] + hc), lsg_s);
           const double tp = fmin(fma(dpe[h][i], a_p, c_p), lsg_p);
+#if GPK_FAST_ABLATE == 2
+          { const double v = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
+            if (v == 12345.678) wrow[i][col] = v; }  // (timing-only ablation: no stores)
+#elif GPK_FAST_ABLATE == 3
+          wrow[i][col] = ts + tp;  // (timing-only ablation: no exps)
+#else
           wrow[i][col] = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
+#endif
         }
       }
     } else {
