@@ -625,141 +625,160 @@ __global__ __launch_bounds__(256) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a,
   }
 }
 
-// The interior off-diagonal tiles of a two-leaf SE + periodic tree whose bounds hold, from pair_feat_kernel's
-// features: one 256-thread workgroup per lower tile (the assemble grid).  The tile's 2 x 64 feature rows (contiguous
-// in HBM, L2-resident) go to LDS -- row stride 3 D + 2 doubles, so that the 16 points x 2 k-lanes of an MFMA operand
-// read hit 32 distinct bank pairs -- then wave w takes rows 16 w .. 16 w + 15 against the 64 columns: per 16 x 16
-// block D / 4 MFMAs (u_i . u_j) and D / 2 (sum_k C_ik C_jk + S_ik S_jk), then per element
+// The interior tiles of a two-leaf SE + periodic tree whose bounds hold (and the tail rows), from pair_feat_kernel's
+// features: one 256-thread workgroup per chunk of consecutive lower tiles (below).  The tile's 2 x 64 feature rows
+// (contiguous in HBM, L2-resident; the row's kept from the previous tile of the same tile row) go to LDS -- row
+// stride 3 D + 2 doubles, so that the 16 points x 2 k-lanes of an MFMA operand read hit 32 distinct bank pairs --
+// then wave w takes rows 16 w .. 16 w + 15 against the 64 columns: per 16 x 16 block D / 4 MFMAs (u_i . u_j) and
+// D / 2 (sum_k C_ik C_jk + S_ik S_jk), then per element
 //   ADD  2^(ts / 32) + 2^(tp / 32),  MUL  2^((ts + tp) / 32),
 //   ts = min(a_s dse + hr_i + hc_j, lsg_s), tp = min(a_p dpe + c_p, lsg_p)   (pair_feat_kernel's member constants)
-// Every other tile (the diagonal, edge tiles, tiles outside the bounds) is appended to the tile list for the general
-// instantiation.  No class logic, no staging, no sin / cos: ~31 VALU operations per element with ADD (two exps of
-// 14), ~17 with MUL -- a kernel of its own, so that none of the general path's registers weigh on it.
+// Edge tiles and tiles outside the bounds are appended to the tile list for the general instantiation.  No class
+// logic, no staging, no sin / cos: ~31 VALU operations per element with ADD (two exps of 14), ~17 with MUL -- a
+// kernel of its own, so that none of the general path's registers weigh on it.
 #ifndef GPK_FAST_MINB
 #define GPK_FAST_MINB 4  // pair_fast_kernel: workgroups per CU the register allocation must allow (A/B)
 #endif
+#ifndef GPK_FAST_CHUNK
+#define GPK_FAST_CHUNK 8  // pair_fast_kernel: consecutive lower tiles per workgroup (C5 K build 0.465 -> 0.450 ms)
+#endif
+// Workgroup c of member b walks the lower tiles c * chunk .. c * chunk + chunk - 1 (row-major: mostly one tile row,
+// whose feature rows it loads once); each tile as one workgroup per tile would -- the same values bit for bit.
 template <int D, bool MUL>
-__global__ __launch_bounds__(256, GPK_FAST_MINB) void pair_fast_kernel(gpk_kdesc kd, AsmArgs a) {
+__global__ __launch_bounds__(256, GPK_FAST_MINB) void pair_fast_kernel(gpk_kdesc kd, AsmArgs a, int64_t ntl,
+                                                                      int chunk) {
 #pragma clang fp contract(on)
   constexpr int FS = 3 * D + 2, SS = D / 4, PS = 2 * D / 4;
   __shared__ __attribute__((aligned(16))) double fr[ATILE * FS];
   __shared__ __attribute__((aligned(16))) double fc[ATILE * FS];
   __shared__ double tab[32];
   const int b = blockIdx.y;
-  int64_t ti, tj;
-  lower_tile(a, blockIdx.x, ti, tj);
-  const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
   const int64_t nm = member_n(a, b), mm = member_m(a, b);
-  const int tid = threadIdx.x;
-  if (gi0 >= a.n_pad + mm) {
-    // tail tiles (the y row and the zero rows below it): y^T on the y row, zeros elsewhere -- the general loop's
-    // values (CLS_Y / CLS_ZERO rows), without its staging
-    const int c = tid & 63;
-    const int64_t gj = gj0 + c;
-    const double yv = gj < nm ? a.y[(int64_t)b * a.y_bs + gj] : 0.0;
-    double* const Wc = reinterpret_cast<double*>(a.W) + (int64_t)b * a.w_bs + gj;
-    for (int rr = tid >> 6; rr < ATILE; rr += 4) Wc[(gi0 + rr) * a.ld] = gi0 + rr == a.y_row ? yv : 0.0;
-    return;
-  }
-  const double* xr = a.faux + 2 * ((int64_t)b * a.ntile + ti);
-  const double* xc = a.faux + 2 * ((int64_t)b * a.ntile + tj);
   const double* mc = a.faux + 2 * (int64_t)gridDim.y * a.ntile + 8 * b;
-  const bool fast = gi0 + ATILE <= nm && gj0 + ATILE <= nm && mc[5] != 0.0 && xr[1] != 0.0 && xc[1] != 0.0 &&
-                    (xr[0] + xc[0]) * mc[6] <= PAIR_MFMA_MAX_NORM;
-  if (!fast) {
-    if (tid == 0) {
-      int32_t* tl = const_cast<int32_t*>(a.tlist);
-      const int k = atomicAdd(tl, 1);
-      tl[1 + 3 * k] = b;
-      tl[2 + 3 * k] = (int32_t)ti;
-      tl[3 + 3 * k] = (int32_t)tj;
-    }
-    return;
-  }
   const double* fb = a.feat + (int64_t)b * a.feat_bs;
-  {
-    const double2* sr = reinterpret_cast<const double2*>(fb + gi0 * FS);
-    const double2* sc = reinterpret_cast<const double2*>(fb + gj0 * FS);
-    double2* dr = reinterpret_cast<double2*>(fr);
-    double2* dc = reinterpret_cast<double2*>(fc);
-    for (int e = tid; e < ATILE * FS / 2; e += 256) {
-      dr[e] = sr[e];
-      dc[e] = sc[e];
+  if (threadIdx.x < 32) tab[threadIdx.x] = kExp2Tab32[threadIdx.x];
+  int64_t loaded = -1;  // the tile row whose features are in fr
+  const int64_t t_end = std::min<int64_t>(ntl, ((int64_t)blockIdx.x + 1) * chunk);
+  for (int64_t t = (int64_t)blockIdx.x * chunk; t < t_end; ++t) {
+    // (the lane's offsets recomputed per tile: hoisted out of the loop they would hold registers across it)
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    int64_t ti, tj;
+    lower_tile(a, t, ti, tj);
+    const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
+    if (gi0 >= a.n_pad + mm) {
+      // tail tiles (the y row and the zero rows below it): y^T on the y row, zeros elsewhere -- the general loop's
+      // values (CLS_Y / CLS_ZERO rows), without its staging
+      const int c = tid & 63;
+      const int64_t gj = gj0 + c;
+      const double yv = gj < nm ? a.y[(int64_t)b * a.y_bs + gj] : 0.0;
+      double* const Wc = reinterpret_cast<double*>(a.W) + (int64_t)b * a.w_bs + gj;
+      for (int rr = tid >> 6; rr < ATILE; rr += 4) Wc[(gi0 + rr) * a.ld] = gi0 + rr == a.y_row ? yv : 0.0;
+      continue;
     }
-    if (tid < 32) tab[tid] = kExp2Tab32[tid];
-  }
-  const double a_s = mc[0], lsg_s = mc[1], a_p = mc[2], c_p = mc[3], lsg_p = mc[4];
-  const bool diag = ti == tj;
-  const double kself = mc[7] + (diag ? a.noise[(int64_t)b * a.noise_stride] : 0.0);
-  __syncthreads();
-  const int lane = tid & 63, w = tid >> 6;
-  const int lr = lane & 15, kq = lane >> 4;
-  double ase[SS], ape[PS];
-  const int prow_pt = 16 * w + lr;
-#pragma unroll
-  for (int t = 0; t < SS; ++t) ase[t] = fr[prow_pt * FS + 4 * t + kq];
-#pragma unroll
-  for (int t = 0; t < PS; ++t) ape[t] = fr[prow_pt * FS + D + 4 * t + kq];
-  double hr[4];
-  double* wrow[4];
-  double* const Wt = reinterpret_cast<double*>(a.W) + (int64_t)b * a.w_bs + gi0 * a.ld + gj0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    hr[i] = fma(-0.5 * a_s, fr[(16 * w + kq + 4 * i) * FS + 3 * D], lsg_s);
-    wrow[i] = Wt + (int64_t)(16 * w + kq + 4 * i) * a.ld;
-  }
-#pragma unroll 1
-  for (int cp = 0; cp < 2; ++cp) {
-    d4 dse[2], dpe[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      dse[h] = d4{0.0, 0.0, 0.0, 0.0};
-      dpe[h] = d4{0.0, 0.0, 0.0, 0.0};
-    }
-#pragma unroll
-    for (int t = 0; t < SS; ++t)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        dse[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ase[t], fc[(16 * (2 * cp + h) + lr) * FS + 4 * t + kq], dse[h],
-                                                      0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < PS; ++t)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        dpe[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ape[t], fc[(16 * (2 * cp + h) + lr) * FS + D + 4 * t + kq],
-                                                      dpe[h], 0, 0, 0);
-    if (!diag) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int col = 16 * (2 * cp + h) + lr;
-        const double hc = -0.5 * a_s * fc[col * FS + 3 * D];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const double ts = fmin(fma(dse[h][i], a_s, hr[i] + hc), lsg_s);
-          const double tp = fmin(fma(dpe[h][i], a_p, c_p), lsg_p);
-#if GPK_FAST_ABLATE == 2
-          { const double v = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
-            if (v == 12345.678) wrow[i][col] = v; }  // (timing-only ablation: no stores)
-#elif GPK_FAST_ABLATE == 3
-          wrow[i][col] = ts + tp;  // (timing-only ablation: no exps)
-#else
-          wrow[i][col] = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
-#endif
-        }
+    const double* xr = a.faux + 2 * ((int64_t)b * a.ntile + ti);
+    const double* xc = a.faux + 2 * ((int64_t)b * a.ntile + tj);
+    const bool fast = gi0 + ATILE <= nm && gj0 + ATILE <= nm && mc[5] != 0.0 && xr[1] != 0.0 && xc[1] != 0.0 &&
+                      (xr[0] + xc[0]) * mc[6] <= PAIR_MFMA_MAX_NORM;
+    if (!fast) {
+      if (tid == 0) {
+        int32_t* tl = const_cast<int32_t*>(a.tlist);
+        const int k = atomicAdd(tl, 1);
+        tl[1 + 3 * k] = b;
+        tl[2 + 3 * k] = (int32_t)ti;
+        tl[3 + 3 * k] = (int32_t)tj;
       }
-    } else {
-      // the diagonal tile: the symmetric form of the SE exponent (K bitwise symmetric), k(x, x) + noise exactly
+      continue;
+    }
+    if (loaded >= 0) __syncthreads();  // (the previous tile's LDS reads are done)
+    {
+      const double2* sr = reinterpret_cast<const double2*>(fb + gi0 * FS);
+      const double2* sc = reinterpret_cast<const double2*>(fb + gj0 * FS);
+      double2* dr = reinterpret_cast<double2*>(fr);
+      double2* dc = reinterpret_cast<double2*>(fc);
+      if (ti != loaded) {
+        for (int e = tid; e < ATILE * FS / 2; e += 256) {
+          dr[e] = sr[e];
+          dc[e] = sc[e];
+        }
+      } else {
+        for (int e = tid; e < ATILE * FS / 2; e += 256) dc[e] = sc[e];
+      }
+      loaded = ti;
+    }
+    const double a_s = mc[0], lsg_s = mc[1], a_p = mc[2], c_p = mc[3], lsg_p = mc[4];
+    const bool diag = ti == tj;
+    const double kself = mc[7] + (diag ? a.noise[(int64_t)b * a.noise_stride] : 0.0);
+    __syncthreads();
+    const int lane = tid & 63, w = tid >> 6;
+    const int lr = lane & 15, kq = lane >> 4;
+    double ase[SS], ape[PS];
+    const int prow_pt = 16 * w + lr;
+#pragma unroll
+    for (int t2 = 0; t2 < SS; ++t2) ase[t2] = fr[prow_pt * FS + 4 * t2 + kq];
+#pragma unroll
+    for (int t2 = 0; t2 < PS; ++t2) ape[t2] = fr[prow_pt * FS + D + 4 * t2 + kq];
+    double hr[4];
+    double* wrow[4];
+    double* const Wt = reinterpret_cast<double*>(a.W) + (int64_t)b * a.w_bs + gi0 * a.ld + gj0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hr[i] = fma(-0.5 * a_s, fr[(16 * w + kq + 4 * i) * FS + 3 * D], lsg_s);
+      wrow[i] = Wt + (int64_t)(16 * w + kq + 4 * i) * a.ld;
+    }
+#pragma unroll 1
+    for (int cp = 0; cp < 2; ++cp) {
+      d4 dse[2], dpe[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int col = 16 * (2 * cp + h) + lr;
-        const double ncol = fc[col * FS + 3 * D];
+        dse[h] = d4{0.0, 0.0, 0.0, 0.0};
+        dpe[h] = d4{0.0, 0.0, 0.0, 0.0};
+      }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 16 * w + kq + 4 * i;
-          const double ts = fmin(fma(dse[h][i], a_s, fma(-0.5 * a_s, fr[row * FS + 3 * D] + ncol, lsg_s)), lsg_s);
-          const double tp = fmin(fma(dpe[h][i], a_p, c_p), lsg_p);
-          const double v = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
-          wrow[i][col] = row == col ? kself : v;
+      for (int t2 = 0; t2 < SS; ++t2)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          dse[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ase[t2], fc[(16 * (2 * cp + h) + lr) * FS + 4 * t2 + kq],
+                                                        dse[h], 0, 0, 0);
+#pragma unroll
+      for (int t2 = 0; t2 < PS; ++t2)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          dpe[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ape[t2], fc[(16 * (2 * cp + h) + lr) * FS + D + 4 * t2 + kq],
+                                                        dpe[h], 0, 0, 0);
+      if (!diag) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int col = 16 * (2 * cp + h) + lr;
+          const double hc = -0.5 * a_s * fc[col * FS + 3 * D];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const double ts = fmin(fma(dse[h][i], a_s, hr[i] + hc), lsg_s);
+            const double tp = fmin(fma(dpe[h][i], a_p, c_p), lsg_p);
+#if GPK_FAST_ABLATE == 2
+            { const double v = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
+              if (v == 12345.678) wrow[i][col] = v; }  // (timing-only ablation: no stores)
+#elif GPK_FAST_ABLATE == 3
+            wrow[i][col] = ts + tp;  // (timing-only ablation: no exps)
+#else
+            wrow[i][col] = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
+#endif
+          }
+        }
+      } else {
+        // the diagonal tile: the symmetric form of the SE exponent (K bitwise symmetric), k(x, x) + noise exactly
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int col = 16 * (2 * cp + h) + lr;
+          const double ncol = fc[col * FS + 3 * D];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = 16 * w + kq + 4 * i;
+            const double ts = fmin(fma(dse[h][i], a_s, fma(-0.5 * a_s, fr[row * FS + 3 * D] + ncol, lsg_s)), lsg_s);
+            const double tp = fmin(fma(dpe[h][i], a_p, c_p), lsg_p);
+            const double v = MUL ? exp2_32(ts + tp, tab) : exp2_32(ts, tab) + exp2_32(tp, tab);
+            wrow[i][col] = row == col ? kself : v;
+          }
         }
       }
     }
@@ -1606,18 +1625,21 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
       const int q = sc_node(kd);
       const bool mul = kd.nodes[2].op == GPK_OP_MUL;
       const dim3 fgrid((unsigned)a.ntile, (unsigned)batch, 1);
+      const int64_t tiles = (int64_t)grid.x;  // lower tiles per member
+      const int chunk = GPK_FAST_CHUNK;
+      const dim3 cgrid((unsigned)((tiles + chunk - 1) / chunk), (unsigned)batch, 1);
       if (a.d == 8) {
         hipLaunchKernelGGL((pair_feat_kernel<8>), fgrid, dim3(256), 0, s, kd, af, 1 - q, q);
         if (mul)
-          hipLaunchKernelGGL((pair_fast_kernel<8, true>), grid, dim3(256), 0, s, kd, af);
+          hipLaunchKernelGGL((pair_fast_kernel<8, true>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk);
         else
-          hipLaunchKernelGGL((pair_fast_kernel<8, false>), grid, dim3(256), 0, s, kd, af);
+          hipLaunchKernelGGL((pair_fast_kernel<8, false>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk);
       } else {
         hipLaunchKernelGGL((pair_feat_kernel<4>), fgrid, dim3(256), 0, s, kd, af, 1 - q, q);
         if (mul)
-          hipLaunchKernelGGL((pair_fast_kernel<4, true>), grid, dim3(256), 0, s, kd, af);
+          hipLaunchKernelGGL((pair_fast_kernel<4, true>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk);
         else
-          hipLaunchKernelGGL((pair_fast_kernel<4, false>), grid, dim3(256), 0, s, kd, af);
+          hipLaunchKernelGGL((pair_fast_kernel<4, false>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk);
       }
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) {
