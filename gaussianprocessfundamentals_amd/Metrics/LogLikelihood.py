@@ -73,8 +73,8 @@ class LogLikelihood(AbstractLogLikelihood):
             # log-determinant would otherwise reach every member through the summed penalty, Q7);
             # the reference raises from tf.linalg.cholesky (get_metric_checked does)
             return torch.where(torch.any(f.info != 0), torch.full_like(res, math.inf), res)
-        # a copy: f.out is the factorisation's buffer, overwritten by the next evaluation
-        return f.nlml().reshape(1, 1).clone()
+        # (no copy: every evaluation writes a fresh read-out buffer, engine.AugmentedFactorization._fresh_out)
+        return f.nlml().reshape(1, 1)
 
     def _get_metric_by_strategy(self, hyper_parameter: List, noise, indices=None) -> torch.Tensor:
         """The reference's formula with the bound get_alpha / get_log_determinant (LogLikelihood.py:36-49)
@@ -143,8 +143,8 @@ class LogLikelihood(AbstractLogLikelihood):
                 not self._positive_definite(hyper_parameter, noise):
             return self._eigen_metric_and_gradient(hyper_parameter, noise)
         f = self.covariance_matrix.inverse_factorization(hyper_parameter, noise, gradient=True)
-        g = f.gradient()[0].clone()
-        return f.nlml().reshape(1, 1).clone(), _split_like(g[:-1], hyper_parameter), g[-1]
+        g = f.gradient()[0]   # (fresh buffers per evaluation: no copies needed)
+        return f.nlml().reshape(1, 1), _split_like(g[:-1], hyper_parameter), g[-1]
 
     def _batch_metric_and_gradient(self, hyper_parameter: List, noise):
         """BatchDataInput (quirk Q7).  CHOLESKY_BASED: -LML = -agg_b(-1/2 fit_b - 1/2 sum_b' logdet_b' - c):

@@ -102,11 +102,11 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
         x, y = self._xy()
         batch, n, d = self._shape(x)
         kd = engine.kernel_descriptor(self.kernel, d)
-        hyp = engine.pack_hyper_parameter(hyper_parameter, kd.n_hyp)
+        hyp, nz = engine.pack_hyper_parameter_and_noise(hyper_parameter, noise, kd.n_hyp)
         x = x.contiguous()
         yv = y.reshape(batch, n).to(torch.float64).contiguous()
-        fact.run(kd, hyp, 0, noise_vector(noise), 0, x, n * d if batch > 1 else 0, yv, n if batch > 1 else 0,
-                 E=E, e_bstride=0)
+        fact.run(kd, hyp, 0, nz if nz is not None else noise_vector(noise), 0, x, n * d if batch > 1 else 0, yv,
+                 n if batch > 1 else 0, E=E, e_bstride=0)
         self.kernel._record_hyper_parameter(list(hyper_parameter))
         return fact
 
@@ -193,12 +193,12 @@ class HolisticCovarianceMatrix(CovarianceMatrix):
         x, y = self._xy()
         batch, n, d = self._shape(x)
         kd = engine.kernel_descriptor(self.kernel, d)
-        hyp = engine.pack_hyper_parameter(hyper_parameter, kd.n_hyp)
+        hyp, nz = engine.pack_hyper_parameter_and_noise(hyper_parameter, noise, kd.n_hyp)
         f = engine.InverseFactorization(n, d, batch, global_param.p_dtype)
         yv = y.reshape(batch, n).to(torch.float64)
         yv = (yv * y_scale if y_scale != 1.0 else yv).contiguous()
-        f.run(kd, hyp, 0, noise_vector(noise), 0, x.contiguous(), n * d if batch > 1 else 0, yv,
-              n if batch > 1 else 0, gradient=gradient)
+        f.run(kd, hyp, 0, nz if nz is not None else noise_vector(noise), 0, x.contiguous(),
+              n * d if batch > 1 else 0, yv, n if batch > 1 else 0, gradient=gradient)
         self.kernel._record_hyper_parameter(list(hyper_parameter))
         return f
 

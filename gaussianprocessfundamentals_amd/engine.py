@@ -107,6 +107,37 @@ def host_f64_to_device(values) -> torch.Tensor:
     return t.to(dev)
 
 
+def _host_values(hyper_parameter: Sequence) -> Optional[List[float]]:
+    """The flat host floats of a hyperparameter list, or None if an entry lives on the device."""
+    for h in hyper_parameter:
+        if isinstance(h, torch.Tensor) and h.device.type != "cpu":
+            return None
+    vals: List[float] = []
+    for h in hyper_parameter:
+        if isinstance(h, torch.Tensor):
+            vals.extend(float(v) for v in h.detach().reshape(-1).tolist())
+        else:
+            try:
+                vals.extend(float(v) for v in h)
+            except TypeError:
+                vals.append(float(h))
+    return vals
+
+
+def pack_hyper_parameter_and_noise(hyper_parameter: Sequence, noise, n_expected: int):
+    """(hyperparameter vector, 1-element noise vector) on the device; when both are host values, through ONE
+    asynchronous copy (one buffer, two views) instead of one per operand.  noise None: the caller's own."""
+    host_noise = not isinstance(noise, torch.Tensor) or (noise.device.type == "cpu" and not noise.requires_grad)
+    vals = _host_values(hyper_parameter) if host_noise and not (
+        isinstance(hyper_parameter, torch.Tensor) and hyper_parameter.dim() == 1) else None
+    if vals is None:
+        return pack_hyper_parameter(hyper_parameter, n_expected), None
+    if len(vals) != n_expected:
+        raise ValueError("hyperparameter vector has %d values, kernel expects %d" % (len(vals), n_expected))
+    t = host_f64_to_device(vals + [float(noise)])
+    return t[:n_expected], t[n_expected:]
+
+
 def pack_hyper_parameter(hyper_parameter: Sequence, n_expected: Optional[int] = None) -> torch.Tensor:
     """Flat fp64 device vector of a hyperparameter list (each entry reshaped to [-1], concatenated;
     BasicGPComponent.serialize_hyper_parameter, gpbasics/Auxiliary/BasicGPComponent.py:16-23)."""
@@ -115,21 +146,8 @@ def pack_hyper_parameter(hyper_parameter: Sequence, n_expected: Optional[int] = 
         flat = hyper_parameter.to(device=dev, dtype=torch.float64)
     else:
         parts = []
-        host_vals = []
-        all_host = True
-        for h in hyper_parameter:
-            if isinstance(h, torch.Tensor) and h.device.type != "cpu":
-                all_host = False
-                break
-        if all_host:
-            for h in hyper_parameter:
-                if isinstance(h, torch.Tensor):
-                    host_vals.extend(float(v) for v in h.detach().reshape(-1).tolist())
-                else:
-                    try:
-                        host_vals.extend(float(v) for v in h)
-                    except TypeError:
-                        host_vals.append(float(h))
+        host_vals = _host_values(hyper_parameter)
+        if host_vals is not None:
             flat = host_f64_to_device(host_vals)
         else:
             for h in hyper_parameter:
@@ -273,11 +291,17 @@ class AugmentedFactorization:
         self._defer_verify(lambda: self._run_once(*args))
         return self
 
+    def _fresh_out(self) -> None:
+        """A new read-out buffer per evaluation (the caching allocator's, no device work): views of an earlier
+        evaluation's -LML stay valid without a copy (LogLikelihood.get_metric returns one)."""
+        self._out = torch.empty(self.batch * 4, dtype=torch.float64, device=self._W.device)
+
     def _run_once(self, kd, hyp, hyp_stride, noise, noise_stride, X, x_bstride, y, y_bstride, Xs, xs_bstride,
                   E, e_bstride):
         lay = self.layout
         B, n, m, d = self.batch, self.n, self.m, self.d
         self._alphas = None
+        self._fresh_out()
         # the device reads these extents blindly: check them here (an undersized operand would
         # be read out of bounds, not reported)
         _check_operand("hyper_parameter", hyp, hyp_stride, kd.n_hyp, B, self.W.device)
@@ -423,6 +447,7 @@ class InverseFactorization(AugmentedFactorization):
         B, n, d = self.batch, self.n, self.d
         dev = self.W.device
         self._alphas = None
+        self._fresh_out()
         _check_operand("hyper_parameter", hyp, hyp_stride, kd.n_hyp, B, dev)
         _check_operand("noise", noise, noise_stride, 1, B, dev)
         _check_operand("X", X, x_bstride, n * d, B, dev)
