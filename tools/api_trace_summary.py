@@ -2,6 +2,7 @@
 timed loop of `calls` get_metric calls): kernels per call, summed kernel time, device span and the gaps between
 dependent kernels.  usage: python tools/api_trace_summary.py TRACE.csv CALLS"""
 import csv
+import re
 import statistics
 import sys
 from collections import Counter
@@ -12,7 +13,7 @@ def main(path, calls):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows]
     # the last 2 * calls calls' worth of kernels: the script's timed loop and its profiled loop
-    names = Counter(k[2].split("(")[0][:70] for k in ks)
+    ks = [(s, e, re.sub(r"\(anonymous namespace\)::", "", n).split("(")[0][:70]) for s, e, n in ks]
     per_call = len(ks) / (2 * calls + 20)
     tail = ks[-int(per_call * calls):]
     busy = sum(e - s for s, e, _ in tail) / calls / 1e3
@@ -22,11 +23,10 @@ def main(path, calls):
     durs = Counter()
     cnt = Counter()
     for s, e, n in tail:
-        durs[n.split("(")[0][:70]] += (e - s) / 1e3
-        cnt[n.split("(")[0][:70]] += 1
+        durs[n] += (e - s) / 1e3
+        cnt[n] += 1
     for n, d in durs.most_common(12):
         print("  %-70s %6d  %8.2f us per call  %6.2f us avg" % (n, cnt[n], d / calls, d / cnt[n]))
-    del names
 
 
 if __name__ == "__main__":
