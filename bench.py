@@ -486,6 +486,12 @@ def main():
                 mine[i][chunk:chunk + batch] = info_dev.to(torch.float64)
                 dist.all_gather_into_tensor(gathered[i], mine[i])
 
+    # every slot once before the warm-up (setup, not a warm-up step): a stream's first launch allocates libgpk's
+    # per-stream scratch, a device synchronisation that would otherwise land in the timed region whenever the
+    # warm-up has fewer steps than there are slots (C2 at 8 in flight: 198 instead of 1715 evals/s with 3)
+    for i in range(P):
+        step(slot=i)
+    torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
