@@ -9,7 +9,11 @@ from collections import Counter
 def main(path, calls):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    tail = rows[-len(rows) // 3:]  # the profiled loop: the last of the script's three loops of `calls`
+    # the script's last two loops of `calls` get_metric each: from the (2 calls)-th last memset of info (one per
+    # get_metric, gpk_nlml's first call) to the end
+    ms = [i for i, r in enumerate(rows) if r["Function"] == "hipMemsetAsync"]
+    tail = rows[ms[-2 * calls]:]
+    calls *= 2
     t = Counter()
     c = Counter()
     for r in tail:
