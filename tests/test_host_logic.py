@@ -60,6 +60,24 @@ def test_pack_hyper_parameter_dfs_order():
         gp.p_device = "cuda"
 
 
+def test_pack_hyper_parameter_and_noise_one_buffer():
+    """Host hyperparameters + host noise: one buffer, two views (one copy to the device); a noise that needs its
+    gradient keeps its own path (None: the caller's noise_vector)."""
+    gp.p_device = "cpu"
+    try:
+        h, nz = engine.pack_hyper_parameter_and_noise([torch.tensor(0.5), [1.0, 2.0]], torch.tensor(0.01, dtype=torch.float64), 3)
+        assert h.tolist() == [0.5, 1.0, 2.0] and nz.tolist() == [0.01]
+        assert h.untyped_storage().data_ptr() == nz.untyped_storage().data_ptr()
+        h, nz = engine.pack_hyper_parameter_and_noise([0.5], 0.25, 1)
+        assert h.tolist() == [0.5] and nz.tolist() == [0.25]
+        h, nz = engine.pack_hyper_parameter_and_noise([0.5], torch.tensor(0.1, requires_grad=True), 1)
+        assert h.tolist() == [0.5] and nz is None
+        with pytest.raises(ValueError):
+            engine.pack_hyper_parameter_and_noise([1.0, 2.0], 0.1, 3)
+    finally:
+        gp.p_device = "cuda"
+
+
 def test_reference_hyperparameter_plumbing():
     set_flags(scaled=True)
     se = bk.SquaredExponentialKernel(1)
