@@ -495,6 +495,10 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # persistent launches are not verified inside the timed region (no step reads a result): a launch whose waits
+    # timed out (info = -1, its candidates not evaluated) is counted on the device (gpk_chain_stats) and its
+    # candidates are left out of `value` below
+    timeouts0 = nat.chain_timeouts()
     # timed region: no per-launch HIP events (they would add a marker packet to every launch)
     if use_dist:
         dist.barrier()
@@ -507,10 +511,17 @@ def main():
     if use_dist:
         dist.barrier()
     el = t1 - t0
+    timed_out = nat.chain_timeouts() - timeouts0
+    if timed_out:
+        sys.stderr.write("bench.py: %d persistent launches timed out in the timed region; their candidates are not "
+                         "counted\n" % timed_out)
     if use_dist:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+        to = torch.tensor([timed_out], dtype=torch.int64, device=dev)
+        dist.all_reduce(to, op=dist.ReduceOp.SUM)
+        timed_out = int(to.item())
     # per-class kernel spans of the production schedule (look-ahead on): a separate events pass
     use_events = not args.no_events
     timing = None
@@ -553,6 +564,8 @@ def main():
 
     if rank == 0:
         evals = args.steps * ((len(c4_candidates()) if args.slice_of == 1 else batch) if sweep else world * batch)
+        # (a timed-out persistent launch evaluated none of its batch's candidates; summed over the ranks)
+        evals -= timed_out * batch
         value = evals / el
         ms = el / args.steps * 1000.0
         lay = fact.layout
@@ -620,7 +633,8 @@ def main():
             else:
                 cpu, cpu_nl0 = cpu_baseline(args.config, n, args.cpu_seconds, rows[0])
         # parity of the bench's own numbers: -LML of spread candidates against the oracle on the same inputs
-        check = {"nlml": nl, "info": info, **({"allgather_ok": gathered_ok} if use_dist else {})}
+        check = {"nlml": nl, "info": info, "chain_timeouts_timed": timed_out,
+                 **({"allgather_ok": gathered_ok} if use_dist else {})}
         if not args.no_check:
             idx = ([int(v) for v in args.check_candidates.split(",")] if args.check_candidates else
                    sorted({0, batch // 2, batch - 1}))

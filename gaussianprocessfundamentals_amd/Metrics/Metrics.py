@@ -12,7 +12,7 @@ The reference binds ``get_alpha`` / ``get_log_determinant`` per numerical handli
 
 slogdet(K)[1] is log|det K| = 2 sum log diag L for a positive-definite K (the device Cholesky) and
 sum log|lam_i| from the eigenvalues (gpk_syevd) otherwise; STRICT_INVERSE of an indefinite nonsingular K
-(LU in the reference) is V diag(1/lam) V^T.  The eigendecomposition fallback is limited to n <= 16384.
+(LU in the reference) is V diag(1/lam) V^T.  The eigendecomposition fallback takes n <= 46340 (gpk_syevd).
 Subset-of-data approximations (SOD_GRID, SOD_RANDOM) evaluate the exact path on the subset
 (:60-68).  Matrix approximations (:77-126) swap get_covariance_matrix / get_log_determinant:
 
@@ -181,9 +181,9 @@ class Metric(AbstractMetric):
             return engine.gemv(f.k_inv(0).contiguous(), self._y(y))
         return engine.gemv(self.covariance_matrix.get_K_inv(hyper_parameter, noise).contiguous(), self._y(y))
 
-    # largest n for the eigendecomposition fallback of a matrix that is not positive definite (gpk_syevd's
-    # cap: its divide-and-conquer gather holds a row of a merged block in LDS)
-    EIGEN_FALLBACK_MAX_N = 16384
+    # largest n for the eigendecomposition fallback of a matrix that is not positive definite (gpk_syevd's cap: its
+    # kernels index the m x m matrix with 32-bit products, m^2 < 2^31; n = 46340 is 17 GB per m x m buffer)
+    EIGEN_FALLBACK_MAX_N = 46340
 
     def _positive_definite(self, hyper_parameter: List, noise, indices=None) -> bool:
         f = (self._approx_factorization(hyper_parameter, noise, indices) if self._approximate()

@@ -106,16 +106,18 @@ class NystroemMatrix:
             nv = _noise_value(noise)
             G, sgn, GtG, n_neg = self._signed_core(hyper_parameter, indices)
             if n_neg == 0:
-                a = self.get_K_approx(hyper_parameter, indices).contiguous()
+                # K_hat = K_nm U U^T K_nm^T = G G^T (S = I): no second kernel build and eigendecomposition
+                a = engine.dgemm(G, G, trans_b=True)
                 n = a.shape[0]
                 f = engine.DenseFactorization(n, inverse=True).run(a, nv)
                 f.check_info()
                 self.K_approx_inv = f.k_inv(0).to(torch.float64)
             else:
-                # Woodbury (:73-90): (I - G C^-1 G^T) / noise, C = noise S + G^T G symmetric indefinite
+                # Woodbury (:73-90): (I - G C^+ G^T) / noise, C = noise S + G^T G symmetric indefinite; the reference
+                # takes tf.linalg.pinv of its inner matrix, so C^+ keeps pinv's cutoff (10 m eps max|lam|)
                 C = GtG.clone()
                 C.diagonal().add_(nv * sgn)
-                Ci = sym_inverse(C)
+                Ci = sym_inverse(C, cutoff=True)
                 out = engine.dgemm(engine.dgemm(G, Ci), G, trans_b=True, alpha=-1.0 / nv)
                 self.K_approx_inv = engine.add_diagonal(out, 1.0 / nv)
         return self.K_approx_inv
@@ -152,11 +154,12 @@ def signed_pinv_factor(lam: torch.Tensor, V: torch.Tensor):
     return U, sgn, int((sgn < 0).sum()), mu
 
 
-def sym_inverse(C: torch.Tensor) -> torch.Tensor:
-    """Inverse of a symmetric nonsingular (possibly indefinite) device matrix: V diag(1/lam) V^T from gpk_syevd
-    (no cutoff), on the MFMA GEMM."""
+def sym_inverse(C: torch.Tensor, cutoff: bool = False) -> torch.Tensor:
+    """Inverse of a symmetric (possibly indefinite) device matrix: V diag(1/lam) V^T from gpk_syevd, on the MFMA
+    GEMM.  cutoff=False: every eigenvalue (the true inverse, e.g. d log|det C| / dC); cutoff=True: tf.linalg.pinv's
+    (eigenvalues with |lam| <= 10 m eps max|lam| dropped), as the reference's pinv of the Woodbury inner matrix."""
     lam, V = engine.syevd(C.contiguous())
-    U, _ = engine.pinv_factor(lam, V, 0, rcond=0.0)
+    U, _ = engine.pinv_factor(lam, V, 0) if cutoff else engine.pinv_factor(lam, V, 0, rcond=0.0)
     return engine.dgemm(U, V, trans_b=True)
 
 

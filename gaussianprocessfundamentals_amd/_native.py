@@ -241,6 +241,15 @@ def chain_stats() -> dict:
             "forced_pending": int(out[3])}
 
 
+def chain_timeouts() -> int:
+    """Persistent launches on the current device whose waits timed out since the library was loaded (each set
+    info = -1 on its unfinished members; forced timeouts count too).  A device read: it waits for the work
+    enqueued so far, so callers read it outside timed regions."""
+    out = (c_int64 * 5)()
+    check(load_library().gpk_chain_stats(out, 5), "gpk_chain_stats")
+    return int(out[4])
+
+
 def last_factorisation_was_chain() -> bool:
     out = (c_int64 * 3)()
     check(load_library().gpk_chain_stats(out, 3), "gpk_chain_stats")

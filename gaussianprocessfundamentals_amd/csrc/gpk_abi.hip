@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <initializer_list>
 #include <map>
@@ -191,6 +192,11 @@ struct Tune {
   int64_t chain_min_p_eye;  // ... and for identity-augmented factorisations (value + gradient): N = 1024 / 1280
                             // 0.554 / 0.657 ms on the launch path vs 0.590 / 0.683, N = 1536 0.809 vs 0.786
                             // (profiles/r05al_api_crossover.jsonl)
+  int64_t chain_group_corner;  // identity-augmented plans: panels per deferred update of the corner's tiles (-K^-1,
+                               // read by no later task)
+  int64_t chain_corner_tail;   //   ... except the last this many panels, which keep chain_group
+  int64_t chain_group_la;      // deferred (grouped) tile updates only for block columns at least this many columns
+                               // past the group's last panel
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -215,7 +221,9 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_MAX_BATCH", 8), env_i64("GPK_CHAIN_BATCH_MAX_ROWS", 17500),
                          env_i64("GPK_CHAIN_UQ", 1), env_i64("GPK_CHAIN_EYE", 1),
                          env_i64("GPK_CHAIN_MAX_P_EYE", 16640), env_i64("GPK_ASM_FEAT", 1),
-                         env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 3072)};
+                         env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 3072),
+                         env_i64("GPK_CHAIN_GROUP_CORNER", 16), env_i64("GPK_CHAIN_CORNER_TAIL", 8),
+                         env_i64("GPK_CHAIN_GROUP_LA", 2)};
   return t;
 }
 
@@ -242,7 +250,8 @@ const Knob kKnobs[] = {
     {"chain_batch_max_rows", &Tune::chain_batch_max_rows}, {"chain_uq", &Tune::chain_uq},
     {"chain_eye", &Tune::chain_eye},         {"chain_max_p_eye", &Tune::chain_max_p_eye},
     {"asm_feat", &Tune::asm_feat},           {"chain_min_p", &Tune::chain_min_p},
-    {"chain_min_p_eye", &Tune::chain_min_p_eye},
+    {"chain_min_p_eye", &Tune::chain_min_p_eye}, {"chain_group_corner", &Tune::chain_group_corner},
+    {"chain_corner_tail", &Tune::chain_corner_tail}, {"chain_group_la", &Tune::chain_group_la},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -375,7 +384,8 @@ struct ChainPlan {
   int32_t nblk = 0, nsl = 0, nbc = 0;
 };
 std::mutex g_chain_mu;
-std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int>, ChainPlan> g_chain_plans;
+// key: device, n_pad, y_row, grid, members, eye, and every knob chain_order reads (ChainKnobs)
+std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int>, ChainPlan> g_chain_plans;
 // Counter scratch of the persistent launch, per (host thread, device, stream): the counters are zeroed
 // by a memset enqueued before each launch, so two threads enqueueing on one stream (torch's null stream
 // is shared by every thread) must never share them -- memset A, memset B, launch A, launch B would hand
@@ -461,6 +471,32 @@ int chain_group_for(int64_t knob, int64_t n_pad) {
   return n_pad / NB >= 80 ? 8 : 4;
 }
 
+// Every tuning input of chain_order, resolved once per call from the knobs (and part of the plan cache key, so a
+// cached device plan and gpk_chain_plan_ex always agree)
+struct ChainKnobs {
+  int group, uq, group_corner, corner_tail, group_la;
+};
+ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad) {
+  ChainKnobs k;
+  k.group = std::max(1, std::min(chain_group_for(tn.chain_group, n_pad), 16));
+  k.uq = (int)std::max<int64_t>(0, std::min<int64_t>(2, tn.chain_uq));
+  k.group_corner = (int)std::max<int64_t>(1, std::min<int64_t>(tn.chain_group_corner, 16));
+  k.corner_tail = (int)std::max<int64_t>(0, tn.chain_corner_tail);
+  k.group_la = (int)std::max<int64_t>(1, tn.chain_group_la);
+  return k;
+}
+
+// list-scheduling durations (us) of D / S / U32 / BLK: the measured per-task run times (round 4, profiles/r04y_*;
+// UQ: half of U32); GPK_CHAIN_DUR="d,s,u,b" overrides them (A/B), read once per process
+const float* chain_durations() {
+  static const std::array<float, 4> dur = [] {
+    std::array<float, 4> d = {28.f, 6.5f, 12.f, 22.5f};
+    if (const char* e = getenv("GPK_CHAIN_DUR")) sscanf(e, "%f,%f,%f,%f", &d[0], &d[1], &d[2], &d[3]);
+    return d;
+  }();
+  return dur.data();
+}
+
 // Type word of a task: ty (bits 0..1) | (g - 1) << 2 (BLK over g panels; UQ: quarter + 1, bits 2..5) |
 // kChainFirst (bit 6: the (slice, block column) cells the task updates have no earlier update -- its counter
 // wait is for 0, not for the task's first panel; identity-augmented lists only) | member << 8.
@@ -475,8 +511,11 @@ constexpr int kChainSq = 1 << 7;
 // every task that would only move zeros -- the panel solves of such slices and the tile updates where either
 // block is still zero -- so the factorisation does n^3 flops (potrf + trtri + lauum) like the launch path's
 // band skip.  The block holding the y row is live in every panel.
-std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int group, int nmem, int chain_uq,
+// Returns the task words (four per task); empty if the graph exceeds a bound of the device tasks (the caller
+// reports that as an error -- never reached for graphs built here, whose in-degrees are bounded by construction).
+std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int nmem, const ChainKnobs& kn,
                                  bool eye = false) {
+  const int group = kn.group, chain_uq = kn.uq;
   const int nblk = (int)(n_pad / NB), yb = (int)(y_row / NB), rlast = (int)(y_row / 32);
   // block i holds a nonzero row in the columns of panel q (monotone in q): from panel live_from(i) on
   auto live_from = [&](int i) { return (!eye || i < nblk || i == yb) ? 0 : i - nblk; };
@@ -512,25 +551,17 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
   };
   auto s_of = [&](int k, int r) { return S[(size_t)k * nr + r]; };
   auto u_of = [&](int k, int r) { return U[(size_t)k * nr + r]; };
-  // list-scheduling durations (us) of D / S / U32 / BLK: the measured per-task run times
-  // (profiles/r03p_chain_task_profile_n4096.txt); GPK_CHAIN_DUR="d,s,u,b" overrides them (A/B).  A tile
-  // update over g panels is estimated at b (0.25 + 0.75 g): the C read / write and the pipeline fill are
-  // paid once per task.
-  float dur[4] = {28.f, 6.5f, 12.f, 22.5f};  // round 4: measured D, S, U32 (UQ: half), BLK g = 1 (profiles/r04y_*)
-  if (const char* e = getenv("GPK_CHAIN_DUR")) sscanf(e, "%f,%f,%f,%f", &dur[0], &dur[1], &dur[2], &dur[3]);
+  // list-scheduling durations (chain_durations); a tile update over g panels is estimated at b (0.25 + 0.75 g):
+  // the C read / write and the pipeline fill are paid once per task
+  const float* dur = chain_durations();
   // Deferred tile updates: the panels of group [q0, q1) (G panels) are applied to a tile of block column j
   // by ONE task of depth 128 (q1 - q0) when j >= q1 + L -- the column is not needed until L steps after
   // the group's last panel solve; the columns nearer the diagonal take each panel on its own (depth 128),
   // so the diagonal chain never waits for a deep update.  G = 1 disables it.
-  const int G = std::max(1, std::min(group, 16));
-  const int Gc = std::max(1, std::min<int>((int)env_i64("GPK_CHAIN_GROUP_CORNER", 16), 16));
-  const int tail_c = (int)std::max<int64_t>(0, env_i64("GPK_CHAIN_CORNER_TAIL", 8));
-  const int LA = (int)std::max<int64_t>(1, env_i64("GPK_CHAIN_GROUP_LA", 2));
+  const int G = group, Gc = kn.group_corner, tail_c = kn.corner_tail, LA = kn.group_la;
+  bool overflow = false;  // a task with more than MAXDEP dependencies (unreachable: bounded by construction)
   auto add = [&](const Task& t) {
-    if (t.nd > MAXDEP) {  // (unreachable: the graph's in-degrees are bounded by construction)
-      fprintf(stderr, "libgpk: chain_order: a task with %d dependencies (at most %d)\n", t.nd, MAXDEP);
-      abort();
-    }
+    if (t.nd > MAXDEP) overflow = true;
     T.push_back(t);
     return (int)T.size() - 1;
   };
@@ -656,6 +687,7 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int gro
         T.push_back(c);
       }
   }
+  if (overflow) return {};
   const int n = (int)T.size();
   // successors in CSR form, each task's in the order its dependants were built
   std::vector<int> indeg(n, 0), soff(n + 1, 0);
@@ -732,12 +764,17 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   size_t ctl_ints = 0;
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
-    const int group = chain_group_for(tn.chain_group, lay->n_pad), nmem = lay->batch;
-    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq, eye ? 1 : 0);
+    const ChainKnobs kn = chain_knobs(tn, lay->n_pad);
+    const int nmem = lay->batch;
+    auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, nmem, eye ? 1 : 0, kn.group, kn.uq,
+                               kn.group_corner, kn.corner_tail, kn.group_la);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
-      const std::vector<int32_t> ord =
-          chain_order(lay->n_pad, lay->y_row, grid, group, nmem, (int)tn.chain_uq, eye);
+      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, nmem, kn, eye);
+      if (ord.empty()) {
+        // (an internal failure, not a bad argument: reported like a HIP error, > 0)
+        return fail_hip(hipErrorUnknown, "chain_order: a task exceeds the device's dependency bound");
+      }
       ChainPlan p;
       p.ntasks = (int32_t)(ord.size() / 4);
       p.nblk = (int32_t)(lay->n_pad / NB);
@@ -785,7 +822,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.w_bs = lay->w_batch_stride;
   a.inv_bs = lay->inv_batch_stride;
   a.ctl_stride = 2 * (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
-  a.uq = (int32_t)std::max<int64_t>(0, std::min<int64_t>(2, tn.chain_uq));
+  a.uq = (int32_t)chain_knobs(tn, lay->n_pad).uq;
   // rows of L_kk^-1 behind D's early flag: later (more of the panel solve early) for short chains, where the
   // diagonal chain is all there is; earlier for long ones, where the S tasks' waiting CUs cost tile-update time
   // (N = 4096: 112 rows 1.501 vs 96 rows 1.515 ms; 6144 / 8192 2.42 / 4.44 vs 2.37 / 4.39, profiles/r04ab_*)
@@ -1809,7 +1846,8 @@ int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
 // ------------------------------------------------------------------- tridiagonal eigensolver (gpk_eig.hip)
 namespace {
 constexpr int kEigNb = 32;  // reflectors per compact-WY block of the back-transformation
-#define GPK_SYEVD_MAX_M 16384  // dc_gather_kernel holds a row of a merged block in LDS (128 KB)
+// m^2 < 2^31: the eigensolver's kernels index a row-major m x m matrix with 32-bit products of two indices
+#define GPK_SYEVD_MAX_M 46340
 
 struct EigWs {  // carving of the gpk_syevd workspace
   double *W, *Qg, *U, *d, *e, *tau, *Y, *T1, *T2, *Gs, *S, *PV, *vg, *yg, *Sall;
@@ -1880,7 +1918,7 @@ size_t gpk_syevd_workspace_bytes(int64_t m) {
 
 int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
               void* work, size_t work_bytes, void* stream) {
-  if (m < 0 || m > GPK_SYEVD_MAX_M) return fail_arg(1, "m (gpk_syevd: m <= 16384)");
+  if (m < 0 || m > GPK_SYEVD_MAX_M) return fail_arg(1, "m (gpk_syevd: m <= 46340)");
   if (batch < 0) return fail_arg(2, "batch");
   if (m == 0 || batch == 0) return 0;
   if (!A) return fail_arg(3, "A");
@@ -2052,12 +2090,11 @@ int gpk_chain_trace(int32_t* out, int64_t n) {
   return 0;
 }
 
-int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_out, int64_t cap, int64_t* ntasks) {
-  return gpk_chain_plan_ex(n_pad, y_row, grid, 0, tasks_out, cap, ntasks);
-}
-
-int gpk_chain_plan_ex(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, int32_t* tasks_out, int64_t cap,
-                      int64_t* ntasks) {
+namespace {
+// gpk_chain_plan(_ex): ap = the argument positions of (tasks_out, cap, ntasks) in the entry point's own signature,
+// so that -i names the caller's i-th argument (gpk.h's convention) for both entry points
+int chain_plan_impl(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, int32_t* tasks_out, int64_t cap,
+                    int64_t* ntasks, int ap_cap, int ap_ntasks) {
   if (n_pad <= 0 || n_pad % NB != 0) return fail_arg(1, "n_pad (a positive multiple of 128)");
   if (y_row < n_pad) return fail_arg(2, "y_row (>= n_pad)");
   if (grid <= 0) return fail_arg(3, "grid");
@@ -2065,15 +2102,27 @@ int gpk_chain_plan_ex(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags,
   const bool eye = (flags & GPK_AUG_EXTRA_IDENTITY) != 0;
   if (eye && (y_row - n_pad < 1 || y_row - n_pad > n_pad))
     return fail_arg(2, "y_row (identity extra rows: n_pad + n with 0 < n <= n_pad)");
-  if (!ntasks) return fail_arg(7, "ntasks");
-  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, chain_group_for(tune_now().chain_group, n_pad), 1,
-                                               (int)tune_now().chain_uq, eye);
+  if (!ntasks) return fail_arg(ap_ntasks, "ntasks");
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, 1, chain_knobs(tune_now(), n_pad), eye);
+  if (ord.empty()) {
+    return fail_hip(hipErrorUnknown, "chain_order: a task exceeds the device's dependency bound");
+  }
   *ntasks = (int64_t)(ord.size() / 4);
   if (tasks_out) {
-    if (cap < *ntasks) return fail_arg(6, "cap (fewer than ntasks)");
+    if (cap < *ntasks) return fail_arg(ap_cap, "cap (fewer than ntasks)");
     memcpy(tasks_out, ord.data(), ord.size() * sizeof(int32_t));
   }
   return 0;
+}
+}  // namespace
+
+int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_out, int64_t cap, int64_t* ntasks) {
+  return chain_plan_impl(n_pad, y_row, grid, 0, tasks_out, cap, ntasks, 5, 6);
+}
+
+int gpk_chain_plan_ex(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, int32_t* tasks_out, int64_t cap,
+                      int64_t* ntasks) {
+  return chain_plan_impl(n_pad, y_row, grid, flags, tasks_out, cap, ntasks, 6, 7);
 }
 
 int gpk_tune(const char* key, int64_t value, int64_t* old) {
@@ -2109,6 +2158,11 @@ int gpk_chain_stats(int64_t* out, int32_t n) {
   const int64_t v[4] = {g_chain_launches.load(), g_chain_declined.load(), t_chain_last ? 1 : 0,
                         g_chain_force_timeout.load()};
   for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
+  if (n >= 5) {  // (a device read: waits for the work enqueued so far on the null stream's device)
+    int64_t t = 0;
+    GPK_HIP(chain_timeouts_read(&t), "chain timeouts");
+    out[4] = t;
+  }
   return 0;
 }
 

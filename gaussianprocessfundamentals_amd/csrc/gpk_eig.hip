@@ -338,7 +338,6 @@ __global__ __launch_bounds__(256) void dc_init_kernel(const double* d, const dou
 // same arrays in the level's HBM scratch L.gscr (pair p at offset 2a / a: the pairs' regions never overlap),
 // ordered by the same workgroup barriers (one workgroup, one CU: its stores and loads meet in that CU's L1 / L2).
 constexpr int DC_LDS_MAX_K = 4096;
-constexpr int DC_MAX_M = 16384;  // gpk_syevd's cap: dc_gather_kernel holds a row of the merged block in LDS
 __global__ __launch_bounds__(256) void dc_deflate_kernel(const double* __restrict__ e, const double* __restrict__ Q,
                                                          int m, int w, DcLevel L) {
   extern __shared__ __attribute__((aligned(16))) double sh[];
@@ -467,15 +466,23 @@ __global__ __launch_bounds__(256) void dc_deflate_kernel(const double* __restric
 }
 
 // One wave per row r of a pair's block: the row in sorted column order, the deflation rotations, then written
-// kept columns first.  LDS: k doubles.
-__global__ __launch_bounds__(64) void dc_gather_kernel(const double* __restrict__ Q, int m, int w, DcLevel L,
+// kept columns first.  LDS: k doubles for merged blocks of up to DC_GATHER_LDS_MAX_K rows.  Larger ones (m >
+// 16384: the top merge of the non-positive-definite fallbacks at large n) stage the row in HBM instead: the sorted
+// row goes to Qg's row (the output's own place), is rotated there, written permuted into Q's row (read by no one
+// else: Q's row r is this wave's input only, and the level's GEMM overwrites Q afterwards) and copied back.
+constexpr int DC_GATHER_LDS_MAX_K = 16384;  // 128 KB of LDS
+__global__ __launch_bounds__(64) void dc_gather_kernel(double* __restrict__ Q, int m, int w, DcLevel L,
                                                        double* __restrict__ Qg) {
-  extern __shared__ __attribute__((aligned(16))) double x[];
+  extern __shared__ __attribute__((aligned(16))) double xs[];
   const int r = blockIdx.x, lane = threadIdx.x;
   const int p = r / (2 * w);
   const int a = 2 * w * p, c = min(a + 2 * w, m), k = c - a;
-  const double* row = Q + (int64_t)r * m + a;
+  double* row = Q + (int64_t)r * m + a;
+  double* out = Qg + (int64_t)r * m + a;
+  const bool lds = k <= DC_GATHER_LDS_MAX_K;
+  double* x = lds ? xs : out;
   for (int s = lane; s < k; s += 64) x[s] = row[L.idx[a + s]];
+  if (!lds) __threadfence_block();
   __syncthreads();
   if (lane == 0) {
     const int nr = L.rcnt[p];
@@ -487,9 +494,16 @@ __global__ __launch_bounds__(64) void dc_gather_kernel(const double* __restrict_
       x[j] = cs * xj - sn * xi;
     }
   }
+  if (!lds) __threadfence_block();
   __syncthreads();
-  double* out = Qg + (int64_t)r * m + a;
-  for (int t = lane; t < k; t += 64) out[t] = x[L.ord[a + t]];
+  if (lds) {
+    for (int t = lane; t < k; t += 64) out[t] = x[L.ord[a + t]];
+    return;
+  }
+  for (int t = lane; t < k; t += 64) row[t] = x[L.ord[a + t]];
+  __threadfence_block();
+  __syncthreads();
+  for (int t = lane; t < k; t += 64) out[t] = row[t];
 }
 
 // One wave per root (position s of a pair's kept set): 1 + r sum z_j^2 / (d_j - lambda) = 0 on (d_t, d_{t+1})
@@ -827,8 +841,8 @@ hipError_t launch_eig_dc(const double* d, const double* e, int m, const DcLevel&
                          hipStream_t s) {
   {
     hipError_t err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_deflate_kernel), dc_deflate_lds(DC_LDS_MAX_K));
-    if (err == hipSuccess)  // (a pair's row of up to DC_MAX_M doubles)
-      err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_gather_kernel), (size_t)DC_MAX_M * 8);
+    if (err == hipSuccess)  // (a pair's row of up to DC_GATHER_LDS_MAX_K doubles; longer rows are staged in HBM)
+      err = ensure_dyn_lds(reinterpret_cast<const void*>(dc_gather_kernel), (size_t)DC_GATHER_LDS_MAX_K * 8);
     if (err != hipSuccess) return err;
   }
   const int64_t mm = (int64_t)m * m;
@@ -839,7 +853,8 @@ hipError_t launch_eig_dc(const double* d, const double* e, int m, const DcLevel&
     const int R = std::min(2 * P * w, m);  // rows / positions covered by the pairs (an unpaired last block stays)
     const int kmax = std::min(2 * w, m);
     hipLaunchKernelGGL(dc_deflate_kernel, dim3(P), dim3(256), dc_deflate_lds(kmax), s, e, Q, m, w, L);
-    hipLaunchKernelGGL(dc_gather_kernel, dim3(R), dim3(64), sizeof(double) * kmax, s, Q, m, w, L, Qg);
+    hipLaunchKernelGGL(dc_gather_kernel, dim3(R), dim3(64), kmax <= DC_GATHER_LDS_MAX_K ? sizeof(double) * kmax : 0,
+                       s, Q, m, w, L, Qg);
     hipLaunchKernelGGL(dc_secular_kernel, dim3((R + 3) / 4), dim3(256), 0, s, m, w, L);
     hipLaunchKernelGGL(dc_zhat_kernel, dim3((R + 255) / 256), dim3(256), 0, s, m, w, L);
     hipLaunchKernelGGL(dc_vec_kernel, dim3((R + 3) / 4), dim3(256), 0, s, m, w, L, U);

@@ -262,6 +262,7 @@ hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t 
 hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s);
 hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s);
+hipError_t chain_timeouts_read(int64_t* out);  // timed-out persistent launches on this device (synchronous)
 hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_t batch, hipStream_t s);
 size_t vjp_workspace_elems(const gpk_kdesc& kd, int64_t n, int64_t m, int32_t d, bool want_z);
 hipError_t launch_vjp(const gpk_kdesc& kd, const VjpArgs& g, const double* X, int64_t n, const double* Z, int64_t m,

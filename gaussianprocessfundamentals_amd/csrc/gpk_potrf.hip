@@ -1459,4 +1459,12 @@ hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
+// persistent launches that timed out on the current device so far (g_chain_timeouts_dev; synchronous copy)
+hipError_t chain_timeouts_read(int64_t* out) {
+  unsigned long long v = 0;
+  hipError_t e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_chain_timeouts_dev), sizeof(v), 0, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) *out = (int64_t)v;
+  return e;
+}
+
 }  // namespace gpk

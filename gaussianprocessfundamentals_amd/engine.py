@@ -715,14 +715,11 @@ def syevd(A: torch.Tensor):
     """Eigendecomposition of a symmetric [m, m] (or [B, m, m]) device matrix by the tridiagonal route
     (gpk_syevd: blocked Householder tridiagonalisation, divide and conquer on the tridiagonal matrix,
     compact-WY back-transformation): returns (lam, V with the eigenvectors in its columns), eigenvalues in no
-    particular order.  m > 16384 goes to the Jacobi solver (gpk_syevj)."""
+    particular order (any m up to gpk_syevd's cap, 46340)."""
     A3, lda, abs_ = _mat_args(A, "A")
     batch, m = A3.shape[0], A3.shape[1]
     if A3.shape[2] != m:
         raise ValueError("A must be square")
-    if m > 16384:
-        lam, V, _ = syevj(A)
-        return lam, V
     L = nat.lib()
     V = torch.empty((batch, m, m), dtype=torch.float64, device=A.device)
     lam = torch.empty((batch, m), dtype=torch.float64, device=A.device)

@@ -311,7 +311,8 @@ int gpk_syevj(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_
  * tridiagonalisation, divide and conquer on the tridiagonal matrix (deflation, Gu-Eisenstat eigenvectors,
  * MFMA GEMM merges), compact-WY back-transformation on the f64 MFMA GEMM.  Same outputs as gpk_syevj
  * (V [m, m] row-major, eigenvectors in its columns; lam in no particular order); A's lower triangle is read.
- * m <= 16384 (merged blocks above 4096 rows sort in the workspace instead of LDS).  Asynchronous on the stream.
+ * m <= 46340 (merged blocks above 4096 rows sort in the workspace instead of LDS, and above 16384 rows their
+ * gather stages each row in the workspace too).  Asynchronous on the stream.
  * work: gpk_syevd_workspace_bytes(m) (reused across the batch). */
 size_t gpk_syevd_workspace_bytes(int64_t m);
 int gpk_syevd(int64_t m, int32_t batch, const double* A, int64_t lda, int64_t a_bstride, double* V, double* lam,
@@ -411,6 +412,10 @@ int gpk_timing_reset(void);
  * waits for another's workgroups (bench.py's C2 schedule: 8 in flight, 64 workgroups each on 256 CUs).
  * With "chain" 1 (auto) factorisations of fewer than "chain_min_p" (768) rows -- identity-augmented ones:
  * "chain_min_p_eye" (3072) -- keep the launch path (a handful of panels: its few launches are faster).
+ * Identity-augmented plans defer the corner's tile updates (-K^-1, read by no later task) in groups of
+ * "chain_group_corner" (16) panels, except the last "chain_corner_tail" (8) panels, which keep "chain_group"; a
+ * deferred (grouped) update covers only block columns at least "chain_group_la" (2) columns past the group's last
+ * panel.  Every knob the planner reads is part of its plan cache key.
  * "asm_feat" (1: the K build of a two-leaf SE + periodic tree at D = 4 or 8 computes the per-point features in a
  * pre-pass and runs its interior tiles on the f64 MFMA fast-tile kernel; 0: every tile stages its points itself
  * -- the same bits, slower; A/B).
@@ -432,7 +437,10 @@ int gpk_tune_thread(const char* key, int64_t value, int32_t set, int64_t* old_va
 /* Counters of the persistent factorisation: out[0] persistent launches enqueued (all threads),
  * out[1] factorisations that took the launch path because another stream was busy (chain = 1),
  * out[2] 1 if the calling thread's last factorisation was a persistent launch (its info must then be
- * checked for -1, see gpk_tune "chain"), out[3] forced timeouts still pending.  Writes min(n, 4). */
+ * checked for -1, see gpk_tune "chain"), out[3] forced timeouts still pending, out[4] (n >= 5 only: a
+ * synchronous device read) persistent launches on the current device whose waits timed out so far (each
+ * such launch aborted and set info = -1 on its unfinished members; forced timeouts included).
+ * Writes min(n, 5). */
 int gpk_chain_stats(int64_t* out, int32_t n);
 
 /* The task list of the persistent single-member factorisation (gpk_tune "chain"; no reference

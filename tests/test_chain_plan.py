@@ -290,6 +290,47 @@ def test_chain_plan_rejects_bad_shapes():
         nat.chain_plan(128, 100, 8)
 
 
+def test_chain_plan_error_codes_name_each_entry_points_own_argument():
+    """gpk.h: -i means the i-th argument of the called entry point.  gpk_chain_plan(n_pad, y_row, grid, tasks_out,
+    cap, ntasks) and gpk_chain_plan_ex(n_pad, y_row, grid, flags, tasks_out, cap, ntasks) put cap / ntasks at
+    positions 5 / 6 and 6 / 7."""
+    import ctypes
+    _lib_or_skip()
+    L = nat.load_library()
+    nt = ctypes.c_int64(0)
+    buf = (ctypes.c_int32 * 4)()
+    assert L.gpk_chain_plan(1024, 1024, 8, None, 0, None) == -6
+    assert L.gpk_chain_plan_ex(1024, 1024, 8, 0, None, 0, None) == -7
+    assert L.gpk_chain_plan(1024, 1024, 8, buf, 1, ctypes.byref(nt)) == -5     # cap below the task count
+    assert L.gpk_chain_plan_ex(1024, 1024, 8, 0, buf, 1, ctypes.byref(nt)) == -6
+    assert nt.value > 1
+    assert L.gpk_chain_plan(1024, 1024, 0, None, 0, ctypes.byref(nt)) == -3
+    assert L.gpk_chain_plan_ex(1024, 1024, 8, 1 << 20, None, 0, ctypes.byref(nt)) == -4
+    assert L.gpk_chain_plan(1024, 1024, 8, None, 0, ctypes.byref(nt)) == 0
+
+
+def test_chain_plan_corner_knobs_are_tune_knobs():
+    """The identity-augmented planner's corner grouping (chain_group_corner, chain_corner_tail, chain_group_la) are
+    gpk_tune knobs, read per call (and part of the device plan cache key): changing them changes the list that
+    gpk_chain_plan_ex returns, and every list still applies each live update once."""
+    _lib_or_skip()
+    n = 3000
+    n_pad = -(-n // NB) * NB
+    y_row = n_pad + n
+    nblk, yb = n_pad // NB, y_row // NB
+    base = plan(n_pad, y_row, 64, 4, 1, eye=True)
+    for knobs in ({"chain_group_corner": 4}, {"chain_corner_tail": 0}, {"chain_group_la": 3}):
+        with nat.thread_tune(**knobs):
+            alt = plan(n_pad, y_row, 64, 4, 1, eye=True)
+        assert alt.shape != base.shape or not np.array_equal(alt, base), knobs
+        upd = applied_panels(alt, nblk)
+        assert len(upd) == len(set(upd))
+        live = {(q, i, j) for q in range(nblk) for j in range(q + 2, yb + 1) for i in range(j, yb + 1)
+                if eye_live(i, q, nblk, yb) and eye_live(j, q, nblk, yb)}
+        assert live <= set(upd)
+    assert np.array_equal(plan(n_pad, y_row, 64, 4, 1, eye=True), base)   # restored knobs, the same list
+
+
 # ------------------------------------------------------------------ identity-augmented lists (gradient path)
 def eye_live(i, q, nblk, yb):
     """Block i holds a nonzero row in panel q's columns: training blocks always, the y row's block always, extra

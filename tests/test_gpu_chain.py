@@ -192,6 +192,7 @@ def test_timed_out_wait_falls_back_to_the_launch_path():
     (info = -1, W left half factored).  The same run() call re-assembles and factors on the launch path and
     counts the fallback; the result is the oracle's -LML."""
     before = engine.CHAIN_FALLBACKS
+    t_before = engine.nat.chain_timeouts()
     engine.nat.tune("chain_force_timeout", 1)
     try:
         f, (x, y) = _run(2000, 0, 1)
@@ -200,6 +201,8 @@ def test_timed_out_wait_falls_back_to_the_launch_path():
     assert engine.CHAIN_FALLBACKS == before          # (verified lazily: nothing read yet)
     assert int(f.info.cpu()[0]) == 0                 # the first read re-runs it
     assert engine.CHAIN_FALLBACKS == before + 1
+    # the device counts the aborted launch once (gpk_chain_stats out[4], the bench's check of its timed region)
+    assert engine.nat.chain_timeouts() == t_before + 1
     assert float(f.nlml().cpu()[0]) == pytest.approx(o.nlml(SE, [0.1], 1e-2, x, y), rel=1e-9)
     # with verification off the timeout surfaces as an infrastructure error, never as "not PD"
     engine.CHAIN_VERIFY = False

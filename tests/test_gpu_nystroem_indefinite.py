@@ -98,3 +98,43 @@ def test_gradient_matches_the_oracle(noise):
     exp = np.concatenate([np.asarray(gh[0]).reshape(-1), [gn]])
     assert np.max(np.abs(got - exp)) <= 1e-6 * np.max(np.abs(exp)), (got, exp)
     assert np.max(np.abs(zt.grad.numpy() - gz)) <= 1e-6 * np.max(np.abs(gz))
+
+
+def _inputs_with_a_duplicate(seed=21):
+    """The same inputs with the last inducing input replaced by a copy of the first: K_mm keeps its negative
+    eigenvalues and gains an exact zero one, below tf.linalg.pinv's cutoff (dropped)."""
+    x, y, z = _inputs(seed)
+    z = z.copy()
+    z[-1] = z[0]
+    return x, y, z
+
+
+def test_kmm_with_a_duplicate_is_indefinite_with_a_dropped_eigenvalue():
+    _, _, z = _inputs_with_a_duplicate()
+    lam = np.linalg.eigvalsh(o.kernel_matrix(TREE, HYP, z, z))
+    cut = 10 * M * np.finfo(np.float64).eps * np.abs(lam).max()
+    assert (lam < -cut).sum() >= 2 and (np.abs(lam) <= cut).sum() == 1
+
+
+@pytest.mark.parametrize("handling", ["STRICT_INVERSE", "PSEUDO_INVERSE"])
+def test_indefinite_kmm_with_dropped_eigenvalues_metric_and_gradient(handling):
+    """the signed reverse mode where an indefinite K_mm also has eigenvalues below the cutoff (the
+    kept x dropped block of pinv's reverse mode, Metrics/_approx_grad.py nystroem_logdet) -- value rel 1e-9,
+    gradients 1e-6 max-relative against the autodiff oracle (torch's tape through pinv's SVD with TF's cutoff)."""
+    x, y, z = _inputs_with_a_duplicate()
+    noise = 0.5
+    met = _metric(_gp(x, y), mht.NumericalMatrixHandlingType[handling])
+    h = [torch.tensor(v, dtype=F64, requires_grad=True) for v in HYP]
+    nz = torch.tensor(noise, dtype=F64, requires_grad=True)
+    zt = torch.tensor(z, dtype=F64, requires_grad=False)
+    out = met.get_metric(h, nz, zt)
+    exp_v = o.nystroem_nlml(TREE, HYP, noise, x, y, z, handling=handling)
+    print("duplicate inducing input, %s: -LML %.12g vs oracle %.12g" % (handling, float(out.detach()), exp_v))
+    assert abs(float(out.detach()) - exp_v) <= 1e-9 * abs(exp_v)
+    out.sum().backward()
+    nl, gh, gn, _ = ad.nystroem_nlml_and_grad(TREE, HYP, noise, x, y, z, handling)
+    assert abs(nl - exp_v) <= 1e-9 * abs(exp_v)
+    got = np.concatenate([h[0].grad.numpy().reshape(-1), [float(nz.grad)]])
+    exp = np.concatenate([np.asarray(gh[0]).reshape(-1), [gn]])
+    print("gradient", got, "oracle", exp)
+    assert np.max(np.abs(got - exp)) <= 1e-6 * np.max(np.abs(exp)), (got, exp)

@@ -132,6 +132,37 @@ def test_handlings_of_an_indefinite_covariance_large(handling, n):
     assert rel(got, ref) <= 1e-8, (got, ref)
 
 
+@pytest.mark.parametrize("handling", [H.STRICT_INVERSE, H.PSEUDO_INVERSE])
+def test_handlings_of_an_indefinite_covariance_beyond_16384(handling):
+    """the eigendecomposition fallback above its old n <= 16384 cap (Metrics.py raised there; the
+    reference's tf.linalg.inv / pinv take any n, M/Metrics.py:132-136).  n = 16400 SE inputs in 8 clusters 10 apart,
+    shuffled: K - 0.3 I is a permuted block-diagonal indefinite matrix, so the reference alpha and log|det| come
+    from numpy's eigh block by block (no eigenvalue near pinv's cutoff: pinv = inv).  NLL rel <= 1e-8."""
+    n, nc, noise = 16400, 8, -0.3
+    rng = np.random.default_rng(100)
+    per = n // nc
+    x = np.concatenate([10.0 * c + rng.uniform(0, 1, per) for c in range(nc)])
+    perm = rng.permutation(n)
+    xs = x[perm]
+    y = np.sin(6 * xs) + 0.1 * np.random.default_rng(7).standard_normal(n)
+    fit, logdet = 0.0, 0.0
+    for c in range(nc):
+        idx = np.nonzero((xs >= 10.0 * c) & (xs < 10.0 * c + 1.0))[0]
+        lam, V = np.linalg.eigh(o.k_noised(SE, [0.1], noise, xs[idx].reshape(-1, 1)))
+        assert np.min(np.abs(lam)) > 1e-3
+        fit += float(y[idx] @ (V @ ((V.T @ y[idx]) / lam)))
+        logdet += float(np.sum(np.log(np.abs(lam))))
+    ref = 0.5 * fit + 0.5 * logdet + 0.5 * n * np.log(2.0 * np.pi)
+    di = DataInput(xs.reshape(-1, 1), y.reshape(-1, 1), xs[:8].reshape(-1, 1), y[:8].reshape(-1, 1))
+    di.set_mean_function(ZeroMeanFunction(1))
+    g = GaussianProcess(make_kernel(SE, 1), ZeroMeanFunction(1))
+    g.set_data_input(di)
+    met = get_metric_by_type(MetricType.LL, g, numerical_matrix_handling=handling)
+    got = float(met.get_metric(hyp_list([0.1]), T(noise)).reshape(-1)[0])
+    print("n = %d %s: -LML %.12g vs numpy blockwise %.12g (rel %.2e)" % (n, handling.name, got, ref, rel(got, ref)))
+    assert rel(got, ref) <= 1e-8, (got, ref)
+
+
 def test_pseudo_inverse_of_a_singular_covariance():
     """Duplicated inputs and zero noise: K is singular (rank 150 of 300), pinv truncates below
     10 n eps max|lam| exactly like tf.linalg.pinv.  alpha compared through K alpha (= the projection

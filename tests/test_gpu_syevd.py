@@ -101,3 +101,37 @@ def test_syevd_large_indefinite(m):
     assert np.max(np.abs(np.sort(lam) - ref)) <= 1e-12 * sc
     assert np.max(np.abs(A @ V - V * lam)) <= 1e-11 * sc
     assert np.max(np.abs(V.T @ V - np.eye(m))) <= 1e-11
+
+
+def _clustered_indefinite(n=16400, nc=8, seed=100):
+    """K - 0.3 I of n SE inputs (l = 0.1) in nc clusters 10 apart, the points shuffled: a permuted block-diagonal
+    matrix (cross-cluster entries exp(-4050) round to exactly 0) whose spectrum is the union of the blocks' -- so
+    numpy checks it block by block.  Returns (x shuffled, A, reference eigenvalues sorted)."""
+    rng = np.random.default_rng(seed)
+    per = n // nc
+    x = np.concatenate([10.0 * c + rng.uniform(0, 1, per) for c in range(nc)])
+    ref = np.sort(np.concatenate([np.linalg.eigvalsh(o.k_noised(("SE", {}), [0.1], -0.3, x[c * per:(c + 1) * per]
+                                                                   .reshape(-1, 1))) for c in range(nc)]))
+    perm = rng.permutation(n)
+    xs = x[perm].reshape(-1, 1)
+    return xs, ref
+
+
+def test_syevd_beyond_16384_rows():
+    """gpk_syevd above the old 16384 cap: at m = 16400 the top merge's rows no longer fit in LDS and
+    dc_gather_kernel stages them in the workspace.  A permuted block-diagonal indefinite K - 0.3 I (16288
+    eigenvalues in a cluster at -0.3): eigenvalues vs numpy block by block <= 1e-12 max|lam|, residual
+    |A V - V diag(lam)| and orthogonality |V^T V - I| <= 1e-11 (checked on the device by torch's fp64 matmul)."""
+    xs, ref = _clustered_indefinite()
+    m = xs.shape[0]
+    A = torch.tensor(o.k_noised(("SE", {}), [0.1], -0.3, xs), device="cuda")
+    lam, V = engine.syevd(A)
+    sc = float(np.max(np.abs(ref)))
+    err = float(np.max(np.abs(np.sort(lam.cpu().numpy()) - ref)))
+    res = float((A @ V - V * lam[None, :]).abs().max())
+    orth = float((V.T @ V - torch.eye(m, dtype=torch.float64, device="cuda")).abs().max())
+    print("m = %d: eigenvalues max err %.2e (x max|lam| %.3g), residual %.2e, orthogonality %.2e" % (
+        m, err / sc, sc, res / sc, orth))
+    assert err <= 1e-12 * sc
+    assert res <= 1e-11 * sc
+    assert orth <= 1e-11
