@@ -197,6 +197,9 @@ struct Tune {
   int64_t chain_corner_tail;   //   ... except the last this many panels, which keep chain_group
   int64_t chain_group_la;      // deferred (grouped) tile updates only for block columns at least this many columns
                                // past the group's last panel
+  int64_t asm_f32_fast;   // f32 K build of a single SE / MAT32 / MAT52 node: the interior tiles through f32_fast_kernel
+                          // (f64 distances, f32 transcendentals; 0: every tile through the general f64 loop, A/B)
+  int64_t la_per_stream;  // look-ahead side streams per caller stream (1) instead of one set per host thread (0)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -223,7 +226,8 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_MAX_P_EYE", 16640), env_i64("GPK_ASM_FEAT", 1),
                          env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 3072),
                          env_i64("GPK_CHAIN_GROUP_CORNER", 16), env_i64("GPK_CHAIN_CORNER_TAIL", 8),
-                         env_i64("GPK_CHAIN_GROUP_LA", 2)};
+                         env_i64("GPK_CHAIN_GROUP_LA", 2), env_i64("GPK_ASM_F32_FAST", 1),
+                         env_i64("GPK_LA_PER_STREAM", 0)};
   return t;
 }
 
@@ -252,6 +256,7 @@ const Knob kKnobs[] = {
     {"asm_feat", &Tune::asm_feat},           {"chain_min_p", &Tune::chain_min_p},
     {"chain_min_p_eye", &Tune::chain_min_p_eye}, {"chain_group_corner", &Tune::chain_group_corner},
     {"chain_corner_tail", &Tune::chain_corner_tail}, {"chain_group_la", &Tune::chain_group_la},
+    {"asm_f32_fast", &Tune::asm_f32_fast},   {"la_per_stream", &Tune::la_per_stream},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -305,22 +310,38 @@ void release_side_streams() {
   g_side_all.clear();
 }
 
-SideStream* side_stream() {
-  thread_local std::vector<SideStream*> cache;
+// per_stream (gpk_tune "la_per_stream"): one set per caller stream as well, so that factorisations pipelined on
+// several caller streams each keep their own look-ahead (a shared set serialises them: 305.6 evals/s);
+// at most kSidePerThread sets per (thread, device), the oldest caller's set reused beyond that
+constexpr size_t kSidePerThread = 8;
+SideStream* side_stream(hipStream_t caller = nullptr, bool per_stream = false) {
+  thread_local std::map<std::pair<int, hipStream_t>, SideStream*> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
-  if ((int)cache.size() <= dev) cache.resize(dev + 1, nullptr);
-  if (!cache[dev]) {
+  const hipStream_t key_s = per_stream ? caller : nullptr;
+  SideStream*& slot = cache[{dev, key_s}];
+  if (!slot) {
     std::lock_guard<std::mutex> lk(g_side_mu);
     static bool registered = false;
     if (!registered) {
       std::atexit(release_side_streams);
       registered = true;
     }
-    cache[dev] = new SideStream();  // owned by g_side_all (released at exit)
-    g_side_all.push_back(cache[dev]);
+    size_t mine = 0;
+    for (const auto& kv : cache)
+      if (kv.first.first == dev && kv.second) ++mine;
+    if (per_stream && mine >= kSidePerThread) {
+      for (const auto& kv : cache)
+        if (kv.first.first == dev && kv.second) {
+          slot = kv.second;
+          break;
+        }
+    } else {
+      slot = new SideStream();  // owned by g_side_all (released at exit)
+      g_side_all.push_back(slot);
+    }
   }
-  SideStream& ss = *cache[dev];
+  SideStream& ss = *slot;
   if (!ss.panel_s) {
     int least = 0, greatest = 0, ncu = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
@@ -868,6 +889,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
 
 namespace gpk {
 bool tune_asm_feat() { return tune_now().asm_feat != 0; }
+bool tune_asm_f32_fast() { return tune_now().asm_f32_fast != 0; }
 }  // namespace gpk
 
 extern "C" {
@@ -1037,7 +1059,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   const bool la = tn.lookahead == 1 || (tn.lookahead == 2 && lay->p / NB >= tn.la_min_blocks);
   SideStream* ss = nullptr;
   if (la) {
-    ss = side_stream();
+    ss = side_stream(s, tn.la_per_stream != 0);
     if (!ss) return fail_hip(hipErrorInvalidValue, "side stream");
   }
   hipStream_t sp = !la ? s : tn.panel_stream == 1 ? s : tn.panel_stream == 2 ? ss->panel_np : ss->panel_s;

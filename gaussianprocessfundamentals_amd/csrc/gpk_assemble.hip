@@ -785,6 +785,106 @@ __global__ __launch_bounds__(256, GPK_FAST_MINB) void pair_fast_kernel(gpk_kdesc
   }
 }
 
+// ------------------------------------------------------------------ f32 K build of a single base node
+// C3's precision (fp32 storage + f32 MFMA factorisation): a single SE (direct norm) / Matern-3/2 /
+// Matern-5/2 node written as f32.  The general instantiation evaluates every element in f64 (library exp / sqrt,
+// ~50 f64 VALU operations) and rounds; here the squared distance stays f64 (the differences of the scaled points,
+// as the reference's direct form; no cancellation) and the element's transcendental part runs on the f32 hardware
+// instructions (v_sqrt_f32, v_exp_f32: a few operations instead of ~35):
+//   SE     sg 2^(s * (-0.5 il2 log2 e))
+//   MAT32  sg (1 + f) 2^(-f log2 e),           f = sqrt(3 s il2)
+//   MAT52  sg (1 + f + f^2 / 3) 2^(-f log2 e), f = sqrt(5 s il2)      (= ((1 + f) + 5 d^2 / (3 l^2)) e^-f)
+// with s the squared Euclidean distance of the (ARD-scaled) points, or f = c d1 il of the L1 distance d1 for the
+// reference's L1 Matern forms (K/BaseKernels.py:702-720, :859-880).  Element error against the f64 value: a few f32
+// ulps (kernel-matrix tests: 4e-6 of max |K|); K stays exactly symmetric (the f64 differences are antisymmetric, the
+// sums run in one order) and its diagonal is (f32)(sg + noise) as in the general path.  One 256-thread workgroup per
+// chunk of consecutive lower tiles (the tile row's points kept in LDS between tiles): lane c owns column c (its
+// point in registers), wave w the rows 16 w .. 16 w + 15; whole 256-B tile rows per store.  Tiles with test, padding
+// or identity rows go to a device list for the general instantiation; y-row / zero tail tiles are written here.
+template <int D, int OP, bool L1>
+__global__ __launch_bounds__(256) void f32_fast_kernel(gpk_kdesc kd, AsmArgs a, int64_t ntl, int chunk) {
+  __shared__ double rp[ATILE * D];
+  const int b = blockIdx.y;
+  const int64_t nm = member_n(a, b), mm = member_m(a, b);
+  const double* hyp = a.hyp + (int64_t)b * a.hyp_stride;
+  const gpk_node nd = kd.nodes[0];
+  const FastNode fn = make_fast_node(nd, hyp, D);
+  const bool ard = (nd.flags & GPK_NODE_ARD) != 0;
+  double il[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) il[k] = ard ? 1.0 / hyp[nd.hyp_offset + k] : 1.0;
+  constexpr double LOG2E = 1.4426950408889634;
+  // exponent / distance scales (f64 products, rounded once to f32 per element)
+  const double cse = -0.5 * fn.il2 * LOG2E;                              // SE: s -> log2 of the value
+  const double cm2 = (OP == GPK_OP_MAT52 ? 5.0 : 3.0) * fn.il2;          // MAT, Euclidean: s -> f^2
+  const double cm1 = (OP == GPK_OP_MAT52 ? SQRT5 : SQRT3) * fn.il;       // MAT, L1: d1 -> f
+  const float sg = (float)fn.sg;
+  const float kself = (float)(fn.sg + a.noise[(int64_t)b * a.noise_stride]);
+  float* const Wb = reinterpret_cast<float*>(a.W) + (int64_t)b * a.w_bs;
+  const double* Xb = a.X + (int64_t)b * a.x_bs;
+  const int tid = (int)threadIdx.x, c = tid & 63, w = tid >> 6;
+  int64_t loaded = -1;
+  const int64_t t_end = std::min<int64_t>(ntl, ((int64_t)blockIdx.x + 1) * chunk);
+  for (int64_t t = (int64_t)blockIdx.x * chunk; t < t_end; ++t) {
+    int64_t ti, tj;
+    lower_tile(a, t, ti, tj);
+    const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
+    if (gi0 >= a.n_pad + mm) {
+      // tail tiles: y^T on the y row, zeros elsewhere (the general loop's CLS_Y / CLS_ZERO rows)
+      const int64_t gj = gj0 + c;
+      const float yv = gj < nm ? (float)a.y[(int64_t)b * a.y_bs + gj] : 0.0f;
+      for (int rr = w; rr < ATILE; rr += 4) Wb[(gi0 + rr) * a.ld + gj] = gi0 + rr == a.y_row ? yv : 0.0f;
+      continue;
+    }
+    if (!(gi0 + ATILE <= nm && gj0 + ATILE <= nm)) {
+      if (tid == 0) {
+        int32_t* tl = const_cast<int32_t*>(a.tlist);
+        const int k = atomicAdd(tl, 1);
+        tl[1 + 3 * k] = b;
+        tl[2 + 3 * k] = (int32_t)ti;
+        tl[3 + 3 * k] = (int32_t)tj;
+      }
+      continue;
+    }
+    if (ti != loaded) {
+      if (loaded >= 0) __syncthreads();  // (every wave done with the previous row points)
+      for (int e = tid; e < ATILE * D; e += 256) {
+        const int pt = e / D, k = e - pt * D;
+        rp[e] = Xb[(gi0 + pt) * D + k] * il[k];
+      }
+      __syncthreads();
+      loaded = ti;
+    }
+    const int64_t gj = gj0 + c;
+    double xc[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xc[k] = Xb[gj * D + k] * il[k];
+    float* const Wc = Wb + gi0 * a.ld + gj;
+    const bool diag = ti == tj;
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const int row = 16 * w + i;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const double dlt = rp[row * D + k] - xc[k];
+        s = L1 ? s + fabs(dlt) : fma(dlt, dlt, s);
+      }
+      float v;
+      if (OP == GPK_OP_SE) {
+        v = sg * __builtin_amdgcn_exp2f((float)(s * cse));
+      } else {
+        const float f = L1 ? (float)(s * cm1) : __builtin_amdgcn_sqrtf((float)(s * cm2));
+        const float e = __builtin_amdgcn_exp2f(-f * (float)LOG2E);
+        const float poly = OP == GPK_OP_MAT52 ? fmaf(f, fmaf(f, 1.0f / 3.0f, 1.0f), 1.0f) : 1.0f + f;
+        v = sg * (poly * e);
+      }
+      if (diag && row == c) v = kself;
+      Wc[(int64_t)row * a.ld] = v;
+    }
+  }
+}
+
 // TREE: the instantiation for kernel trees (its interior loop holds two column points in registers;
 // single-node kernels get the lighter instantiation and keep four waves per SIMD); 3: two-leaf SE + periodic trees
 // on MFMA (pair_mfma_tile), tiles outside its error bounds through the generic loop -- an instantiation of its own,
@@ -963,8 +1063,9 @@ __global__ __launch_bounds__(256, TREE == 3 ? GPK_ASM3_MINB : 1) void assemble_k
   // (TREE 4: TREE 3's body over the tile list -- the tiles pair_fast_kernel left: diagonal, edge, outside its
   // bounds -- in a persistent loop; an instantiation of its own without the register bound of TREE 3's, whose
   // occupancy its few tiles do not need)
-  constexpr int TB = TREE == 4 ? 3 : TREE;
-  const bool list = TREE == 4;
+  // (TREE 5: TREE 0's body over the tile list f32_fast_kernel left)
+  constexpr int TB = TREE == 4 ? 3 : TREE == 5 ? 0 : TREE;
+  const bool list = TREE >= 4;
   const int cnt = list ? a.tlist[0] : 1;
   for (int e = list ? (int)blockIdx.x : 0; e < cnt; e += list ? (int)gridDim.x : 1) {
     int b;
@@ -1653,6 +1754,55 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
       scratch = nullptr;
     }
   }
+  // f32, one SE (direct) / MAT32 / MAT52 node: f32_fast_kernel over the grid (interior and tail tiles), then the general
+  // instantiation over the tiles it left (TREE 5; the list lives in the same pool's stream-ordered scratch)
+  if (dtype == GPK_F32 && tree == 0 && !a.plain && !a.generic && a.A == nullptr && a.ntile > 0 && tune_asm_f32_fast() &&
+      (a.d == 1 || a.d == 2 || a.d == 3 || a.d == 4 || a.d == 8)) {
+    const gpk_node nd = kd.nodes[0];
+    const bool se = nd.op == GPK_OP_SE && !(nd.flags & GPK_NODE_SE_EXPANDED);
+    const bool mat = nd.op == GPK_OP_MAT32 || nd.op == GPK_OP_MAT52;
+    hipMemPool_t pool = (se || mat) ? feat_pool() : nullptr;
+    const size_t ntl = (size_t)grid.x * batch;
+    if (pool && hipMallocFromPoolAsync(&scratch, sizeof(int32_t) * (1 + 3 * ntl), pool, s) == hipSuccess) {
+      af.tlist = static_cast<const int32_t*>(scratch);
+      {
+        const hipError_t em = hipMemsetAsync(scratch, 0, sizeof(int32_t), s);
+        if (em != hipSuccess) {
+          (void)hipFreeAsync(scratch, s);
+          return em;
+        }
+      }
+      const int64_t tiles = (int64_t)grid.x;
+      const int chunk = GPK_FAST_CHUNK;
+      const dim3 cgrid((unsigned)((tiles + chunk - 1) / chunk), (unsigned)batch, 1);
+      // (L1: the reference's Matern distance beyond D = 1; at D = 1 both forms are |x - y|)
+      const bool l1 = mat && !(nd.flags & GPK_NODE_STANDARD) && a.d > 1;
+#define GPK_F32_LAUNCH(DD)                                                                                         \
+  if (se) hipLaunchKernelGGL((f32_fast_kernel<DD, GPK_OP_SE, false>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk);        \
+  else if (nd.op == GPK_OP_MAT32 && l1) hipLaunchKernelGGL((f32_fast_kernel<DD, GPK_OP_MAT32, true>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk); \
+  else if (nd.op == GPK_OP_MAT32) hipLaunchKernelGGL((f32_fast_kernel<DD, GPK_OP_MAT32, false>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk); \
+  else if (l1) hipLaunchKernelGGL((f32_fast_kernel<DD, GPK_OP_MAT52, true>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk); \
+  else hipLaunchKernelGGL((f32_fast_kernel<DD, GPK_OP_MAT52, false>), cgrid, dim3(256), 0, s, kd, af, tiles, chunk);
+      switch (a.d) {
+        case 1: GPK_F32_LAUNCH(1) break;
+        case 2: GPK_F32_LAUNCH(2) break;
+        case 3: GPK_F32_LAUNCH(3) break;
+        case 4: GPK_F32_LAUNCH(4) break;
+        default: GPK_F32_LAUNCH(8) break;
+      }
+#undef GPK_F32_LAUNCH
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        (void)hipFreeAsync(scratch, s);
+        return e;
+      }
+      grid = dim3((unsigned)std::min<size_t>(ntl, 2048), 1, 1);
+      tree = 5;
+    } else {
+      (void)hipGetLastError();
+      scratch = nullptr;
+    }
+  }
   // (above 64 KB -- e.g. an ARD node beside a standard PER node, whose per-point sin / cos take two more point
   // slots, at d = 16: 71 KB; two ARD nodes: 87 KB -- the kernel's dynamic-LDS limit must be raised first)
   {
@@ -1662,13 +1812,14 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
                             : tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<double, 2>)
                                       : tree == 1 ? reinterpret_cast<const void*>(assemble_kernel<double, 1>)
                                                   : reinterpret_cast<const void*>(assemble_kernel<double, 0>))
-                         : (tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<float, 2>)
+                         : (tree == 5 ? reinterpret_cast<const void*>(assemble_kernel<float, 5>)
+                            : tree == 2 ? reinterpret_cast<const void*>(assemble_kernel<float, 2>)
                                       : tree == 1 ? reinterpret_cast<const void*>(assemble_kernel<float, 1>)
                                                   : reinterpret_cast<const void*>(assemble_kernel<float, 0>));
     hipError_t e = ensure_dyn_lds(fn, lds);
     if (e != hipSuccess) return e;
   }
-  if (af.tlist != nullptr) tree = 4;
+  if (af.tlist != nullptr && dtype == GPK_F64) tree = 4;
   if (dtype == GPK_F64) {
     if (tree == 4)
       hipLaunchKernelGGL((assemble_kernel<double, 4>), grid, dim3(256), lds, s, kd, af);
@@ -1681,7 +1832,9 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
     else
       hipLaunchKernelGGL((assemble_kernel<double, 0>), grid, dim3(256), lds, s, kd, a);
   } else {
-    if (tree == 2)
+    if (tree == 5)
+      hipLaunchKernelGGL((assemble_kernel<float, 5>), grid, dim3(256), lds, s, kd, af);
+    else if (tree == 2)
       hipLaunchKernelGGL((assemble_kernel<float, 2>), grid, dim3(256), lds, s, kd, a);
     else if (tree == 1)
       hipLaunchKernelGGL((assemble_kernel<float, 1>), grid, dim3(256), lds, s, kd, a);

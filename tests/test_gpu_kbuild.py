@@ -71,8 +71,79 @@ def test_interior_loop_flags_and_fp32(tree):
     for scaled, expanded in ((True, False), (False, True)):
         gen, fast = _build_both(tree, 4, 200, 0, 1, torch.float64, scaled=scaled, expanded=expanded)
         assert torch.equal(gen, fast)
-    gen, fast = _build_both(tree, 4, 200, 30, 1, torch.float32)
+    # (fp32 single nodes take f32_fast_kernel by default -- its own f32 arithmetic, tested below; the interior loop
+    # of the general instantiation, with it off, is bitwise the generic loop in fp32 too)
+    old = nat.tune("asm_f32_fast", 0)
+    try:
+        gen, fast = _build_both(tree, 4, 200, 30, 1, torch.float32)
+    finally:
+        nat.tune("asm_f32_fast", old)
     assert torch.equal(gen, fast)
+
+
+F32_TREES = [("SE", {}), ("SE", {"ard": True}), ("MAT32", {}), ("MAT32", {"ard": True, "standard": True}),
+             ("MAT52", {"ard": True, "standard": True}), ("MAT52", {})]
+
+
+def _build_f32(tree, d, n, m, batch, scaled):
+    """The augmented matrix of `tree` in f32 with asm_f32_fast on and off, and in f64 (the general path, which the
+    oracle tests pin): three [batch, p, p] CPU tensors (untriangled: diagonal tiles hold both triangles)."""
+    set_flags(scaled=scaled)
+    try:
+        kd = engine.kernel_descriptor(make_kernel(tree, d), d)
+    finally:
+        set_flags()
+    rng = np.random.default_rng(d * 1000 + n + m)
+    dev = engine.device()
+    X = torch.as_tensor(rng.uniform(0, 1, (n, d)), device=dev).contiguous()
+    Xs = torch.as_tensor(rng.uniform(0, 1, (m, d)), device=dev).contiguous() if m else None
+    Y = torch.as_tensor(rng.standard_normal(n), device=dev).reshape(1, -1).contiguous()
+    H = torch.as_tensor(0.2 + rng.uniform(0, 1, (batch, kd.n_hyp)), device=dev).contiguous()
+    NZ = torch.tensor([1e-2], dtype=torch.float64, device=dev)
+    out = []
+    for dtype, fast in ((torch.float32, 1), (torch.float32, 0), (torch.float64, 0)):
+        old = nat.tune("asm_f32_fast", fast)
+        try:
+            f = engine.AugmentedFactorization(n, d, m, batch, dtype)
+            f.W.fill_(7.0)
+            _assemble(kd, f.layout, H, NZ, X, Xs, Y, f.W)
+            out.append(torch.stack([f.w(b) for b in range(batch)]).cpu())
+        finally:
+            nat.tune("asm_f32_fast", old)
+    return out, f.layout
+
+
+@pytest.mark.parametrize("tree", F32_TREES)
+@pytest.mark.parametrize("d", [1, 2, 3, 4, 8])
+def test_f32_fast_kbuild_against_the_f64_build(tree, d):
+    """f32 K build of one SE / MAT32 / MAT52 node (f32_fast_kernel: f64 distances, the f32 hardware sqrt / exp): its
+    interior tiles within 4e-6 of max|K| of the f64 build of the same inputs (C3's fp32 config); every other tile --
+    test rows, the padding block, the y row and the zero rows -- bitwise the general path's f32 values; the training
+    diagonal exactly (f32)(sg + noise) and the diagonal tiles exactly symmetric."""
+    n, m = 300, 37
+    (fast, gen, ref), lay = _build_f32(tree, d, n, m, 2, scaled=(d % 2 == 0))
+    n64 = 64 * (n // 64)
+    lower = torch.tril(torch.ones(lay.p, lay.p, dtype=torch.bool))
+    interior = torch.zeros(lay.p, lay.p, dtype=torch.bool)
+    interior[:n64, :n64] = True
+    interior &= lower
+    # (lower 64-tiles only are written; compare the lower triangle plus the diagonal tiles' upper halves)
+    written = lower.clone()
+    for t in range(lay.p // 64):
+        written[64 * t:64 * t + 64, 64 * t:64 * t + 64] = True
+    for b in range(2):
+        err = float((fast[b].double() - ref[b])[interior].abs().max())
+        scale = float(ref[b][interior].abs().max())
+        assert err <= 4e-6 * scale, (err, scale)
+        outside = written & ~interior
+        for t in range(n64 // 64):   # (diagonal tiles' upper halves are interior too)
+            outside[64 * t:64 * t + 64, 64 * t:64 * t + 64] = False
+        assert torch.equal(fast[b][outside], gen[b][outside])
+        dg = torch.arange(n)
+        assert torch.equal(fast[b][dg, dg], gen[b][dg, dg])
+        for t in range(n64 // 64):
+            blk = fast[b][64 * t:64 * t + 64, 64 * t:64 * t + 64]
+            assert torch.equal(blk, blk.T)
 
 
 def test_interior_loop_ragged_members_bitwise():
