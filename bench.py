@@ -470,9 +470,41 @@ def main():
     fact = facts[0]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(P - 1)]
     step_no = [0]
-    gathered = [torch.empty(2 * chunk * world, dtype=torch.float64, device=dev) if use_dist else None
-                for _ in range(P)]
-    mine = [torch.full((2 * chunk,), float("nan"), dtype=torch.float64, device=dev) for _ in range(P)]
+    # The sweep's collective, kept off the factorisation streams: every P steps (one per slot in flight) a comm
+    # stream waits for those steps' factorisations, packs their (nlml, info) and issues ONE all-gather over RCCL
+    # for all of them (asynchronous; two alternating buffers, reused only after the gather that read them).  Per
+    # step on the factorisation streams this leaves one event record instead of two copy kernels and a collective
+    # whose stream ordering tied every factorisation queue to RCCL's.
+    comm = torch.cuda.Stream(dev) if use_dist else None
+    done_ev = [torch.cuda.Event() for _ in range(P)] if use_dist else None
+    mine = [torch.full((P, 2 * chunk), float("nan"), dtype=torch.float64, device=dev) for _ in range(2)]
+    gathered = [torch.empty(world * P * 2 * chunk, dtype=torch.float64, device=dev) if use_dist else None
+                for _ in range(2)]
+    works = [None, None]
+    pending = []
+    flushes = [0]
+
+    def flush():
+        if not pending:
+            return None
+        u = flushes[0] % 2
+        flushes[0] += 1
+        with torch.cuda.stream(comm):
+            if works[u] is not None:
+                works[u].wait()   # (device-side: the gather that read this buffer two flushes ago is done)
+            buf = mine[u]
+            for row, j in enumerate(pending):
+                comm.wait_event(done_ev[j])
+                # (device views, no settle: a persistent run is not waited for here; a timed-out one would
+                # arrive as info = -1 and fail the all-gather check)
+                nl_dev, info_dev = facts[j].unsettled_results()
+                nl_dev.record_stream(comm)
+                info_dev.record_stream(comm)
+                buf[row, :batch] = nl_dev
+                buf[row, chunk:chunk + batch] = info_dev.to(torch.float64)
+            works[u] = dist.all_gather_into_tensor(gathered[u], buf.reshape(-1), async_op=True)
+        pending.clear()
+        return u
 
     def step(slot=None):
         i = step_no[0] % P if slot is None else slot
@@ -484,21 +516,26 @@ def main():
             else:
                 f.run(kd, H, H.shape[1], NZ, 0, X, 0, Y, 0)
             if use_dist:
-                # (device views, no settle: a persistent run is not waited for here; a timed-out one would
-                # arrive as info = -1 and fail the all-gather check)
-                nl_dev, info_dev = f.unsettled_results()
-                mine[i][:batch] = nl_dev
-                mine[i][chunk:chunk + batch] = info_dev.to(torch.float64)
-                dist.all_gather_into_tensor(gathered[i], mine[i])
+                done_ev[i].record(streams[i])
+        if use_dist:
+            if i in pending:
+                flush()
+            pending.append(i)
+            if len(pending) == P:
+                flush()
 
     # every slot once before the warm-up (setup, not a warm-up step): a stream's first launch allocates libgpk's
     # per-stream scratch, a device synchronisation that would otherwise land in the timed region whenever the
     # warm-up has fewer steps than there are slots (C2 at 8 in flight: 198 instead of 1715 evals/s with 3)
     for i in range(P):
         step(slot=i)
+    if use_dist:
+        flush()
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
+    if use_dist:
+        flush()
     torch.cuda.synchronize()
     # persistent launches are not verified inside the timed region (no step reads a result): a launch whose waits
     # timed out (info = -1, its candidates not evaluated) is counted on the device (gpk_chain_stats) and its
@@ -511,6 +548,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if use_dist:
+        flush()   # (the last steps' results: every evaluation of the timed region is gathered inside it)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if use_dist:
@@ -559,10 +598,14 @@ def main():
     info = int(fact.info.abs().max().item())
     gathered_ok = None
     if use_dist:
-        # one more step on slot 0: every rank's (nlml, info) pairs must have arrived through RCCL
+        # one more step on slot 0, gathered on its own: every rank's (nlml, info) pairs must have arrived via RCCL
+        torch.cuda.synchronize()   # (the events passes' gathers are done with both buffers)
+        pending.clear()
+        mine[flushes[0] % 2].fill_(float("nan"))
         step(slot=0)
+        u = flush()
         torch.cuda.synchronize()
-        g = gathered[0].view(world, 2 * chunk).cpu()
+        g = gathered[u].view(world, P, 2 * chunk)[:, 0, :].cpu()
         total = len(c4_candidates()) if sweep else world * batch
         vals = g[:, :chunk].reshape(-1)
         gathered_ok = bool(int(torch.isfinite(vals).sum()) == total and float(g[:, chunk:].nan_to_num(0).abs().max()) == 0.0)

@@ -200,6 +200,7 @@ struct Tune {
   int64_t asm_f32_fast;   // f32 K build of a single SE / MAT32 / MAT52 node: the interior tiles through f32_fast_kernel
                           // (f64 distances, f32 transcendentals; 0: every tile through the general f64 loop, A/B)
   int64_t la_per_stream;  // look-ahead side streams per caller stream (1) instead of one set per host thread (0)
+  int64_t chain_group_eye;  // identity-augmented plans: panels per deferred tile update (0: chain_group's rule)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -227,7 +228,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 3072),
                          env_i64("GPK_CHAIN_GROUP_CORNER", 16), env_i64("GPK_CHAIN_CORNER_TAIL", 8),
                          env_i64("GPK_CHAIN_GROUP_LA", 2), env_i64("GPK_ASM_F32_FAST", 1),
-                         env_i64("GPK_LA_PER_STREAM", 0)};
+                         env_i64("GPK_LA_PER_STREAM", 0), env_i64("GPK_CHAIN_GROUP_EYE", 0)};
   return t;
 }
 
@@ -257,6 +258,7 @@ const Knob kKnobs[] = {
     {"chain_min_p_eye", &Tune::chain_min_p_eye}, {"chain_group_corner", &Tune::chain_group_corner},
     {"chain_corner_tail", &Tune::chain_corner_tail}, {"chain_group_la", &Tune::chain_group_la},
     {"asm_f32_fast", &Tune::asm_f32_fast},   {"la_per_stream", &Tune::la_per_stream},
+    {"chain_group_eye", &Tune::chain_group_eye},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -497,9 +499,10 @@ int chain_group_for(int64_t knob, int64_t n_pad) {
 struct ChainKnobs {
   int group, uq, group_corner, corner_tail, group_la;
 };
-ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad) {
+ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye) {
   ChainKnobs k;
-  k.group = std::max(1, std::min(chain_group_for(tn.chain_group, n_pad), 16));
+  const int64_t gk = eye && tn.chain_group_eye > 0 ? tn.chain_group_eye : tn.chain_group;
+  k.group = std::max(1, std::min(chain_group_for(gk, n_pad), 16));
   k.uq = (int)std::max<int64_t>(0, std::min<int64_t>(2, tn.chain_uq));
   k.group_corner = (int)std::max<int64_t>(1, std::min<int64_t>(tn.chain_group_corner, 16));
   k.corner_tail = (int)std::max<int64_t>(0, tn.chain_corner_tail);
@@ -785,7 +788,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   size_t ctl_ints = 0;
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
-    const ChainKnobs kn = chain_knobs(tn, lay->n_pad);
+    const ChainKnobs kn = chain_knobs(tn, lay->n_pad, eye);
     const int nmem = lay->batch;
     auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, nmem, eye ? 1 : 0, kn.group, kn.uq,
                                kn.group_corner, kn.corner_tail, kn.group_la);
@@ -843,7 +846,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.w_bs = lay->w_batch_stride;
   a.inv_bs = lay->inv_batch_stride;
   a.ctl_stride = 2 * (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
-  a.uq = (int32_t)chain_knobs(tn, lay->n_pad).uq;
+  a.uq = (int32_t)chain_knobs(tn, lay->n_pad, eye).uq;
   // rows of L_kk^-1 behind D's early flag: later (more of the panel solve early) for short chains, where the
   // diagonal chain is all there is; earlier for long ones, where the S tasks' waiting CUs cost tile-update time
   // (N = 4096: 112 rows 1.501 vs 96 rows 1.515 ms; 6144 / 8192 2.42 / 4.44 vs 2.37 / 4.39, profiles/r04ab_*)
@@ -2125,7 +2128,7 @@ int chain_plan_impl(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, i
   if (eye && (y_row - n_pad < 1 || y_row - n_pad > n_pad))
     return fail_arg(2, "y_row (identity extra rows: n_pad + n with 0 < n <= n_pad)");
   if (!ntasks) return fail_arg(ap_ntasks, "ntasks");
-  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, 1, chain_knobs(tune_now(), n_pad), eye);
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, 1, chain_knobs(tune_now(), n_pad, eye), eye);
   if (ord.empty()) {
     return fail_hip(hipErrorUnknown, "chain_order: a task exceeds the device's dependency bound");
   }

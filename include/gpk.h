@@ -412,7 +412,8 @@ int gpk_timing_reset(void);
  * waits for another's workgroups (bench.py's C2 schedule: 8 in flight, 64 workgroups each on 256 CUs).
  * With "chain" 1 (auto) factorisations of fewer than "chain_min_p" (768) rows -- identity-augmented ones:
  * "chain_min_p_eye" (3072) -- keep the launch path (a handful of panels: its few launches are faster).
- * Identity-augmented plans defer the corner's tile updates (-K^-1, read by no later task) in groups of
+ * Identity-augmented plans take "chain_group_eye" panels per deferred tile update (0, the default: chain_group's
+ * rule) and defer the corner's tile updates (-K^-1, read by no later task) in groups of
  * "chain_group_corner" (16) panels, except the last "chain_corner_tail" (8) panels, which keep "chain_group"; a
  * deferred (grouped) update covers only block columns at least "chain_group_la" (2) columns past the group's last
  * panel.  Every knob the planner reads is part of its plan cache key.

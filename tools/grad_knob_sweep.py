@@ -63,7 +63,7 @@ if __name__ == "__main__":
     las = [1, 2, 3] if not quick else [2]
     ref = None
     for g, gc, tl, la in itertools.product(groups, corners, tails, las):
-        with nat.thread_tune(chain_group=g, chain_group_corner=gc, chain_corner_tail=tl, chain_group_la=la):
+        with nat.thread_tune(chain_group_eye=g, chain_group_corner=gc, chain_corner_tail=tl, chain_group_la=la):
             med, mn, last = timed(m)
         if ref is None:
             ref = last
