@@ -201,6 +201,9 @@ struct Tune {
                           // (f64 distances, f32 transcendentals; 0: every tile through the general f64 loop, A/B)
   int64_t la_per_stream;  // look-ahead side streams per caller stream (1) instead of one set per host thread (0)
   int64_t chain_group_eye;  // identity-augmented plans: panels per deferred tile update (0: chain_group's rule)
+  int64_t chain_xcd;      // persistent launch: the diagonal chain's tasks as a second list, claimed first by up to
+                          // chain_xcd_seats workgroups of XCD 0 (their hand-offs in one L2); 0: one list
+  int64_t chain_xcd_seats;
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -228,7 +231,8 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 3072),
                          env_i64("GPK_CHAIN_GROUP_CORNER", 16), env_i64("GPK_CHAIN_CORNER_TAIL", 8),
                          env_i64("GPK_CHAIN_GROUP_LA", 2), env_i64("GPK_ASM_F32_FAST", 1),
-                         env_i64("GPK_LA_PER_STREAM", 0), env_i64("GPK_CHAIN_GROUP_EYE", 0)};
+                         env_i64("GPK_LA_PER_STREAM", 0), env_i64("GPK_CHAIN_GROUP_EYE", 0),
+                         env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16)};
   return t;
 }
 
@@ -258,7 +262,8 @@ const Knob kKnobs[] = {
     {"chain_min_p_eye", &Tune::chain_min_p_eye}, {"chain_group_corner", &Tune::chain_group_corner},
     {"chain_corner_tail", &Tune::chain_corner_tail}, {"chain_group_la", &Tune::chain_group_la},
     {"asm_f32_fast", &Tune::asm_f32_fast},   {"la_per_stream", &Tune::la_per_stream},
-    {"chain_group_eye", &Tune::chain_group_eye},
+    {"chain_group_eye", &Tune::chain_group_eye}, {"chain_xcd", &Tune::chain_xcd},
+    {"chain_xcd_seats", &Tune::chain_xcd_seats},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -402,13 +407,34 @@ int32_t* fuse_counters(hipStream_t s) {
 // kernel needs (every task waits only for tasks claimed before it), and puts the diagonal chain ahead
 // of the trailing tiles whenever both are ready.
 struct ChainPlan {
-  int32_t* tasks = nullptr;  // device [ntasks][4]
-  int32_t ntasks = 0;
+  int32_t* tasks = nullptr;  // device [ntasks + ntasks_b][4]: list A, then list B (chain_xcd)
+  int32_t ntasks = 0, ntasks_b = 0;
   int32_t nblk = 0, nsl = 0, nbc = 0;
 };
 std::mutex g_chain_mu;
 // key: device, n_pad, y_row, grid, members, eye, and every knob chain_order reads (ChainKnobs)
-std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int>, ChainPlan> g_chain_plans;
+std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int>, ChainPlan> g_chain_plans;
+
+enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
+
+// chain_xcd: the diagonal chain's tasks -- D, the panel solves of the next diagonal block's slices (S / SQ), its
+// quarter updates (UQ) or, without quarters, its per-slice updates (U32 of block column k + 1 on its own rows) --
+// move to list B, in their order; the rest stays list A.  Both lists keep the topological order.  Returns nb.
+int32_t chain_split_lists(std::vector<int32_t>& ord) {
+  std::vector<int32_t> la, lb;
+  la.reserve(ord.size());
+  for (size_t t = 0; t + 3 < ord.size(); t += 4) {
+    const int tyg = ord[t], ty = tyg & 3, g = ((tyg >> 2) & 15) + 1, k = ord[t + 1], r = ord[t + 2], j = ord[t + 3];
+    const bool chain = ty == CHT_D || (ty == CHT_S && (r >> 2) == k + 1) ||
+                       (ty == CHT_U32 && (g > 1 || (j == k + 1 && (r >> 2) == k + 1)));
+    std::vector<int32_t>& dst = chain ? lb : la;
+    dst.insert(dst.end(), ord.begin() + t, ord.begin() + t + 4);
+  }
+  const int32_t nb = (int32_t)(lb.size() / 4);
+  ord.assign(la.begin(), la.end());
+  ord.insert(ord.end(), lb.begin(), lb.end());
+  return nb;
+}
 // Counter scratch of the persistent launch, per (host thread, device, stream): the counters are zeroed
 // by a memset enqueued before each launch, so two threads enqueueing on one stream (torch's null stream
 // is shared by every thread) must never share them -- memset A, memset B, launch A, launch B would hand
@@ -484,7 +510,6 @@ int32_t* g_chain_trace = nullptr;  // GPK_CHAIN_TRACE=1: pinned host words the k
 uint64_t* g_chain_times = nullptr;  // GPK_CHAIN_TIMES=1: device stamps per task of the last profiled launch
 int64_t g_chain_times_n = 0;
 
-enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
 // panels per deferred tile update: the knob, or (0) 4 below 80 diagonal blocks and 8 from there -- the deep
 // updates' MFMA rate starts to matter more than the columns they hold back (N = 8192 4.46 / 4.49 ms with 4 / 8,
@@ -790,17 +815,20 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     std::lock_guard<std::mutex> lk(g_chain_mu);
     const ChainKnobs kn = chain_knobs(tn, lay->n_pad, eye);
     const int nmem = lay->batch;
+    // (two lists need workgroups of both roles: at least 8 per XCD)
+    const int xcd = tn.chain_xcd != 0 && grid >= 64 ? 1 : 0;
     auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, nmem, eye ? 1 : 0, kn.group, kn.uq,
-                               kn.group_corner, kn.corner_tail, kn.group_la);
+                               kn.group_corner, kn.corner_tail, kn.group_la, xcd);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
-      const std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, nmem, kn, eye);
+      std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, nmem, kn, eye);
       if (ord.empty()) {
         // (an internal failure, not a bad argument: reported like a HIP error, > 0)
         return fail_hip(hipErrorUnknown, "chain_order: a task exceeds the device's dependency bound");
       }
       ChainPlan p;
-      p.ntasks = (int32_t)(ord.size() / 4);
+      p.ntasks_b = xcd ? chain_split_lists(ord) : 0;
+      p.ntasks = (int32_t)(ord.size() / 4) - p.ntasks_b;
       p.nblk = (int32_t)(lay->n_pad / NB);
       p.nsl = (int32_t)(lay->y_row / 32 + 1);
       p.nbc = (int32_t)(lay->y_row / NB + 1);
@@ -833,6 +861,10 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.info = info_dev;
   a.tasks = plan.tasks;
   a.ntasks = env_i64("GPK_CHAIN_MAX_TASKS", 0) > 0 ? (int32_t)std::min<int64_t>(plan.ntasks, env_i64("GPK_CHAIN_MAX_TASKS", 0)) : plan.ntasks;  // (debugging)
+  a.ntasks_b = plan.ntasks_b;
+  if (a.ntasks_b > 0) a.ntasks = plan.ntasks;  // (GPK_CHAIN_MAX_TASKS: one list only)
+  a.xcd_b = plan.ntasks_b > 0 ? 0 : -1;
+  a.b_seats = (int32_t)std::max<int64_t>(1, std::min<int64_t>(tn.chain_xcd_seats, grid / 16));
   a.dbg = (int32_t)env_i64("GPK_CHAIN_DBG", 0);
   a.ctl = ctl;
   a.dflag = ctl + 4;
@@ -866,13 +898,14 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     // (GPK_DIAG_PROF builds: the D tasks' phase stamps follow the task stamps, 8 steps x 8 waves x 6 per block,
     // read back as extra "tasks" of gpk_chain_times)
     const int64_t extra = GPK_DIAG_PROF ? (int64_t)plan.nblk * 8 * 8 : 0;
-    if (g_chain_times_n < a.ntasks + extra) {
+    const int64_t nt = (int64_t)a.ntasks + a.ntasks_b;
+    if (g_chain_times_n < nt + extra) {
       if (g_chain_times) hipFree(g_chain_times);
-      GPK_HIP(hipMalloc(&g_chain_times, (size_t)(a.ntasks + extra) * 6 * sizeof(uint64_t)), "chain times");
-      g_chain_times_n = a.ntasks + extra;
+      GPK_HIP(hipMalloc(&g_chain_times, (size_t)(nt + extra) * 6 * sizeof(uint64_t)), "chain times");
+      g_chain_times_n = nt + extra;
     }
     a.times = g_chain_times;
-    if (extra) a.dprof = g_chain_times + (size_t)a.ntasks * 6;
+    if (extra) a.dprof = g_chain_times + (size_t)nt * 6;
   }
   if (env_i64("GPK_CHAIN_TRACE", 0)) {
     std::lock_guard<std::mutex> lk(g_chain_mu);

@@ -174,9 +174,12 @@ struct ChainArgs {
   int64_t ld;
   double* Winv;
   int32_t* info;
-  const int32_t* tasks;  // [ntasks][4]: type (0 D, 1 S, 2 U32, 3 BLK), panel, slice / block row, block column
-  int32_t ntasks;
-  int32_t* ctl;          // [0] claim counter, [1] timeout flag
+  const int32_t* tasks;  // [ntasks + ntasks_b][4]: type (0 D, 1 S, 2 U32, 3 BLK), panel, slice / block row, block column
+  int32_t ntasks;        // tasks of list A (all of them unless xcd_b >= 0)
+  int32_t ntasks_b;      // chain_xcd: list B (the diagonal chain's D / S / UQ tasks), claimed first by the workgroups
+  int32_t xcd_b;         //   running on XCD xcd_b (up to b_seats of them; -1: one list), then by everyone
+  int32_t b_seats;
+  int32_t* ctl;          // [0] claim counter (list A), [1] timeout flag, [2] list B's claim counter, [3] B seats
   int32_t* dflag;        // [nblk]: D(k) done
   int32_t* sdone;        // [nblk][nsl]: S(k, r) done
   int32_t* ucnt;         // [nsl][nbc]: panels applied to slice r of block column j

@@ -1225,21 +1225,50 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int kprev
   return chain_wait_set<12>(a, p, v, t0);
 }
 
+// XCD of the executing workgroup (HW_REG_XCC_ID, bits 3:0)
+__device__ __forceinline__ int xcc_id() { return (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xf); }
+
 __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   int32_t* slot = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(sm) + CHAIN_SLOT_OFF);
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int total = a.ntasks + a.ntasks_b;
+  // Two lists (chain_xcd, a.xcd_b >= 0): up to b_seats workgroups of XCD xcd_b claim list B (the diagonal chain:
+  // its hand-offs and operands stay in one L2) and everyone else list A; a workgroup whose own list is exhausted
+  // claims from the other.  Both lists are subsequences of one topological order, and a workgroup holds a task of
+  // its own list until that list is exhausted, so with at least one workgroup of each role the earliest claimed,
+  // unfinished task only ever waits for finished tasks (tests/test_chain_plan.py simulates it).  One list
+  // (ntasks_b = 0): list A, then an empty list B.
+  int lst = 0;
+  if (wave == 0) {
+    if (a.xcd_b >= 0 && xcc_id() == a.xcd_b && claim_ticket(a.ctl + 3) < a.b_seats) lst = 1;
+    slot[3] = lst;
+  }
+  __syncthreads();
+  lst = __builtin_amdgcn_readfirstlane(slot[3]);
+  bool switched = false;
   // every branch of this loop is wave-uniform (wave; the task fields through readfirstlane)
   for (;;) {
     if (wave == 0) {
-      int t = claim_ticket(a.ctl);
-      if (t < a.ntasks && __builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) t = a.ntasks;  // timed out
-      slot[0] = t;
-      chain_trace(a, 0, t);
+      int g = total;
+      for (;;) {
+        const int n = lst ? a.ntasks_b : a.ntasks;
+        const int t = claim_ticket(a.ctl + (lst ? 2 : 0));
+        if (t < n) {
+          g = lst ? a.ntasks + t : t;
+          break;
+        }
+        if (switched) break;  // (both lists exhausted)
+        switched = true;
+        lst ^= 1;
+      }
+      if (g < total && __builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) g = total;  // timed out
+      slot[0] = g;
+      chain_trace(a, 0, g);
     }
     __syncthreads();
     const int t = __builtin_amdgcn_readfirstlane(slot[0]);
-    if (t >= a.ntasks) break;
+    if (t >= total) break;
     const int tyg = __builtin_amdgcn_readfirstlane(a.tasks[4 * t]);
     // BLK: updates over g panels; U32 with g > 1: the quarter g - 2 task (UQ); first: the cells the task
     // updates have no earlier update (identity-augmented lists: their counter waits are for 0); member

@@ -11,6 +11,8 @@ waits on counters before it runs.  Here, for several augmented shapes and worker
     Cholesky of K + noise I (the quantities of gpbasics/Statistics/CovarianceMatrix.py:247-265 and
     Metrics/LogLikelihood.py:30-65).
 """
+import heapq
+
 import numpy as np
 import pytest
 
@@ -404,3 +406,111 @@ def test_chain_plan_eye_reproduces_the_inverse(n, group, uq):
     got = np.tril(W[n_pad:n_pad + n, n_pad:n_pad + n])
     np.testing.assert_allclose(got, -np.tril(Kinv), rtol=0, atol=1e-9 * np.abs(Kinv).max())
     np.testing.assert_allclose(-W[y_row, n_pad:n_pad + n], Kinv @ y, rtol=0, atol=1e-8 * np.abs(Kinv @ y).max())
+
+
+# ------------------------------------------------------------------ two task lists (gpk_tune "chain_xcd")
+def split_lists(tasks):
+    """chain_split_lists (gpk_abi.hip): the diagonal chain's tasks -- D, the panel solves of the next diagonal block's
+    slices, its quarter updates (or per-slice updates) -- to list B, in order; the rest is list A."""
+    la, lb = [], []
+    for t in tasks:
+        ty, k, r, j, g = decode(t)
+        chain = ty == D or (ty == S and r // 4 == k + 1) or (ty == U32 and (g > 1 or (j == k + 1 and r // 4 == k + 1)))
+        (lb if chain else la).append(t)
+    return la, lb
+
+
+def simulate_two_lists(tasks, nsl, wa, wb, rng):
+    """Discrete-event run of chain_kernel's claim rule with two lists: wa workgroups claim list A first, wb list B
+    first, a workgroup whose list is exhausted claims from the other; a claimed task starts once every counter it
+    waits for is published.  Asserts progress (no state where claimed tasks wait on counters that no running task
+    will publish and no free workgroup can claim) and, at every start, that each cell the task reads or writes holds
+    the version the one-list (topological) order would give it."""
+    uq = 2 if any(is_sq(t) for t in tasks) else any(decode(t)[0] == U32 and decode(t)[4] > 1 for t in tasks)
+    order = {tuple(t): i for i, t in enumerate(tasks)}
+    la, lb = split_lists(tasks)
+    lists = [la, lb]
+    nxt = [0, 0]
+    writers, readers = {}, {}
+    for i, t in enumerate(tasks):
+        rd, wr = cells(t, nsl, uq)
+        for c in wr:
+            writers.setdefault(c, []).append(i)
+        for c in rd - wr:
+            readers.setdefault(c, []).append(i)
+    pub = {}
+    finished = set()
+    dur = {D: 28.0, S: 7.0, U32: 7.0, BLK: 18.0}
+    workers = [{"lst": 0, "sw": False, "task": None, "run": False, "done": False} for _ in range(wa)] + \
+              [{"lst": 1, "sw": False, "task": None, "run": False, "done": False} for _ in range(wb)]
+    running = []   # (finish time, worker index)
+    now = 0.0
+
+    def ready(task):
+        for cnt, idx, v in waits(task, nsl, uq):
+            got = pub.get((cnt, idx))
+            if isinstance(v, int) and v == 0:
+                continue
+            if got is None or got < v:
+                return False
+        return True
+
+    while True:
+        for w in workers:
+            while w["task"] is None and not w["done"]:
+                l = w["lst"]
+                if nxt[l] < len(lists[l]):
+                    w["task"] = lists[l][nxt[l]]
+                    nxt[l] += 1
+                elif not w["sw"]:
+                    w["sw"] = True
+                    w["lst"] ^= 1
+                else:
+                    w["done"] = True
+        for wi, w in enumerate(workers):
+            if w["task"] is not None and not w["run"] and ready(w["task"]):
+                x = order[tuple(w["task"])]
+                rd, wr = cells(w["task"], nsl, uq)
+                for c in rd | wr:   # every earlier writer finished, no later one
+                    for i in writers.get(c, []):
+                        assert (i in finished) == (i < x), "task %d %s: cell %s writer %d" % (x, w["task"], c, i)
+                for c in wr:        # every earlier reader since ... finished (write-after-read)
+                    for i in readers.get(c, []):
+                        if i < x:
+                            assert i in finished, "task %d %s overwrites %s under reader %d" % (x, w["task"], c, i)
+                w["run"] = True
+                ty, g = decode(w["task"])[0], decode(w["task"])[4]
+                heapq.heappush(running, (now + dur[ty] * g * rng.uniform(0.3, 3.0), wi))
+        if not running:
+            stuck = [w["task"] for w in workers if w["task"] is not None]
+            assert not stuck, "deadlock: %d claimed tasks wait, nothing runs (first %s)" % (len(stuck), stuck[0])
+            assert nxt[0] == len(la) and nxt[1] == len(lb)
+            return
+        now, wi = heapq.heappop(running)
+        w = workers[wi]
+        x = order[tuple(w["task"])]
+        finished.add(x)
+        for cnt, idx, v in publishes(w["task"], nsl):
+            if v == "+1":
+                pub[(cnt, idx)] = pub.get((cnt, idx), 0) + 1
+            else:
+                pub[(cnt, idx)] = max(pub.get((cnt, idx), 0), v)
+        w["task"], w["run"] = None, False
+
+
+@pytest.mark.parametrize("n,m", [(300, 0), (1000, 200), (2048, 0), (3000, 40)])
+@pytest.mark.parametrize("group,uq", [(4, 1), (8, 1), (1, 0), (4, 2)])
+def test_chain_plan_two_lists_progress_and_order(n, m, group, uq):
+    """gpk_tune("chain_xcd"): the diagonal chain's tasks as a second list claimed first by a few workgroups of one
+    XCD.  Both lists are subsequences of the planner's topological order; with at least one workgroup per role every
+    run completes and every task sees the one-list versions of its cells (random durations, several pool sizes)."""
+    _lib_or_skip()
+    n_pad, y_row, p = shape(n, m)
+    nsl = y_row // SL + 1
+    rng = np.random.default_rng(n + m + group)
+    for grid in (64, 256):
+        tasks = [tuple(int(v) for v in t) for t in plan(n_pad, y_row, grid, group, uq)]
+        la, lb = split_lists(tasks)
+        assert len(lb) >= n_pad // NB and all(decode(t)[0] != BLK for t in lb)
+        for wa, wb in ((1, 1), (grid - 4, 4), (grid - 16, 16)):
+            simulate_two_lists(tasks, nsl, wa, wb, rng)

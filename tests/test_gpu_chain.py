@@ -98,6 +98,21 @@ def test_chain_plan_variants_bitwise_vs_launch_path(n, m, group, uq):
     assert fc.out.cpu()[0].item() == fl.out.cpu()[0].item()
 
 
+@pytest.mark.parametrize("n,m,uq", [(2100, 40, 1), (4096, 0, 1), (8192, 0, 1), (5000, 0, 0), (5000, 0, 2)])
+def test_chain_two_lists_bitwise_vs_launch_path(n, m, uq):
+    """gpk_tune("chain_xcd"): the diagonal chain's tasks as a second task list claimed first by workgroups of one
+    XCD (tests/test_chain_plan.py simulates its progress and cell order).  Only which workgroup runs a task changes:
+    bitwise the launch path's results, and the persistent launch really ran with it."""
+    with engine.nat.thread_tune(chain_xcd=1, chain_uq=uq):
+        before = engine.nat.chain_stats()["launches"]
+        fc, _ = _run(n, m, 1)
+        assert engine.nat.chain_stats()["launches"] > before
+    fl, _ = _run(n, m, 0)
+    a, b = _lower(fc), _lower(fl)
+    assert int(np.count_nonzero(a.view(np.uint64) != b.view(np.uint64))) == 0
+    assert fc.out.cpu()[0].item() == fl.out.cpu()[0].item()
+
+
 def test_chain_noise_1e8_matches_the_oracle():
     """The reference's default jitter (1e-8, cond(K) ~ 1e10 at N = 256) through the persistent launch."""
     f, (x, y) = _run(1000, 0, 1, noise=1e-8)
