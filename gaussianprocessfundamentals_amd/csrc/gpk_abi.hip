@@ -200,10 +200,12 @@ struct Tune {
   int64_t asm_f32_fast;   // f32 K build of a single SE / MAT32 / MAT52 node: the interior tiles through f32_fast_kernel
                           // (f64 distances, f32 transcendentals; 0: every tile through the general f64 loop, A/B)
   int64_t la_per_stream;  // look-ahead side streams per caller stream (1) instead of one set per host thread (0)
-  int64_t chain_group_eye;  // identity-augmented plans: panels per deferred tile update (0: chain_group's rule)
+  int64_t chain_group_eye;  // identity-augmented plans: panels per deferred tile update (0: chain_group's rule; 8: value +
+                            // gradient N = 8192 11.33 vs 11.11 ms best, profiles/r06b_grad_sweep_8192.jsonl)
   int64_t chain_xcd;      // persistent launch: the diagonal chain's tasks as a second list, claimed first by up to
                           // chain_xcd_seats workgroups of XCD 0 (their hand-offs in one L2); 0: one list
   int64_t chain_xcd_seats;
+  int64_t asm_f32_chunk;  // f32_fast_kernel: consecutive lower tiles per workgroup
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -231,8 +233,9 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 3072),
                          env_i64("GPK_CHAIN_GROUP_CORNER", 16), env_i64("GPK_CHAIN_CORNER_TAIL", 8),
                          env_i64("GPK_CHAIN_GROUP_LA", 2), env_i64("GPK_ASM_F32_FAST", 1),
-                         env_i64("GPK_LA_PER_STREAM", 0), env_i64("GPK_CHAIN_GROUP_EYE", 0),
-                         env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16)};
+                         env_i64("GPK_LA_PER_STREAM", 0), env_i64("GPK_CHAIN_GROUP_EYE", 8),
+                         env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
+                         env_i64("GPK_ASM_F32_CHUNK", 8)};
   return t;
 }
 
@@ -263,7 +266,7 @@ const Knob kKnobs[] = {
     {"chain_corner_tail", &Tune::chain_corner_tail}, {"chain_group_la", &Tune::chain_group_la},
     {"asm_f32_fast", &Tune::asm_f32_fast},   {"la_per_stream", &Tune::la_per_stream},
     {"chain_group_eye", &Tune::chain_group_eye}, {"chain_xcd", &Tune::chain_xcd},
-    {"chain_xcd_seats", &Tune::chain_xcd_seats},
+    {"chain_xcd_seats", &Tune::chain_xcd_seats}, {"asm_f32_chunk", &Tune::asm_f32_chunk},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -926,6 +929,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
 namespace gpk {
 bool tune_asm_feat() { return tune_now().asm_feat != 0; }
 bool tune_asm_f32_fast() { return tune_now().asm_f32_fast != 0; }
+int tune_asm_f32_chunk() { return (int)std::max<int64_t>(1, std::min<int64_t>(64, tune_now().asm_f32_chunk)); }
 }  // namespace gpk
 
 extern "C" {

@@ -825,7 +825,23 @@ __global__ __launch_bounds__(256) void f32_fast_kernel(gpk_kdesc kd, AsmArgs a, 
   const int tid = (int)threadIdx.x, c = tid & 63, w = tid >> 6;
   int64_t loaded = -1;
   const int64_t t_end = std::min<int64_t>(ntl, ((int64_t)blockIdx.x + 1) * chunk);
-  for (int64_t t = (int64_t)blockIdx.x * chunk; t < t_end; ++t) {
+  // the lane's column point of the next tile is loaded while the current one is evaluated (clamped to a valid
+  // training point: tail / edge tiles ignore it)
+  auto col_point = [&](int64_t t, double (&xv)[D]) {
+    int64_t ti2, tj2;
+    lower_tile(a, t, ti2, tj2);
+    const int64_t gjn = std::min<int64_t>(tj2 * ATILE + c, nm - 1);
+#pragma unroll
+    for (int k = 0; k < D; ++k) xv[k] = Xb[gjn * D + k];
+  };
+  double xn[D];
+  int64_t t = (int64_t)blockIdx.x * chunk;
+  if (t < t_end) col_point(t, xn);
+  for (; t < t_end; ++t) {
+    double xc[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xc[k] = xn[k] * il[k];
+    if (t + 1 < t_end) col_point(t + 1, xn);
     int64_t ti, tj;
     lower_tile(a, t, ti, tj);
     const int64_t gi0 = ti * ATILE, gj0 = tj * ATILE;
@@ -856,9 +872,6 @@ __global__ __launch_bounds__(256) void f32_fast_kernel(gpk_kdesc kd, AsmArgs a, 
       loaded = ti;
     }
     const int64_t gj = gj0 + c;
-    double xc[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) xc[k] = Xb[gj * D + k] * il[k];
     float* const Wc = Wb + gi0 * a.ld + gj;
     const bool diag = ti == tj;
 #pragma unroll 4
@@ -1773,7 +1786,7 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
         }
       }
       const int64_t tiles = (int64_t)grid.x;
-      const int chunk = GPK_FAST_CHUNK;
+      const int chunk = tune_asm_f32_chunk();
       const dim3 cgrid((unsigned)((tiles + chunk - 1) / chunk), (unsigned)batch, 1);
       // (L1: the reference's Matern distance beyond D = 1; at D = 1 both forms are |x - y|)
       const bool l1 = mat && !(nd.flags & GPK_NODE_STANDARD) && a.d > 1;
@@ -1796,7 +1809,8 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
         (void)hipFreeAsync(scratch, s);
         return e;
       }
-      grid = dim3((unsigned)std::min<size_t>(ntl, 2048), 1, 1);
+      // (the edge tiles: about one tile row and column per member -- a persistent loop over the list)
+      grid = dim3((unsigned)std::min<size_t>(ntl, 256), 1, 1);
       tree = 5;
     } else {
       (void)hipGetLastError();

@@ -260,6 +260,7 @@ struct TrsvArgs {
 // ----------------------------------------------------------------------------------- launchers
 bool tune_asm_feat();  // gpk_tune("asm_feat") in effect on this thread
 bool tune_asm_f32_fast();  // gpk_tune("asm_f32_fast") in effect on this thread
+int tune_asm_f32_chunk();  // gpk_tune("asm_f32_chunk"), clamped to 1 .. 64
 hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int32_t batch,
                            hipStream_t s);
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s);

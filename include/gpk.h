@@ -412,14 +412,14 @@ int gpk_timing_reset(void);
  * waits for another's workgroups (bench.py's C2 schedule: 8 in flight, 64 workgroups each on 256 CUs).
  * With "chain" 1 (auto) factorisations of fewer than "chain_min_p" (768) rows -- identity-augmented ones:
  * "chain_min_p_eye" (3072) -- keep the launch path (a handful of panels: its few launches are faster).
- * Identity-augmented plans take "chain_group_eye" panels per deferred tile update (0, the default: chain_group's
+ * Identity-augmented plans take "chain_group_eye" (8) panels per deferred tile update (0: chain_group's
  * rule) and defer the corner's tile updates (-K^-1, read by no later task) in groups of
  * "chain_group_corner" (16) panels, except the last "chain_corner_tail" (8) panels, which keep "chain_group"; a
  * deferred (grouped) update covers only block columns at least "chain_group_la" (2) columns past the group's last
  * panel.  Every knob the planner reads is part of its plan cache key.
  * "asm_f32_fast" (1: the f32 K build of a single SE / MAT32 / MAT52 node writes its interior tiles with f64
  * distances and the f32 hardware sqrt / exp -- a few f32 ulps from the f64 build; 0: every tile through the
- * general f64 evaluation, A/B), "la_per_stream" (1: the look-ahead's side streams are created per caller stream
+ * general f64 evaluation, A/B; "asm_f32_chunk" (8) consecutive lower tiles per workgroup), "la_per_stream" (1: the look-ahead's side streams are created per caller stream
  * -- up to 8 sets per host thread and device -- so factorisations pipelined on several streams keep their own
  * look-ahead; 0, the default: one set per host thread and device).
  * "asm_feat" (1: the K build of a two-leaf SE + periodic tree at D = 4 or 8 computes the per-point features in a

@@ -221,7 +221,7 @@ def run_tasks(W, tasks, nblk):
 
 
 def plan(n_pad, y_row, grid, group, uq=1, eye=False):
-    with nat.thread_tune(chain_group=group, chain_uq=uq):
+    with nat.thread_tune(chain_group=group, chain_group_eye=group, chain_uq=uq):
         return nat.chain_plan(n_pad, y_row, grid, eye)
 
 
