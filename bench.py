@@ -86,9 +86,6 @@ def parse():
     ap.add_argument("--fuse-trsm", type=int, default=None,
                     help="panel solve inside the diagonal-block launch (libgpk fuse_trsm); default 0 when "
                          "--pipeline > 1, else the library default (1)")
-    ap.add_argument("--la-per-stream", action="store_true",
-                    help="look-ahead side streams per pipelined stream (libgpk la_per_stream), so that --lookahead 1 "
-                         "applies with --pipeline > 1")
     ap.add_argument("--chain", type=int, default=None,
                     help="single-member factorisations as one persistent launch (libgpk chain); default 0 when "
                          "--pipeline > 1, else the library default")
@@ -445,8 +442,6 @@ def main():
              PERSIST_PIPELINE if persist else DEFAULT_PIPELINE_OTHER))
     la = args.lookahead if args.lookahead is not None else (0 if P > 1 else 2)
     nat.tune("lookahead", la)
-    if args.la_per_stream:
-        nat.tune("la_per_stream", 1)
     # batches overlapping on P > 1 streams: the panel solve stays a separate launch (fused, its redundant
     # workgroups take CUs from the other batches' updates: C5 at 3 in flight 38.2 -> 36.4 evals/s)
     if args.fuse_trsm is not None or P > 1:

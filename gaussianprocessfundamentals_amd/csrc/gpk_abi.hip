@@ -199,7 +199,6 @@ struct Tune {
                                // past the group's last panel
   int64_t asm_f32_fast;   // f32 K build of a single SE / MAT32 / MAT52 node: the interior tiles through f32_fast_kernel
                           // (f64 distances, f32 transcendentals; 0: every tile through the general f64 loop, A/B)
-  int64_t la_per_stream;  // look-ahead side streams per caller stream (1) instead of one set per host thread (0)
   int64_t chain_group_eye;  // identity-augmented plans: panels per deferred tile update (0: chain_group's rule; 8: value +
                             // gradient N = 8192 11.33 vs 11.11 ms best, profiles/r06b_grad_sweep_8192.jsonl)
   int64_t chain_xcd;      // persistent launch: the diagonal chain's tasks as a second list, claimed first by up to
@@ -233,7 +232,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_MIN_P", 768), env_i64("GPK_CHAIN_MIN_P_EYE", 3072),
                          env_i64("GPK_CHAIN_GROUP_CORNER", 16), env_i64("GPK_CHAIN_CORNER_TAIL", 8),
                          env_i64("GPK_CHAIN_GROUP_LA", 2), env_i64("GPK_ASM_F32_FAST", 1),
-                         env_i64("GPK_LA_PER_STREAM", 0), env_i64("GPK_CHAIN_GROUP_EYE", 8),
+                         env_i64("GPK_CHAIN_GROUP_EYE", 8),
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
                          env_i64("GPK_ASM_F32_CHUNK", 8)};
   return t;
@@ -264,7 +263,7 @@ const Knob kKnobs[] = {
     {"asm_feat", &Tune::asm_feat},           {"chain_min_p", &Tune::chain_min_p},
     {"chain_min_p_eye", &Tune::chain_min_p_eye}, {"chain_group_corner", &Tune::chain_group_corner},
     {"chain_corner_tail", &Tune::chain_corner_tail}, {"chain_group_la", &Tune::chain_group_la},
-    {"asm_f32_fast", &Tune::asm_f32_fast},   {"la_per_stream", &Tune::la_per_stream},
+    {"asm_f32_fast", &Tune::asm_f32_fast},
     {"chain_group_eye", &Tune::chain_group_eye}, {"chain_xcd", &Tune::chain_xcd},
     {"chain_xcd_seats", &Tune::chain_xcd_seats}, {"asm_f32_chunk", &Tune::asm_f32_chunk},
 };
@@ -320,38 +319,22 @@ void release_side_streams() {
   g_side_all.clear();
 }
 
-// per_stream (gpk_tune "la_per_stream"): one set per caller stream as well, so that factorisations pipelined on
-// several caller streams each keep their own look-ahead (a shared set serialises them: 305.6 evals/s);
-// at most kSidePerThread sets per (thread, device), the oldest caller's set reused beyond that
-constexpr size_t kSidePerThread = 8;
-SideStream* side_stream(hipStream_t caller = nullptr, bool per_stream = false) {
-  thread_local std::map<std::pair<int, hipStream_t>, SideStream*> cache;
+SideStream* side_stream() {
+  thread_local std::vector<SideStream*> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0) return nullptr;
-  const hipStream_t key_s = per_stream ? caller : nullptr;
-  SideStream*& slot = cache[{dev, key_s}];
-  if (!slot) {
+  if ((int)cache.size() <= dev) cache.resize(dev + 1, nullptr);
+  if (!cache[dev]) {
     std::lock_guard<std::mutex> lk(g_side_mu);
     static bool registered = false;
     if (!registered) {
       std::atexit(release_side_streams);
       registered = true;
     }
-    size_t mine = 0;
-    for (const auto& kv : cache)
-      if (kv.first.first == dev && kv.second) ++mine;
-    if (per_stream && mine >= kSidePerThread) {
-      for (const auto& kv : cache)
-        if (kv.first.first == dev && kv.second) {
-          slot = kv.second;
-          break;
-        }
-    } else {
-      slot = new SideStream();  // owned by g_side_all (released at exit)
-      g_side_all.push_back(slot);
-    }
+    cache[dev] = new SideStream();  // owned by g_side_all (released at exit)
+    g_side_all.push_back(cache[dev]);
   }
-  SideStream& ss = *slot;
+  SideStream& ss = *cache[dev];
   if (!ss.panel_s) {
     int least = 0, greatest = 0, ncu = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
@@ -1099,7 +1082,7 @@ static int potrf_impl(const gpk_layout* lay, void* W, void* Winv, int32_t* info_
   const bool la = tn.lookahead == 1 || (tn.lookahead == 2 && lay->p / NB >= tn.la_min_blocks);
   SideStream* ss = nullptr;
   if (la) {
-    ss = side_stream(s, tn.la_per_stream != 0);
+    ss = side_stream();
     if (!ss) return fail_hip(hipErrorInvalidValue, "side stream");
   }
   hipStream_t sp = !la ? s : tn.panel_stream == 1 ? s : tn.panel_stream == 2 ? ss->panel_np : ss->panel_s;
