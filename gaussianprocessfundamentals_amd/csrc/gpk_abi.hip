@@ -204,7 +204,8 @@ struct Tune {
   int64_t chain_xcd;      // persistent launch: the diagonal chain's tasks as a second list, claimed first by up to
                           // chain_xcd_seats workgroups of XCD 0 (their hand-offs in one L2); 0: one list
   int64_t chain_xcd_seats;
-  int64_t asm_f32_chunk;  // f32_fast_kernel: consecutive lower tiles per workgroup
+  int64_t asm_f32_chunk;  // f32_fast_kernel: consecutive lower tiles per workgroup (C3: 1 / 2 / 4 / 8 / 16 0.062 / 0.059 /
+                          // 0.059 / 0.063 / 0.073 ms, profiles/r06c_kb_c3_chunks.txt)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -234,7 +235,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_GROUP_LA", 2), env_i64("GPK_ASM_F32_FAST", 1),
                          env_i64("GPK_CHAIN_GROUP_EYE", 8),
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
-                         env_i64("GPK_ASM_F32_CHUNK", 8)};
+                         env_i64("GPK_ASM_F32_CHUNK", 4)};
   return t;
 }
 

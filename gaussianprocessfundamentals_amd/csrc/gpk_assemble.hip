@@ -853,7 +853,7 @@ __global__ __launch_bounds__(256) void f32_fast_kernel(gpk_kdesc kd, AsmArgs a, 
       continue;
     }
     if (!(gi0 + ATILE <= nm && gj0 + ATILE <= nm)) {
-      if (tid == 0) {
+      if (tid == 0 && a.tlist) {  // (NULL only when the host ruled edge tiles out: launch_assemble's no_edges)
         int32_t* tl = const_cast<int32_t*>(a.tlist);
         const int k = atomicAdd(tl, 1);
         tl[1 + 3 * k] = b;
@@ -1774,11 +1774,16 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
     const gpk_node nd = kd.nodes[0];
     const bool se = nd.op == GPK_OP_SE && !(nd.flags & GPK_NODE_SE_EXPANDED);
     const bool mat = nd.op == GPK_OP_MAT32 || nd.op == GPK_OP_MAT52;
-    hipMemPool_t pool = (se || mat) ? feat_pool() : nullptr;
+    // every tile interior (training rows and columns) or tail (y / zero rows): n = n_pad, no test, identity or
+    // dense rows, no ragged members -- then no edge tile can occur and the kernel runs alone (no list, no memset)
+    const bool no_edges = a.n == a.n_pad && a.m == 0 && !a.nb && !a.mb && !a.eye && a.E == nullptr &&
+                          (a.tcol_hi <= 0 || a.tcol_hi >= a.ntile);
+    hipMemPool_t pool = (se || mat) && !no_edges ? feat_pool() : nullptr;
     const size_t ntl = (size_t)grid.x * batch;
-    if (pool && hipMallocFromPoolAsync(&scratch, sizeof(int32_t) * (1 + 3 * ntl), pool, s) == hipSuccess) {
+    if ((se || mat) &&
+        (no_edges || (pool && hipMallocFromPoolAsync(&scratch, sizeof(int32_t) * (1 + 3 * ntl), pool, s) == hipSuccess))) {
       af.tlist = static_cast<const int32_t*>(scratch);
-      {
+      if (scratch) {
         const hipError_t em = hipMemsetAsync(scratch, 0, sizeof(int32_t), s);
         if (em != hipSuccess) {
           (void)hipFreeAsync(scratch, s);
@@ -1806,9 +1811,10 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
 #undef GPK_F32_LAUNCH
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) {
-        (void)hipFreeAsync(scratch, s);
+        if (scratch) (void)hipFreeAsync(scratch, s);
         return e;
       }
+      if (no_edges) return hipSuccess;
       // (the edge tiles: about one tile row and column per member -- a persistent loop over the list)
       grid = dim3((unsigned)std::min<size_t>(ntl, 256), 1, 1);
       tree = 5;

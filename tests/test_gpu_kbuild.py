@@ -225,3 +225,15 @@ def test_d16_ard_vjp_and_gradient_above_64kb_lds(tree):
     exp = np.concatenate([np.asarray(v, dtype=np.float64).reshape(-1) for v in grads] + [[gnoise]])
     assert abs(float(f.nlml().cpu()[0]) - nl) <= 1e-10 * abs(nl)
     assert np.max(np.abs(g - exp)) <= 1e-8 * np.max(np.abs(exp))
+
+
+@pytest.mark.parametrize("tree", [("MAT52", {"ard": True, "standard": True}), ("SE", {})])
+def test_f32_fast_kbuild_without_edge_tiles(tree):
+    """n a multiple of 128, no test rows: every tile is interior or a y / zero tail tile, so f32_fast_kernel runs
+    alone (no tile list, no general launch) -- C3's shape in miniature.  Interior within 4e-6 of max|K| of the f64
+    build, the tail rows bitwise the general path's."""
+    n = 512
+    (fast, gen, ref), lay = _build_f32(tree, 4, n, 0, 1, scaled=False)
+    err = float((torch.tril(fast[0][:n, :n]).double() - torch.tril(ref[0][:n, :n])).abs().max())
+    assert err <= 4e-6 * float(ref[0][:n, :n].abs().max())
+    assert torch.equal(torch.tril(fast[0])[n:], torch.tril(gen[0])[n:])
