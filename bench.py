@@ -48,8 +48,8 @@ DEFAULT_PIPELINE_OTHER = 4
 # ~850 (more streams than the 8 hardware queues), profiles/r05u_*, r05v_*, r05ac_*, r05ad_*.  (Before round 5
 # every persistent run was verified with a host synchronisation inside run(), which serialised them: r04ae
 # measured no overlap.)
-PERSIST_PIPELINE = 8
-PERSIST_CU_SHARE = 1.0 / 4.0
+PERSIST_PIPELINE = int(os.environ.get("GPK_BENCH_PERSIST_P", "8"))
+PERSIST_CU_SHARE = 1.0 / float(os.environ.get("GPK_BENCH_PERSIST_SHARE", "4"))
 
 CONFIGS = {
     # name: (kernel, d, n, noise, dtype, hyp)
@@ -338,11 +338,12 @@ def oracle_check(cfg_name, n, rows, idx, kname, d, noise, got, known=None):
 
 
 # Hardware queues per process: HIP multiplexes streams onto GPU_MAX_HW_QUEUES in-order hardware queues
-# (4 by default). P pipelined factorisation streams + torch's default stream + RCCL's stream exceed 4,
-# and two streams sharing a queue serialise: the all-gather of one batch then waits behind another
-# batch's updates. Measured with the RCCL path on (--dist, N = 8192, P = 3): 321.7 evals/s with 4
-# queues, 338.1 with 8 (P = 2: 302.1 / 329.5); without RCCL 8 queues change nothing (339.0 vs 339.5).
-HW_QUEUES = int(os.environ.get("GPK_BENCH_HW_QUEUES", "8"))  # 0: leave the runtime default
+# (4 by default). P pipelined factorisation streams + torch's default stream + the comm stream + RCCL's stream
+# share them, and two streams sharing a queue serialise.  Measured with the RCCL path on (--dist, N = 8192,
+# P = 3): 321.7 evals/s with 4 queues, 338.1 with 8 (P = 2: 302.1 / 329.5).  Round 6: C2 (8 persistent launches in
+# flight) 1675 / 1706 evals/s with 8 / 16 queues, its --dist rehearsal 1430 / 1684, the metric 357.3 / 357.3
+# (profiles/r06d_hw_queues.txt) -- 16.
+HW_QUEUES = int(os.environ.get("GPK_BENCH_HW_QUEUES", "16"))  # 0: leave the runtime default
 
 
 def main():
