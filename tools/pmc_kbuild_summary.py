@@ -6,7 +6,7 @@ The K build of the C5 tree is three launches since round 5 (pair_feat_kernel, pa
 assemble_kernel): the counters are summed over every K-build kernel of one build (dispatches grouped per launch of
 the build), and the duration is the sum of their median durations.
 
-usage: python tools/pmc_kbuild_summary.py [dir] [n] [d]"""
+usage: python tools/pmc_kbuild_summary.py [dir] [n] [d] [element bytes: 8, or 4 for C3's f32 build]"""
 import collections
 import csv
 import glob
@@ -15,14 +15,15 @@ import sys
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/kb"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
 d = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+es = int(sys.argv[4]) if len(sys.argv) > 4 else 8
 p = -(-(n + 1) // 128) * 128          # augmented rows (m = 0)
 ntile = p // 64
 elements = ntile * (ntile + 1) // 2 * 64 * 64
-alg_bytes = 8 * p * (p + 64) / 2 + 8 * n * d
+alg_bytes = es * p * (p + 64) / 2 + 8 * n * d
 tot = collections.defaultdict(float)
 cnt = collections.Counter()
 dur = []
-KB = ("assemble_kernel", "pair_fast_kernel", "pair_feat_kernel")
+KB = ("assemble_kernel", "pair_fast_kernel", "pair_feat_kernel", "f32_fast_kernel")
 
 
 def fam(name):
