@@ -421,6 +421,21 @@ __device__ __forceinline__ void st_flag(int32_t* p, int32_t v) {
 // (Per translation unit: only gpk_potrf.hip's chain_kernel waits.)
 static __device__ unsigned long long g_chain_timeouts_dev = 0;
 
+// A wait of the persistent launch timed out: raise the launch's abort word (the first to raise it counts the launch in
+// g_chain_timeouts_dev) and set info = -1 on every member where no non-positive pivot was found first.  One wave.
+__device__ __forceinline__ void chain_report_timeout(int32_t* ctl, int32_t* info, int nmem) {
+  const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (lane == __builtin_amdgcn_readfirstlane(lane)) {
+    const int32_t was = __hip_atomic_exchange((gi32*)(ctl + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (was == 0) __hip_atomic_fetch_add(&g_chain_timeouts_dev, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int m = 0; m < nmem; ++m) {
+    int32_t zero = 0;
+    __hip_atomic_compare_exchange_strong((gi32*)(info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // one wave: wait until *p >= v; false on timeout (which it reports) or after another task's timeout.  Plain
 // values (the task bodies call it too, and they must not take the kernel argument by reference)
 __device__ __forceinline__ bool chain_wait_v(const int32_t* p, int32_t v, int32_t* ctl, int32_t* info, int nmem,
@@ -429,19 +444,7 @@ __device__ __forceinline__ bool chain_wait_v(const int32_t* p, int32_t v, int32_
   while (force_abort || __builtin_amdgcn_readfirstlane(ld_flag(p)) < v) {
     if (__builtin_amdgcn_readfirstlane(ld_flag(ctl + 1)) != 0) return false;
     if (force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)timeout) {
-      // (one lane: the exchange tells the first waiter to time out in this launch, which counts it)
-      const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-      if (lane == __builtin_amdgcn_readfirstlane(lane)) {
-        const int32_t was = __hip_atomic_exchange((gi32*)(ctl + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (was == 0)
-          __hip_atomic_fetch_add(&g_chain_timeouts_dev, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      // every member may be incomplete now: info = -1 wherever no non-positive pivot was found first
-      for (int m = 0; m < nmem; ++m) {
-        int32_t zero = 0;
-        __hip_atomic_compare_exchange_strong((gi32*)(info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      }
+      chain_report_timeout(ctl, info, nmem);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);

@@ -700,12 +700,7 @@ __device__ __forceinline__ bool chain_wait_set(const ChainArgs& a, const int32_t
     if (all) return true;
     if (__builtin_amdgcn_readfirstlane(ld_flag(a.ctl + 1)) != 0) return false;
     if (a.force_abort || __builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)a.timeout) {
-      st_flag(a.ctl + 1, 1);
-      for (int m = 0; m < a.nmem; ++m) {
-        int32_t zero = 0;
-        __hip_atomic_compare_exchange_strong((gi32*)(a.info + m), &zero, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      }
+      chain_report_timeout(a.ctl, a.info, a.nmem);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);

@@ -3,6 +3,8 @@
 set -o pipefail
 T=r06fin; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_chain.py -m gpu -q --timeout 240 --timeout-method thread > $O/tests_chain.log 2>&1 || { tail -5 $O/tests_chain.log; exit 1; }
+tail -1 $O/tests_chain.log
 rm -rf gpurun_out/pmc
 GPK_LOOKAHEAD=0 PMC_FILE=tools/pmc_traffic.txt bash tools/pmc_pass.sh || exit 1
 python tools/pmc_traffic.py metric_b64 gpurun_out/pmc profiles/pmc_traffic.json || exit 1
