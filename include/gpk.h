@@ -420,6 +420,10 @@ int gpk_timing_reset(void);
  * "asm_f32_fast" (1: the f32 K build of a single SE / MAT32 / MAT52 node writes its interior tiles with f64
  * distances and the f32 hardware sqrt / exp -- a few f32 ulps from the f64 build; 0: every tile through the
  * general f64 evaluation, A/B; "asm_f32_chunk" (4) consecutive lower tiles per workgroup).
+ * "chain_xcd" (0; 1: the persistent launch's diagonal-chain tasks -- D, the next diagonal block's panel solves and
+ * quarter updates -- as a second task list claimed first by up to "chain_xcd_seats" (16) workgroups of XCD 0, the
+ * rest by everyone else, each workgroup falling back to the other list once its own is exhausted; measured no
+ * faster).
  * "asm_feat" (1: the K build of a two-leaf SE + periodic tree at D = 4 or 8 computes the per-point features in a
  * pre-pass and runs its interior tiles on the f64 MFMA fast-tile kernel; 0: every tile stages its points itself
  * -- the same bits, slower; A/B).
