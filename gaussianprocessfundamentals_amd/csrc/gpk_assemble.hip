@@ -644,13 +644,21 @@ __global__ __launch_bounds__(256) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a,
 #endif
 // Workgroup c of member b walks the lower tiles c * chunk .. c * chunk + chunk - 1 (row-major: mostly one tile row,
 // whose feature rows it loads once); each tile as one workgroup per tile would -- the same values bit for bit.
+// GPK_FAST_DMA: the column features are double-buffered in LDS and the next tile's are fetched by LDS-DMA
+// (global_load_lds, no VGPRs) while the current tile is evaluated -- one barrier per tile instead of two, and the
+// feature fetch off the tile's critical path (0: the round-5 form, loaded through VGPRs after the barrier).
+#ifndef GPK_FAST_DMA
+#define GPK_FAST_DMA 1
+#endif
+typedef __attribute__((address_space(3))) void asm_lds_void;
 template <int D, bool MUL>
 __global__ __launch_bounds__(256, GPK_FAST_MINB) void pair_fast_kernel(gpk_kdesc kd, AsmArgs a, int64_t ntl,
                                                                       int chunk) {
 #pragma clang fp contract(on)
   constexpr int FS = 3 * D + 2, SS = D / 4, PS = 2 * D / 4;
+  constexpr int NPC = ATILE * FS / 2;  // 16-B pieces of one tile edge's feature rows
   __shared__ __attribute__((aligned(16))) double fr[ATILE * FS];
-  __shared__ __attribute__((aligned(16))) double fc[ATILE * FS];
+  __shared__ __attribute__((aligned(16))) double fcb[GPK_FAST_DMA ? 2 : 1][ATILE * FS];
   __shared__ double tab[32];
   const int b = blockIdx.y;
   const int64_t nm = member_n(a, b), mm = member_m(a, b);
@@ -659,7 +667,28 @@ __global__ __launch_bounds__(256, GPK_FAST_MINB) void pair_fast_kernel(gpk_kdesc
   if (threadIdx.x < 32) tab[threadIdx.x] = kExp2Tab32[threadIdx.x];
   int64_t loaded = -1;  // the tile row whose features are in fr
   const int64_t t_end = std::min<int64_t>(ntl, ((int64_t)blockIdx.x + 1) * chunk);
-  for (int64_t t = (int64_t)blockIdx.x * chunk; t < t_end; ++t) {
+  // LDS-DMA of tile tt's column features into fcb[buf]: wave w moves 64 pieces per instruction, lane-linear
+  auto dma_col = [&](int64_t tt, int buf) {
+    int64_t ti2, tj2;
+    lower_tile(a, tt, ti2, tj2);
+    const char* src = reinterpret_cast<const char*>(fb + tj2 * ATILE * FS);
+    char* dst = reinterpret_cast<char*>(fcb[buf]);
+    const int lane = (int)threadIdx.x & 63;
+    for (int base = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * 64; base < NPC; base += 256)
+      if (base + lane < NPC)
+        __builtin_amdgcn_global_load_lds(src + (size_t)(base + lane) * 16, (asm_lds_void*)(dst + base * 16), 16, 0, 0);
+  };
+  int cur = 0;
+  if (GPK_FAST_DMA && (int64_t)blockIdx.x * chunk < t_end) dma_col((int64_t)blockIdx.x * chunk, 0);
+  for (int64_t t = (int64_t)blockIdx.x * chunk; t < t_end; ++t, cur ^= (GPK_FAST_DMA ? 1 : 0)) {
+    if (GPK_FAST_DMA) {
+      // this tile's column features have landed (every wave's DMA: vmcnt, then the barrier), and every wave is done
+      // with the previous tile (its LDS reads of fcb[cur ^ 1] and fr); then the next tile's DMA into the other buffer
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 1 < t_end) dma_col(t + 1, cur ^ 1);
+    }
+    double* const fc = fcb[cur];
     // (the lane's offsets recomputed per tile: hoisted out of the loop they would hold registers across it)
     int tid = (int)threadIdx.x;
     asm volatile("" : "+v"(tid));
@@ -690,26 +719,34 @@ __global__ __launch_bounds__(256, GPK_FAST_MINB) void pair_fast_kernel(gpk_kdesc
       }
       continue;
     }
-    if (loaded >= 0) __syncthreads();  // (the previous tile's LDS reads are done)
-    {
+    if (GPK_FAST_DMA) {
+      if (ti != loaded) {  // (a new tile row: its features through VGPRs, behind a barrier of their own)
+        const double2* sr = reinterpret_cast<const double2*>(fb + gi0 * FS);
+        double2* dr = reinterpret_cast<double2*>(fr);
+        for (int e = tid; e < NPC; e += 256) dr[e] = sr[e];
+        loaded = ti;
+        __syncthreads();
+      }
+    } else {
+      if (loaded >= 0) __syncthreads();  // (the previous tile's LDS reads are done)
       const double2* sr = reinterpret_cast<const double2*>(fb + gi0 * FS);
       const double2* sc = reinterpret_cast<const double2*>(fb + gj0 * FS);
       double2* dr = reinterpret_cast<double2*>(fr);
       double2* dc = reinterpret_cast<double2*>(fc);
       if (ti != loaded) {
-        for (int e = tid; e < ATILE * FS / 2; e += 256) {
+        for (int e = tid; e < NPC; e += 256) {
           dr[e] = sr[e];
           dc[e] = sc[e];
         }
       } else {
-        for (int e = tid; e < ATILE * FS / 2; e += 256) dc[e] = sc[e];
+        for (int e = tid; e < NPC; e += 256) dc[e] = sc[e];
       }
       loaded = ti;
     }
     const double a_s = mc[0], lsg_s = mc[1], a_p = mc[2], c_p = mc[3], lsg_p = mc[4];
     const bool diag = ti == tj;
     const double kself = mc[7] + (diag ? a.noise[(int64_t)b * a.noise_stride] : 0.0);
-    __syncthreads();
+    if (!GPK_FAST_DMA) __syncthreads();
     const int lane = tid & 63, w = tid >> 6;
     const int lr = lane & 15, kq = lane >> 4;
     double ase[SS], ape[PS];
