@@ -436,6 +436,8 @@ def main():
     # --pipeline P: P factorisation buffers on P streams, consecutive steps round-robin over them,
     # so that one batch's exposed panel chain (start and tail of the factorisation) overlaps the
     # trailing updates of the next (the batches are independent candidate sets of the sweep)
+    # (f64 only: C3 on 8 f32 persistent launches side by side 428 evals/s against 469 for the f32 launch path at 4 in
+    # flight, profiles/r06k_c3_f32_chain.txt -- one at a time the f32 persistent launch wins, 297 vs 236)
     persist = (args.pipeline is None and args.chain is None and not grad_mode and not sweep and batch == 1 and
                dtn == "f64" and n <= 12288)
     P = max(1, args.pipeline if args.pipeline is not None else
@@ -639,12 +641,12 @@ def main():
             if persist and ov["launches"] > 0 and ov["ms"] > 0:
                 # the persistent launches (timing class "update": the whole factorisation is one chain_kernel
                 # launch) as they run in the timed schedule, P side by side: each launch's algorithmic flops /
-                # its own HIP-event span, against the fp64 MFMA peak of the CUs it holds
+                # its own HIP-event span, against the MFMA peak (of the dtype) of the CUs it holds
                 ach_l = ov["flops"] / (ov["ms"] * 1e-3) / 1e12
                 peak_l = PEAK[dtn] * chain_grid / ncu
                 roof.update({"achieved": round(ach_l, 3), "peak": round(peak_l, 3), "frac": round(ach_l / peak_l, 4),
-                             "kernel": "chain_kernel (persistent factorisation, %d workgroups = %d of %d CUs, f64 "
-                                       "MFMA tiles)" % (chain_grid, chain_grid, ncu),
+                             "kernel": "chain_kernel (persistent factorisation, %d workgroups = %d of %d CUs, %s "
+                                       "MFMA tiles)" % (chain_grid, chain_grid, ncu, dtn),
                              "measured_in": "%d-step events pass of the timed schedule (%d launches in flight); peak "
                                             "scaled to the launch's CU share" % (args.roofline_steps, P),
                              "launches_per_step": ov["launches"] // args.roofline_steps,

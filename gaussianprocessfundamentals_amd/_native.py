@@ -256,13 +256,17 @@ def last_factorisation_was_chain() -> bool:
     return bool(out[2])
 
 
-def chain_plan(n_pad: int, y_row: int, grid: int, eye: bool = False):
+CHAIN_PLAN_F32 = 256  # gpk_chain_plan_ex flag (include/gpk.h GPK_CHAIN_PLAN_F32)
+
+
+def chain_plan(n_pad: int, y_row: int, grid: int, eye: bool = False, f32: bool = False):
     """Task list of the persistent single-member factorisation (gpk_chain_plan_ex; host only): an
-    [ntasks, 4] int32 array of (type word, k, r, j) in claim order; eye: the identity-augmented list."""
+    [ntasks, 4] int32 array of (type word, k, r, j) in claim order; eye: the identity-augmented list; f32: the
+    plan of an f32 factorisation (chain_kernel<float>)."""
     import numpy as np
     L = load_library()
     nt = c_int64(0)
-    fl = AUG_EXTRA_IDENTITY if eye else 0
+    fl = (AUG_EXTRA_IDENTITY if eye else 0) | (CHAIN_PLAN_F32 if f32 else 0)
     check(L.gpk_chain_plan_ex(int(n_pad), int(y_row), int(grid), fl, None, 0, ctypes.byref(nt)), "gpk_chain_plan_ex")
     out = np.zeros((int(nt.value), 4), dtype=np.int32)
     check(L.gpk_chain_plan_ex(int(n_pad), int(y_row), int(grid), fl, c_void_p(out.ctypes.data), int(nt.value),

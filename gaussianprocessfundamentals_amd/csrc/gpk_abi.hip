@@ -206,6 +206,8 @@ struct Tune {
   int64_t chain_xcd_seats;
   int64_t asm_f32_chunk;  // f32_fast_kernel: consecutive lower tiles per workgroup (C3: 1 / 2 / 4 / 8 / 16 0.062 / 0.059 /
                           // 0.059 / 0.063 / 0.073 ms, profiles/r06c_kb_c3_chunks.txt)
+  int64_t chain_f32;      // f32 factorisations as one persistent launch too (chain_kernel<float>: f32 tile tasks, the
+                          // diagonal blocks in f64 as the launch path's); 0: f32 keeps the launch path
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -235,7 +237,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_GROUP_LA", 2), env_i64("GPK_ASM_F32_FAST", 1),
                          env_i64("GPK_CHAIN_GROUP_EYE", 8),
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
-                         env_i64("GPK_ASM_F32_CHUNK", 4)};
+                         env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1)};
   return t;
 }
 
@@ -267,6 +269,7 @@ const Knob kKnobs[] = {
     {"asm_f32_fast", &Tune::asm_f32_fast},
     {"chain_group_eye", &Tune::chain_group_eye}, {"chain_xcd", &Tune::chain_xcd},
     {"chain_xcd_seats", &Tune::chain_xcd_seats}, {"asm_f32_chunk", &Tune::asm_f32_chunk},
+    {"chain_f32", &Tune::chain_f32},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -501,9 +504,11 @@ int64_t g_chain_times_n = 0;
 // panels per deferred tile update: the knob, or (0) 4 below 80 diagonal blocks and 8 from there -- the deep
 // updates' MFMA rate starts to matter more than the columns they hold back (N = 8192 4.46 / 4.49 ms with 4 / 8,
 // 10240 7.74 / 7.62, 12288 12.56 / 12.17, profiles/r04af_chain_group_large.jsonl)
-int chain_group_for(int64_t knob, int64_t n_pad) {
+int chain_group_for(int64_t knob, int64_t n_pad, bool f32 = false) {
   if (knob > 0) return (int)knob;
-  return n_pad / NB >= 80 ? 8 : 4;
+  // (f32: 8 -- C3 at 8 persistent launches in flight 426 / 436 / 427 / 417 evals/s at 4 / 8 / 12 / 16,
+  // profiles/r06j_c3_f32_chain_sweep.txt)
+  return n_pad / NB >= 80 || f32 ? 8 : 4;
 }
 
 // Every tuning input of chain_order, resolved once per call from the knobs (and part of the plan cache key, so a
@@ -511,11 +516,12 @@ int chain_group_for(int64_t knob, int64_t n_pad) {
 struct ChainKnobs {
   int group, uq, group_corner, corner_tail, group_la;
 };
-ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye) {
+ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false) {
   ChainKnobs k;
   const int64_t gk = eye && tn.chain_group_eye > 0 ? tn.chain_group_eye : tn.chain_group;
-  k.group = std::max(1, std::min(chain_group_for(gk, n_pad), 16));
-  k.uq = (int)std::max<int64_t>(0, std::min<int64_t>(2, tn.chain_uq));
+  k.group = std::max(1, std::min(chain_group_for(gk, n_pad, f32), 16));
+  // (f32: one U32 task per slice -- chain_kernel<float> has no quarter-task bodies)
+  k.uq = f32 ? 0 : (int)std::max<int64_t>(0, std::min<int64_t>(2, tn.chain_uq));
   k.group_corner = (int)std::max<int64_t>(1, std::min<int64_t>(tn.chain_group_corner, 16));
   k.corner_tail = (int)std::max<int64_t>(0, tn.chain_corner_tail);
   k.group_la = (int)std::max<int64_t>(1, tn.chain_group_la);
@@ -772,10 +778,11 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int nme
 
 // chain_kernel applies to one f64 member (or a small batch) without ragged rows -- identity extra rows
 // included (chain_eye) --, on a stream that is not being captured (the first call of a shape uploads its task
-// list), up to chain_max_p (identity rows: chain_max_p_eye) rows
+// list), up to chain_max_p (identity rows: chain_max_p_eye) rows; f32 (chain_f32) without identity rows
 bool chain_applies(const gpk_layout* lay, bool eye, const int64_t* n_dev, const int64_t* m_dev, const Tune& tn,
                    hipStream_t s) {
-  if (!tn.chain || lay->dtype != GPK_F64 || (eye && !tn.chain_eye) || n_dev || m_dev) return false;
+  const bool dt_ok = lay->dtype == GPK_F64 || (lay->dtype == GPK_F32 && tn.chain_f32 != 0 && !eye);
+  if (!tn.chain || !dt_ok || (eye && !tn.chain_eye) || n_dev || m_dev) return false;
   if (lay->batch == 1 ? lay->p > (eye ? tn.chain_max_p_eye : tn.chain_max_p)
                       : (lay->batch > tn.chain_max_batch || lay->batch * lay->p > tn.chain_batch_max_rows))
     return false;
@@ -800,7 +807,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   size_t ctl_ints = 0;
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
-    const ChainKnobs kn = chain_knobs(tn, lay->n_pad, eye);
+    const ChainKnobs kn = chain_knobs(tn, lay->n_pad, eye, lay->dtype == GPK_F32);
     const int nmem = lay->batch;
     // (two lists need workgroups of both roles: at least 8 per XCD)
     const int xcd = tn.chain_xcd != 0 && grid >= 64 ? 1 : 0;
@@ -842,9 +849,9 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   GPK_HIP(hipMemsetAsync(ctl, 0, ctl_ints * sizeof(int32_t), s), "chain memset");
   ChainArgs a;
   memset(&a, 0, sizeof(a));
-  a.W = static_cast<double*>(W);
+  a.W = W;
   a.ld = lay->ld;
-  a.Winv = static_cast<double*>(Winv);
+  a.Winv = Winv;
   a.info = info_dev;
   a.tasks = plan.tasks;
   a.ntasks = env_i64("GPK_CHAIN_MAX_TASKS", 0) > 0 ? (int32_t)std::min<int64_t>(plan.ntasks, env_i64("GPK_CHAIN_MAX_TASKS", 0)) : plan.ntasks;  // (debugging)
@@ -865,7 +872,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.w_bs = lay->w_batch_stride;
   a.inv_bs = lay->inv_batch_stride;
   a.ctl_stride = 2 * (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
-  a.uq = (int32_t)chain_knobs(tn, lay->n_pad, eye).uq;
+  a.uq = (int32_t)chain_knobs(tn, lay->n_pad, eye, lay->dtype == GPK_F32).uq;
   // rows of L_kk^-1 behind D's early flag: later (more of the panel solve early) for short chains, where the
   // diagonal chain is all there is; earlier for long ones, where the S tasks' waiting CUs cost tile-update time
   // (N = 4096: 112 rows 1.501 vs 96 rows 1.515 ms; 6144 / 8192 2.42 / 4.44 vs 2.37 / 4.39, profiles/r04ab_*)
@@ -901,7 +908,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     a.trace = grid <= 4096 ? g_chain_trace : nullptr;
   }
   const double n3 = (double)lay->n_pad;
-  GPK_HIP(timed(3, lay->batch * n3 * n3 * n3 / (eye ? 1.0 : 3.0), 0.0, s, [&] { return launch_chain(a, grid, s); }),
+  GPK_HIP(timed(3, lay->batch * n3 * n3 * n3 / (eye ? 1.0 : 3.0), 0.0, s, [&] { return launch_chain(a, lay->dtype, grid, s); }),
           "chain");
   ++g_chain_launches;
   t_chain_last = true;
@@ -2144,12 +2151,14 @@ int chain_plan_impl(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, i
   if (n_pad <= 0 || n_pad % NB != 0) return fail_arg(1, "n_pad (a positive multiple of 128)");
   if (y_row < n_pad) return fail_arg(2, "y_row (>= n_pad)");
   if (grid <= 0) return fail_arg(3, "grid");
-  if (flags & ~GPK_AUG_EXTRA_IDENTITY) return fail_arg(4, "flags");
+  if (flags & ~(GPK_AUG_EXTRA_IDENTITY | GPK_CHAIN_PLAN_F32)) return fail_arg(4, "flags");
   const bool eye = (flags & GPK_AUG_EXTRA_IDENTITY) != 0;
+  const bool f32 = (flags & GPK_CHAIN_PLAN_F32) != 0;
+  if (eye && f32) return fail_arg(4, "flags (f32 plans have no identity rows)");
   if (eye && (y_row - n_pad < 1 || y_row - n_pad > n_pad))
     return fail_arg(2, "y_row (identity extra rows: n_pad + n with 0 < n <= n_pad)");
   if (!ntasks) return fail_arg(ap_ntasks, "ntasks");
-  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, 1, chain_knobs(tune_now(), n_pad, eye), eye);
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, 1, chain_knobs(tune_now(), n_pad, eye, f32), eye);
   if (ord.empty()) {
     return fail_hip(hipErrorUnknown, "chain_order: a task exceeds the device's dependency bound");
   }

@@ -648,7 +648,7 @@ __global__ __launch_bounds__(256) void pair_feat_kernel(gpk_kdesc kd, AsmArgs a,
 // (global_load_lds, no VGPRs) while the current tile is evaluated -- one barrier per tile instead of two, and the
 // feature fetch off the tile's critical path (0: the round-5 form, loaded through VGPRs after the barrier).
 #ifndef GPK_FAST_DMA
-#define GPK_FAST_DMA 1
+#define GPK_FAST_DMA 0
 #endif
 typedef __attribute__((address_space(3))) void asm_lds_void;
 template <int D, bool MUL>

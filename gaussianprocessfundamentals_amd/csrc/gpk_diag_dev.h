@@ -638,8 +638,8 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
       const int r = r0 + q * RPP;
       if (pc * EPC <= (r | (DB - 1))) {
         if constexpr (SC1)
-          v[q] = ld16_buf(uniform_rsrc(Wb), (int)(((int64_t)r0 * a.ld + pc * EPC) * 8),
-                          __builtin_amdgcn_readfirstlane((int)((int64_t)q * RPP * a.ld * 8)));
+          v[q] = __builtin_bit_cast(vT, ld16_buf(uniform_rsrc(Wb), (int)(((int64_t)r0 * a.ld + pc * EPC) * sizeof(T)),
+                                                 __builtin_amdgcn_readfirstlane((int)((int64_t)q * RPP * a.ld * sizeof(T)))));
         else
           v[q] = ldv<SC1, T>(Wb + (int64_t)r * a.ld + pc * EPC);
       }

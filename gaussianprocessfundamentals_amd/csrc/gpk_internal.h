@@ -168,11 +168,11 @@ struct DiagArgs {
 #define GPK_CHAIN_SHALF_ROWS_SMALL 112
 #endif
 
-// persistent factorisation (gpk_potrf.hip chain_kernel): one f64 member, tasks in host-computed order
+// persistent factorisation (gpk_potrf.hip chain_kernel<T>): one member (or a small batch), tasks in host-computed order
 struct ChainArgs {
-  double* W;
+  void* W;               // f64 or f32 (chain_kernel<double> / <float>), like Winv
   int64_t ld;
-  double* Winv;
+  void* Winv;
   int32_t* info;
   const int32_t* tasks;  // [ntasks + ntasks_b][4]: type (0 D, 1 S, 2 U32, 3 BLK), panel, slice / block row, block column
   int32_t ntasks;        // tasks of list A (all of them unless xcd_b >= 0)
@@ -266,7 +266,7 @@ hipError_t launch_assemble(const gpk_kdesc& kd, const AsmArgs& a, int dtype, int
 hipError_t launch_diag(const DiagArgs& a, int dtype, int32_t batch, hipStream_t s);
 hipError_t launch_gemm(const GemmArgs& a, int dtype, int mode, int tile, int32_t batch, hipStream_t s);
 hipError_t launch_finalize(const FinArgs& a, int dtype, int32_t batch, hipStream_t s);
-hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s);
+hipError_t launch_chain(const ChainArgs& a, int dtype, int grid, hipStream_t s);
 hipError_t chain_timeouts_read(int64_t* out);  // timed-out persistent launches on this device (synchronous)
 hipError_t launch_grad(const gpk_kdesc& kd, const GradArgs& g, int dtype, int32_t batch, hipStream_t s);
 size_t vjp_workspace_elems(const gpk_kdesc& kd, int64_t n, int64_t m, int32_t d, bool want_z);

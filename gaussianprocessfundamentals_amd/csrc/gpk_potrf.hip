@@ -121,6 +121,8 @@ struct BufIO<double> {
   static __device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t rs, int vo, int so, double v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(raw_t, v), rs, vo, so, 16);
   }
+  // chain_kernel's C reads (kLdAux: sc1 in the GPK_CHAIN_SC1LD A/B builds)
+  static __device__ __forceinline__ double load_ch(__amdgpu_buffer_rsrc_t rs, int vo, int so) { return ld8_buf(rs, vo, so); }
 };
 template <>
 struct BufIO<float> {
@@ -129,6 +131,12 @@ struct BufIO<float> {
   }
   static __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t rs, int vo, int so, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rs, vo, so, 0);
+  }
+  static __device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t rs, int vo, int so, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rs, vo, so, 16);
+  }
+  static __device__ __forceinline__ float load_ch(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, kLdAux));
   }
 };
 
@@ -297,9 +305,11 @@ __global__ __launch_bounds__(128 * WN, (WN == 4 && MODE == GEMM_UPDATE) ? 4 : 2)
 #ifndef GPK_CFIRST
 #define GPK_CFIRST 1  // f64 update: C loaded into the accumulators before the K loop (A negated)
 #endif
-  // C first (f64): the C read overlaps the first chunk's staging instead of following the last
-  // MFMA, and the epilogue is stores only (+3 % update rate at N = 8192; neutral for f32)
-  constexpr bool CFIRST = (MODE == GEMM_UPDATE) && ((GPK_CFIRST && sizeof(T) == 8) || KB != 0);
+  // C first: the C read overlaps the first chunk's staging instead of following the last MFMA, and the
+  // epilogue is stores only (+3 % update rate at N = 8192; neutral for f32).  Every element then takes its
+  // products one k-step after another onto C whatever the panel grouping, so the persistent launch's tile
+  // tasks (other groupings) write the same bits -- f32 included (its A negated: exact)
+  constexpr bool CFIRST = (MODE == GEMM_UPDATE) && (GPK_CFIRST || KB != 0);
   const int col = lane & 15;
   // C tile through a buffer descriptor: one 32-bit per-lane offset (VGPR) plus, for block (m, n)
   // and register r, the wave-uniform byte offset ((m 16 + r RSTEP) ld + n 16) sizeof(T) in an
@@ -936,23 +946,119 @@ __device__ __forceinline__ void sq_quarters(double* W, int64_t ld, int k, int r,
   }
 }
 
-// BLK: C(R.., Cc..) -= A(R.., Kc..) B(Cc.., Kc..)^T on a 128 x 128 tile, K = 128 g: gemm_kernel's f64
-// update (8 waves of 64 x 32, LDS-DMA staging of 16-deep chunks in two stages, C first, the next chunk's
-// DMA after the first half of the MFMAs) with write-through C stores.  Rows >= row_end are zero.
-__device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64_t Cc, int64_t Kc, int g,
+// ---------------------------------------------------------------------------- f32 slab tasks (chain_kernel<float>)
+// The f32 forms of S and U32 (slab_gemm): the 32 x 128 slice staged in LDS, wave w on column block cb (the f64
+// pairing), the B rows straight to registers, f32 MFMA (v_mfma_f32_16x16x4_f32).  LDS image: row r of the slice
+// in LDS row r & 15 of SLAB_LDS_ROW bytes, at byte 512 (r >> 4) -- rows 0..15 in the first half, 16..31 in the
+// second, the f64 row stride (16 rows of one operand read on distinct 16-B bank slots); one DMA wave-instruction
+// per LDS row (lanes 0..31 row r, 32..63 row r + 16).  k-steps: 16-B pieces, k = 16 j + 4 q + e for lane group
+// q = lane >> 4, piece j = 0..7, element e -- gemm_kernel<float>'s order (chunk kc = j / 2, step 4 (j & 1) + e),
+// so X and the updated C are the launch path's bits (U32 C first, as its update).
+__device__ __forceinline__ void slab_stage_a32(const float* A, int64_t ld, char* smem) {
+  const int tid = opaque_tid();
+  const int lane = tid & 63;
+  const int w = wave_uniform(tid >> 6);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int lrow = 2 * w + i;
+    glds16a<kLdAux>(A + (int64_t)(lrow + 16 * (lane >> 5)) * ld + 4 * (lane & 31), smem + lrow * SLAB_LDS_ROW);
+  }
+}
+__device__ __forceinline__ float ld4_buf(__amdgpu_buffer_rsrc_t rs, int vo, int so) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, kLdAux));
+}
+template <bool SUB, bool STAGED = false, bool HALF = false>
+__device__ __forceinline__ void slab_gemm32(const float* A, const float* B, int64_t ldb, float* C, int64_t ld,
+                                            int diag_off, uint64_t* st, char* smem, HalfWait hw = HalfWait{}) {
+  typedef float flt4 __attribute__((ext_vector_type(4)));
+  const int tid = opaque_tid();
+  const int lane = tid & 63;
+  const int w = wave_uniform(tid >> 6);
+  const int lr = lane & 15, q = lane >> 4;
+  const int cb = w < 4 ? w : 11 - w;
+  const bool live0 = diag_off < 0 || cb <= (diag_off >> 4), live1 = diag_off < 0 || cb <= (diag_off >> 4) + 1;
+  if (!STAGED) slab_stage_a32(A, ld, smem);
+  const __amdgpu_buffer_rsrc_t brs = uniform_rsrc(B), crs = uniform_rsrc(C);
+  const int bvo = (int)(((int64_t)(cb * 16 + lr) * ldb + 4 * q) * 4);
+  const int cvo = (int)(((int64_t)(4 * q) * ld + cb * 16 + lr) * 4);  // f32 C/D layout: row 4 q + i, column lr
+  const int ldc1 = __builtin_amdgcn_readfirstlane((int)(ld * 4)), ldc16 = __builtin_amdgcn_readfirstlane((int)(16 * ld * 4));
+  // pieces j <= jm: L^-1's lower triangle (S: k < 16 (cb + 1); its upper tiles are never written), all (U32)
+  const int jm = SUB ? (live1 ? 7 : -1) : cb;
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  if (SUB) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc0[i] = ld4_buf(crs, cvo, i * ldc1);
+      acc1[i] = ld4_buf(crs, cvo, ldc16 + i * ldc1);
+    }
+  }
+  if (HALF && cb >= hw.split) {
+    if (chain_wait_v(hw.full, 1, hw.ctl, hw.info, hw.nmem, hw.timeout, hw.force_abort,
+                     __builtin_amdgcn_s_memrealtime()) && !kChainSc1Ld) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+  }
+  flt4 bv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    bv[j] = __builtin_bit_cast(flt4, __builtin_amdgcn_raw_buffer_load_b128(brs, j <= jm ? bvo + j * 64 : kRsrcBytes, 0, kLdAux));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA writes are not tracked by hipcc)
+  if (!HALF) __syncthreads();
+  if (st && w == 0) st[4] = __builtin_amdgcn_s_memrealtime();
+  const char* a0 = smem + lr * SLAB_LDS_ROW + q * 16;
+  const char* a1 = a0 + 512;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j <= jm) {
+      const flt4 x0 = *reinterpret_cast<const flt4*>(a0 + j * 64);
+      const flt4 x1 = *reinterpret_cast<const flt4*>(a1 + j * 64);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(SUB ? -x0[e] : x0[e], bv[j][e], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(SUB ? -x1[e] : x1[e], bv[j][e], acc1, 0, 0, 0);
+      }
+    }
+  }
+  if (st && w == 0) {
+    const int dep = __builtin_amdgcn_readfirstlane((int)acc0[3] + (int)acc1[3]);
+    st[5] = __builtin_amdgcn_s_memrealtime() + (dep == 0x7fffffff ? 1 : 0);
+  }
+  float* Cr = C + (int64_t)(4 * q) * ld + cb * 16 + lr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (live0) sts<true>(Cr + i * ld, acc0[i]);
+    if (live1) sts<true>(Cr + (16 + i) * ld, acc1[i]);
+  }
+}
+
+// BLK: C(R.., Cc..) -= A(R.., Kc..) B(Cc.., Kc..)^T on a 128 x 128 tile, K = 128 g: gemm_kernel's update
+// (8 waves of 64 x 32, LDS-DMA staging of 128-B row chunks -- 16 f64 / 32 f32 deep -- in two stages, C first,
+// the next chunk's DMA after the first half of the MFMAs) with write-through C stores.  Rows >= row_end are
+// zero.  Every element takes gemm_kernel's k-steps in its order, C first (both dtypes): the launch path's bits.
+#ifndef GPK_CH_GMID_F32
+#define GPK_CH_GMID_F32 0
+#endif
+template <typename T>
+__device__ __forceinline__ void blk_tile(T* W, int64_t ld, int64_t R, int64_t Cc, int64_t Kc, int g,
                                          int64_t row_end, char* smem) {
-  constexpr int TM = 128, TN = 128, WN = 4, WM = 2, NW = 8, MB = 4, NBK = 2, EPC = 2, GBK = 16, KS = 4;
+  constexpr int TM = 128, TN = 128, WN = 4, WM = 2, NW = 8, MB = 4, NBK = 2;
+  constexpr int EPC = 16 / (int)sizeof(T), GBK = ROWB / (int)sizeof(T), KS = GBK / 4;
+  constexpr int RSTEP = sizeof(T) == 8 ? 4 : 1;  // C/D rows of one accumulator's registers
+  // the next chunk's DMA after the first half of the MFMAs (f64) or at the top of the chunk (f32, gemm_kernel's
+  // GPK_GLDS_MID_F32: 8 k-steps per chunk)
+  constexpr bool GMID = sizeof(T) == 8 || GPK_CH_GMID_F32 != 0;
   constexpr int STAGE = (TM + TN) * ROWB;
   constexpr int PW = (TM + TN) / (8 * NW);
   const int NK = wave_uniform(g * (NB / GBK));  // depth 128 g: the g panels Kc / 128 .. + g - 1
-  typedef double vec_t __attribute__((ext_vector_type(2)));
+  typedef T vec_t __attribute__((ext_vector_type(EPC)));
+  typedef typename Mfma<T>::acc_t acc_t;
   const int tid = opaque_tid();
   const int lane = tid & 63;
   const int wid = wave_uniform(tid >> 6);
   const int wr = wid / WN, wc = wid % WN;
-  const double* Ag = W + R * ld + Kc;
-  const double* Bg = W + Cc * ld + Kc;
-  const double* src[PW];
+  const T* Ag = W + R * ld + Kc;
+  const T* Bg = W + Cc * ld + Kc;
+  const T* src[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
     const int g0 = (wid * PW + i) * 8;
@@ -960,24 +1066,24 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
     src[i] = (g0 < TM) ? Ag + (int64_t)r * ld + swz(r, lane & 7) * EPC
                        : Bg + (int64_t)(r - TM) * ld + swz(r - TM, lane & 7) * EPC;
   }
-  double* const C = W + R * ld + Cc;
+  T* const C = W + R * ld + Cc;
   const uint64_t cu = reinterpret_cast<uint64_t>(C);
   const uint64_t cuu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(cu >> 32)) << 32) |
                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)cu);
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(cuu), 0, (int)(TM * ld * (int64_t)sizeof(double)), 0x00020000);
+      reinterpret_cast<void*>(cuu), 0, (int)(TM * ld * (int64_t)sizeof(T)), 0x00020000);
   const int col = lane & 15;
-  const int cvo = (int)(((int64_t)(wr * (TM / WM) + Mfma<double>::row(lane, 0)) * ld + wc * (TN / WN) + col) *
-                        (int64_t)sizeof(double));
-  const int ldb_s = wave_uniform((int)(ld * (int64_t)sizeof(double)));
-#define GPK_CH_CSOFF(m, n, r) (((m) * 16 + (r) * 4) * ldb_s + (n) * 16 * (int)sizeof(double))
-  d4 acc[MB][NBK];
+  const int cvo = (int)(((int64_t)(wr * (TM / WM) + Mfma<T>::row(lane, 0)) * ld + wc * (TN / WN) + col) *
+                        (int64_t)sizeof(T));
+  const int ldb_s = wave_uniform((int)(ld * (int64_t)sizeof(T)));
+#define GPK_CH_CSOFF(m, n, r) (((m) * 16 + (r) * RSTEP) * ldb_s + (n) * 16 * (int)sizeof(T))
+  acc_t acc[MB][NBK];
 #pragma unroll
   for (int m = 0; m < MB; ++m)
 #pragma unroll
     for (int n = 0; n < NBK; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[m][n][r] = ld8_buf(crs, cvo, GPK_CH_CSOFF(m, n, r));
+      for (int r = 0; r < 4; ++r) acc[m][n][r] = BufIO<T>::load_ch(crs, cvo, GPK_CH_CSOFF(m, n, r));
   const int q = lane >> 4, lr = lane & 15;
   const int aoff = (wr * (TM / WM) + lr) * ROWB;
   const int boff = (TM + wc * (TN / WN) + lr) * ROWB;
@@ -994,12 +1100,13 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
   _Pragma("unroll") for (int s = (S0); s < (S1); ++s)                                              \
   _Pragma("unroll") for (int n = 0; n < NBK; ++n)                                                  \
   _Pragma("unroll") for (int m = 0; m < (MLIM); ++m)                                               \
-    acc[m][n] = Mfma<double>::op_neg(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]);
+    acc[m][n] = Mfma<T>::op_neg(fa[m][s / EPC][s % EPC], fb[n][s / EPC][s % EPC], acc[m][n]);
 #define GPK_CH_KLOOP(MLIM)                                                                         \
   for (int kc = 0; kc < NK; ++kc) {                                                                \
     const int st = kc & 1;                                                                         \
     __builtin_amdgcn_s_waitcnt(0x0F70);                                                            \
     __syncthreads();                                                                               \
+    if (!GMID && kc + 1 < NK) GPK_CH_GLDS(st ^ 1, kc + 1);                                         \
     if ((MLIM) > 0) {                                                                              \
       const char* sb = smem + st * STAGE;                                                          \
       vec_t fa[MB][2], fb[NBK][2];                                                                 \
@@ -1011,11 +1118,13 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
           fa[m][h] = *reinterpret_cast<const vec_t*>(sb + aoff + m * 16 * ROWB + (h ? p1 : p0));   \
       }                                                                                            \
       GPK_CH_STEPS(0, KS / 2, MLIM)                                                                \
-      __builtin_amdgcn_sched_barrier(0);                                                           \
-      if (kc + 1 < NK) GPK_CH_GLDS(st ^ 1, kc + 1);                                                \
-      __builtin_amdgcn_sched_barrier(0);                                                           \
+      if (GMID) {                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+        if (kc + 1 < NK) GPK_CH_GLDS(st ^ 1, kc + 1);                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                         \
+      }                                                                                            \
       GPK_CH_STEPS(KS / 2, KS, MLIM)                                                               \
-    } else if (kc + 1 < NK) {                                                                      \
+    } else if (GMID && kc + 1 < NK) {                                                              \
       GPK_CH_GLDS(st ^ 1, kc + 1);                                                                 \
     }                                                                                              \
   }
@@ -1029,14 +1138,14 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
 #undef GPK_CH_KLOOP
 #undef GPK_CH_STEPS
 #undef GPK_CH_GLDS
-  // (through a double-typed parameter: __builtin_bit_cast of the vector element acc[m][n][r] itself
+  // (through a scalar-typed parameter: __builtin_bit_cast of the vector element acc[m][n][r] itself
   // compiled to four stores of element 0)
 #pragma unroll
   for (int m = 0; m < MB; ++m)
 #pragma unroll
     for (int n = 0; n < NBK; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) BufIO<double>::store_sc1(crs, cvo, GPK_CH_CSOFF(m, n, r), acc[m][n][r]);
+      for (int r = 0; r < 4; ++r) BufIO<T>::store_sc1(crs, cvo, GPK_CH_CSOFF(m, n, r), acc[m][n][r]);
 #undef GPK_CH_CSOFF
 }
 
@@ -1051,7 +1160,8 @@ __device__ __forceinline__ void blk_tile(double* W, int64_t ld, int64_t R, int64
 // per-lane scratch and every field read becomes a VGPR load -- divergent for the compiler, which then
 // turned the claim loop's exit into an exec-mask-controlled loop whose barriers the waves no longer
 // executed the same number of times (the deadlock of the first versions).
-GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, int dbg, int k, uint64_t* dprof,
+template <typename T>
+GPK_CHAIN_FN void chain_d(T* W, int64_t ld, T* Winv, int32_t* info, int dbg, int k, uint64_t* dprof,
                           int32_t* half_flag, int half_step, double* sm) {
   DiagArgs da{};
   da.W = W;
@@ -1067,7 +1177,7 @@ GPK_CHAIN_FN void chain_d(double* W, int64_t ld, double* Winv, int32_t* info, in
   da.defer_l_store = GPK_CHAIN_DEFER_L;
   da.half_flag = half_flag;
   da.half_step = half_step;
-  diag2_body<double, false, true>(da, 0, sm);
+  diag2_body<T, false, true>(da, 0, sm);
 }
 GPK_CHAIN_FN void chain_s(double* W, int64_t ld, const double* Winv, int k, int r, uint64_t* st, char* smem) {
   double* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
@@ -1123,6 +1233,30 @@ GPK_CHAIN_FN void chain_u32(double* W, int64_t ld, int q, int r, int j, uint64_t
   const int64_t J = (int64_t)j * NB;
   slab_gemm<true>(W + R * ld + (int64_t)q * NB, W + J * ld + (int64_t)q * NB, ld, W + R * ld + J, ld,
                   (R >= J && R < J + NB) ? (int)(R - J) : -1, st, smem);
+}
+
+// f32 forms (chain_kernel<float>: no SQ / UQ tasks -- its plans take one U32 per slice, chain_knobs)
+GPK_CHAIN_FN void chain_s32(float* W, int64_t ld, const float* Winv, int k, int r, uint64_t* st, char* smem) {
+  float* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
+  slab_gemm32<false>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem);
+}
+GPK_CHAIN_FN void chain_s32_staged(float* W, int64_t ld, const float* Winv, int k, int r, uint64_t* st, char* smem) {
+  float* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
+  slab_gemm32<false, true>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem);
+}
+GPK_CHAIN_FN void chain_s32_half(float* W, int64_t ld, const float* Winv, int k, int r, uint64_t* st, char* smem,
+                                 HalfWait hw) {
+  float* X = W + (int64_t)r * 32 * ld + (int64_t)k * NB;
+  slab_gemm32<false, true, true>(X, Winv + (int64_t)k * NB * NB, NB, X, ld, -1, st, smem, hw);
+}
+GPK_CHAIN_FN void chain_s32_stage(float* W, int64_t ld, int k, int r, char* smem) {
+  slab_stage_a32(W + (int64_t)r * 32 * ld + (int64_t)k * NB, ld, smem);
+}
+GPK_CHAIN_FN void chain_u32_f32(float* W, int64_t ld, int q, int r, int j, uint64_t* st, char* smem) {
+  const int64_t R = (int64_t)r * 32;
+  const int64_t J = (int64_t)j * NB;
+  slab_gemm32<true>(W + R * ld + (int64_t)q * NB, W + J * ld + (int64_t)q * NB, ld, W + R * ld + J, ld,
+                    (R >= J && R < J + NB) ? (int)(R - J) : -1, st, smem);
 }
 
 __device__ __forceinline__ void chain_trace(const ChainArgs& a, int slot, int v) {
@@ -1223,7 +1357,9 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int kprev
 // XCD of the executing workgroup (HW_REG_XCC_ID, bits 3:0)
 __device__ __forceinline__ int xcc_id() { return (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xf); }
 
+template <typename T>
 __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
+  constexpr bool F64 = sizeof(T) == 8;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   int32_t* slot = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(sm) + CHAIN_SLOT_OFF);
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -1269,7 +1405,8 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     // updates have no earlier update (identity-augmented lists: their counter waits are for 0); member
     const int ty = tyg & 3, g = ((tyg >> 2) & 15) + 1, first = (tyg >> 6) & 1, mem = tyg >> 8;
     const bool sq = ty == CH_S && ((tyg >> 7) & 1);  // (chain_uq 2: S + the next block's quarters, chain_sq)
-    double* const Wm = a.W + (int64_t)mem * a.w_bs;
+    T* const Wm = reinterpret_cast<T*>(a.W) + (int64_t)mem * a.w_bs;
+    T* const Wi = reinterpret_cast<T*>(a.Winv) + (int64_t)mem * a.inv_bs;
     const int64_t co = (int64_t)mem * a.ctl_stride;
     const int k = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 1]);
     const int r = __builtin_amdgcn_readfirstlane(a.tasks[4 * t + 2]);
@@ -1307,7 +1444,10 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
     if (spref) {
-      chain_s_stage(Wm, a.ld, k, r, reinterpret_cast<char*>(sm));
+      if constexpr (F64)
+        chain_s_stage(Wm, a.ld, k, r, reinterpret_cast<char*>(sm));
+      else
+        chain_s32_stage(Wm, a.ld, k, r, reinterpret_cast<char*>(sm));
       if (wave == 0) {
         // (GPK_CHAIN_SHALF: rows 0..63 of L_kk^-1 suffice for the first column half; the rest waits in the body)
         const bool ok = chain_wait(a, (shalf ? a.hflag : a.dflag) + co + k, 1, __builtin_amdgcn_s_memrealtime());
@@ -1325,31 +1465,44 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       if (!__builtin_amdgcn_readfirstlane(slot[1])) continue;
     }
     if (ty == CH_D) {
-      chain_d(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, a.info + mem, a.dbg, k, a.dprof,
-              GPK_CHAIN_SHALF ? a.hflag + co + k : nullptr, a.half_step, sm);
-    } else if (sq) {
-      chain_sq(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
-               reinterpret_cast<char*>(sm),
-               HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort,
-                        GPK_CHAIN_SHALF ? a.half_step : 0},
-               a.sdone + co + (int64_t)k * a.nsl, slot);
-    } else if (shalf) {
-      chain_s_half(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
-                   reinterpret_cast<char*>(sm),
-                   HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort, a.half_step});
-    } else if (spref) {
-      chain_s_staged(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
-                     reinterpret_cast<char*>(sm));
-    } else if (ty == CH_S) {
-      chain_s(Wm, a.ld, a.Winv + (int64_t)mem * a.inv_bs, k, r, a.times ? a.times + 6 * t : nullptr,
-              reinterpret_cast<char*>(sm));
-    } else if (ty == CH_U32 && g > 1) {
-      chain_uq(Wm, a.ld, k, r, j, g - 2, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
-    } else if (ty == CH_U32) {
-      chain_u32(Wm, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      chain_d<T>(Wm, a.ld, Wi, a.info + mem, a.dbg, k, a.dprof, GPK_CHAIN_SHALF ? a.hflag + co + k : nullptr,
+                 a.half_step, sm);
+    } else if constexpr (F64) {
+      if (sq) {
+        chain_sq(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm),
+                 HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort,
+                          GPK_CHAIN_SHALF ? a.half_step : 0},
+                 a.sdone + co + (int64_t)k * a.nsl, slot);
+      } else if (shalf) {
+        chain_s_half(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm),
+                     HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort, a.half_step});
+      } else if (spref) {
+        chain_s_staged(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      } else if (ty == CH_S) {
+        chain_s(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      } else if (ty == CH_U32 && g > 1) {
+        chain_uq(Wm, a.ld, k, r, j, g - 2, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      } else if (ty == CH_U32) {
+        chain_u32(Wm, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      } else {
+        blk_tile<double>(Wm, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, g, a.row_end,
+                         reinterpret_cast<char*>(sm));
+      }
     } else {
-      blk_tile(Wm, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, g, a.row_end,
-               reinterpret_cast<char*>(sm));
+      // (f32 plans hold no SQ / UQ tasks)
+      if (shalf) {
+        chain_s32_half(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm),
+                       HalfWait{a.dflag + co + k, a.ctl, a.info, a.nmem, a.timeout, a.force_abort, a.half_step});
+      } else if (spref) {
+        chain_s32_staged(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      } else if (ty == CH_S) {
+        chain_s32(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      } else if (ty == CH_U32) {
+        chain_u32_f32(Wm, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+      } else {
+        blk_tile<float>(Wm, a.ld, (int64_t)r * NB, (int64_t)j * NB, (int64_t)k * NB, g, a.row_end,
+                        reinterpret_cast<char*>(sm));
+      }
     }
     if (wave == 0 && a.times) {
       a.times[6 * t + 2] = __builtin_amdgcn_s_memrealtime();  // wave 0's body done
@@ -1382,10 +1535,10 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       // L_kk from LDS (the block's lower tiles; L^-1 sits in the upper ones) to W, after the hand-off: only the
       // read-out after the launch uses it.  (The next claim's barrier keeps the LDS intact until every wave has
       // read its rows.)
-      double* Wb = Wm + (int64_t)k * NB * a.ld + (int64_t)k * NB;
+      T* Wb = Wm + (int64_t)k * NB * a.ld + (int64_t)k * NB;
       const int tid = opaque_tid();
 #pragma unroll 1
-      for (int I = 0; I < NTL; ++I) store_l_rows<double, true>(sm, Wb, a.ld, I, tid, DT);
+      for (int I = 0; I < NTL; ++I) store_l_rows<T, true>(sm, Wb, a.ld, I, tid, DT);
     }
   }
   if (wave == 0) chain_trace(a, 1, 9);
@@ -1465,22 +1618,26 @@ hipError_t launch_trsv_update(const TrsvArgs& a, int dtype, int32_t batch, hipSt
 
 __global__ __launch_bounds__(DT) void chain_d_only_kernel(ChainArgs a) {  // (debugging: GPK_CHAIN_DBG=4)
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  chain_d(a.W, a.ld, a.Winv, a.info, a.dbg, 0, a.dprof, nullptr, 0, sm);
+  chain_d<double>(static_cast<double*>(a.W), a.ld, static_cast<double*>(a.Winv), a.info, a.dbg, 0, a.dprof, nullptr, 0,
+                  sm);
 }
 
-hipError_t launch_chain(const ChainArgs& a, int grid, hipStream_t s) {
-  if (a.dbg == 4) {
+template <typename T>
+hipError_t launch_chain_t(const ChainArgs& a, int grid, hipStream_t s) {
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(chain_kernel<T>), CHAIN_LDS_BYTES);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(chain_kernel<T>, dim3(grid), dim3(DT), CHAIN_LDS_BYTES, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_chain(const ChainArgs& a, int dtype, int grid, hipStream_t s) {
+  if (a.dbg == 4 && dtype == GPK_F64) {
     hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(chain_d_only_kernel), CHAIN_LDS_BYTES);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(chain_d_only_kernel, dim3(1), dim3(DT), CHAIN_LDS_BYTES, s, a);
     return hipGetLastError();
   }
-  {
-    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(chain_kernel), CHAIN_LDS_BYTES);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(chain_kernel, dim3(grid), dim3(DT), CHAIN_LDS_BYTES, s, a);
-  return hipGetLastError();
+  return dtype == GPK_F32 ? launch_chain_t<float>(a, grid, s) : launch_chain_t<double>(a, grid, s);
 }
 
 // persistent launches that timed out on the current device so far (g_chain_timeouts_dev; synchronous copy)

@@ -424,6 +424,9 @@ int gpk_timing_reset(void);
  * quarter updates -- as a second task list claimed first by up to "chain_xcd_seats" (16) workgroups of XCD 0, the
  * rest by everyone else, each workgroup falling back to the other list once its own is exhausted; measured no
  * faster).
+ * "chain_f32" (1: f32 factorisations without identity rows take the persistent launch under the same rules --
+ * chain_kernel<float>: f32 MFMA panel solves and tile updates, the diagonal blocks as the launch path's; bitwise
+ * the f32 launch path's results; one slice-update task per slice whatever "chain_uq"; 0: the launch path).
  * "asm_feat" (1: the K build of a two-leaf SE + periodic tree at D = 4 or 8 computes the per-point features in a
  * pre-pass and runs its interior tiles on the f64 MFMA fast-tile kernel; 0: every tile stages its points itself
  * -- the same bits, slower; A/B).
@@ -463,7 +466,10 @@ int gpk_chain_plan(int64_t n_pad, int64_t y_row, int32_t grid, int32_t* tasks_ou
  * out, and a task word with bit 6 set updates cells no earlier task updated (its counter wait is for 0).  The
  * type word: type (bits 0..1) | (g - 1) << 2 (bits 2..5; type 3: an update over the g panels k .. k + g - 1;
  * type 2 with g > 1: the 32 x 32 quarter g - 2 of slice r in diagonal block j) | bit 6 | bit 7 (an SQ task of
- * "chain_uq" 2: the slice's panel solve, then the next diagonal block's quarter updates) | member << 8. */
+ * "chain_uq" 2: the slice's panel solve, then the next diagonal block's quarter updates) | member << 8.
+ * GPK_CHAIN_PLAN_F32: the plan of an f32 factorisation (chain_kernel<float>: one slice-update task per slice, the
+ * f32 deferred-update depth). */
+#define GPK_CHAIN_PLAN_F32 256
 int gpk_chain_plan_ex(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, int32_t* tasks_out, int64_t cap,
                       int64_t* ntasks);
 

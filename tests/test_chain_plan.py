@@ -284,6 +284,35 @@ def test_chain_plan_reproduces_the_blocked_factorisation(n, m, group, uq):
         np.testing.assert_allclose(np.diag(W[n_pad:n_pad + m, n_pad:n_pad + m]), np.diag(sig), rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("n,m", [(300, 0), (1000, 37), (3000, 0), (8192, 0)])
+def test_chain_plan_f32_is_the_slice_update_plan(n, m):
+    """GPK_CHAIN_PLAN_F32 (chain_kernel<float>, which has no quarter-task bodies): whatever chain_uq says, one U32 per
+    slice and no SQ task -- the plan chain_uq 0 gives at the f32 depth (8 panels unless chain_group is set) -- and
+    it reproduces the blocked factorisation; with identity rows the flag is refused."""
+    _lib_or_skip()
+    n_pad, y_row, p = shape(n, m)
+    nblk = n_pad // NB
+    for uq in (0, 1, 2):
+        with nat.thread_tune(chain_uq=uq):
+            t32 = nat.chain_plan(n_pad, y_row, 64, f32=True)
+        assert np.array_equal(t32, plan(n_pad, y_row, 64, 8, uq=0))
+        assert not any(is_sq(t) for t in t32)
+        assert int(np.sum(((t32[:, 0] & 3) == U32) & (((t32[:, 0] >> 2) & 15) > 0))) == 0
+    if nblk >= 18:
+        assert (t32[(t32[:, 0] & 3) == BLK, 0] >> 2).max() == 7
+    with nat.thread_tune(chain_group=4):
+        assert np.array_equal(nat.chain_plan(n_pad, y_row, 64, f32=True), plan(n_pad, y_row, 64, 4, uq=0))
+    if n <= 3000:
+        rng = np.random.default_rng(11)
+        simulate(t32, y_row // SL + 1, 16, rng)
+        W0, (xt, xs, y, noise, k) = augmented(n, m, rng)
+        W = run_tasks(W0.copy(), t32, nblk)
+        np.testing.assert_allclose(np.tril(W[:n, :n]), np.linalg.cholesky(k(xt, xt) + noise * np.eye(n)), rtol=0,
+                                   atol=1e-12)
+    with pytest.raises(nat.GpkError):
+        nat.chain_plan(n_pad, n_pad + n, 64, eye=True, f32=True)
+
+
 def test_chain_plan_rejects_bad_shapes():
     _lib_or_skip()
     with pytest.raises(nat.GpkError):

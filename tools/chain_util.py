@@ -1,7 +1,8 @@
 """Where the workgroups of one persistent factorisation spend the launch (GPK_CHAIN_TIMES=1): per task type the
 summed run time (inputs ready -> published) and wait time (claimed -> inputs ready) as fractions of grid x span,
 the claim gaps, the tail after the last diagonal task, and the fraction of workgroups running a task in 10 time
-bins.  usage: python tools/chain_util.py n [eye]   (eye: the identity-augmented value + gradient factorisation)"""
+bins.  usage: python tools/chain_util.py n [eye] [f32] [grid=G]   (eye: the identity-augmented value + gradient
+factorisation; f32: chain_kernel<float>, whose plans take one slice-update task per slice; grid: workgroups)"""
 import ctypes
 import os
 import sys
@@ -19,21 +20,27 @@ from gaussianprocessfundamentals_amd import engine  # noqa: E402
 from gaussianprocessfundamentals_amd.KernelBasics import BaseKernels as bk  # noqa: E402
 
 n = int(sys.argv[1])
-eye = len(sys.argv) > 2 and sys.argv[2] == "eye"
+eye = "eye" in sys.argv[2:]
+f32 = "f32" in sys.argv[2:]
 nat.tune("chain", 2)
 dev = torch.device("cuda", 0)
 grid = torch.cuda.get_device_properties(0).multi_processor_count
+for a in sys.argv[2:]:
+    if a.startswith("grid="):
+        grid = int(a[5:])
+        nat.tune("chain_grid", grid)
+dt = torch.float32 if f32 else torch.float64
 kd = engine.kernel_descriptor(bk.SquaredExponentialKernel(1), 1)
 X = torch.sort(torch.rand(n, 1, dtype=torch.float64, device=dev), dim=0).values.contiguous()
 Y = torch.rand(1, n, dtype=torch.float64, device=dev)
 H = torch.full((1, 1), 0.1, dtype=torch.float64, device=dev)
 NZ = torch.tensor([1e-2], dtype=torch.float64, device=dev)
-f = engine.InverseFactorization(n, 1, 1) if eye else engine.AugmentedFactorization(n, 1, 0, 1)
+f = engine.InverseFactorization(n, 1, 1, dt) if eye else engine.AugmentedFactorization(n, 1, 0, 1, dt)
 for _ in range(3):
     f.run(kd, H, 1, NZ, 0, X, 0, Y, 0)
 torch.cuda.synchronize()
 lay = f.layout
-tasks = nat.chain_plan(lay.n_pad, lay.y_row, grid, eye).copy()
+tasks = nat.chain_plan(lay.n_pad, lay.y_row, grid, eye, f32).copy()
 gsz = ((tasks[:, 0] >> 2) & 15) + 1
 ty = tasks[:, 0] & 3
 nt = len(tasks)
@@ -43,7 +50,7 @@ T = np.frombuffer(buf, dtype=np.uint64).reshape(nt, 6).astype(np.float64)[:, :4]
 T -= T[:, 0].min()
 span = T[:, 3].max()
 names = ["D", "S", "U32", "BLK"]
-print("rc %d n %d eye %d tasks %d grid %d span %.1f us" % (rc, n, eye, nt, grid, span))
+print("rc %d n %d eye %d %s tasks %d grid %d span %.1f us" % (rc, n, eye, "f32" if f32 else "f64", nt, grid, span))
 tot = grid * span
 for t in range(4):
     m = ty == t
