@@ -596,6 +596,26 @@ __device__ __forceinline__ bool panel_zero_rows(const DiagArgs& a, int b, int64_
   return a.mb != nullptr && r0 >= a.n_pad + a.mb[b] && r1 <= a.y_row;
 }
 
+// The end of QR_s without wave 0 (GPK_DIAG_QR_LDSBAR): wave 0's next step needs only its own QR_s result (the pivot
+// tile (s + 1, s + 1); the P_s barrier already covered the trailing update of it), so waves 1..7 meet on an LDS counter
+// instead of the workgroup barrier (they exchange the X_i of QR_s for P_{s+1}'s trailing tiles) and wave 0 goes on
+// into potf2(s + 1) at once.  Its one write that waves 1..7 could still be reading -- X_{s+1} into tile (s + 1, s),
+// whose pre-solve values their QR_s reads -- waits for the counter, after the potf2.  Phase-profile (N = 4096,
+// r06m): wave 0 waited 600-2550 cycles per step at that barrier for the other waves' longer QR work.
+#ifndef GPK_DIAG_QR_LDSBAR
+#define GPK_DIAG_QR_LDSBAR 1
+#endif
+__device__ __forceinline__ void lds_counter_arrive(int* cnt) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // (this wave's LDS reads and writes retired first)
+  const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (lane == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_counter_wait(int* cnt, int target) {
+  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target)
+    __builtin_amdgcn_s_sleep(0);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // FUSE (f64): a workgroup with ticket t (DiagArgs) also solves the 64 rows R = row0 + 64 t .. +63 of the panel:
 // X = A L_kk^-T with the same MFMA k-order as gemm_kernel<TRSM> (k-step s of chunk kc takes k = 16 kc +
 // 2 q + 8 (s >> 1) + (s & 1) in lane group q; chunks kc > the column block skipped), so X is bitwise
@@ -615,6 +635,7 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
   const int lr = lane & 15;
   const int lk = lane >> 4;
   int* ticket = flag + 1;
+  int* qrcnt = flag + 2;  // (GPK_DIAG_QR_LDSBAR) arrivals of waves 1..7 at the ends of the QR phases
   T* Wb = reinterpret_cast<T*>(a.W) + (int64_t)b * a.w_bs + a.j0 * a.ld + a.j0;
   T* Ib = reinterpret_cast<T*>(a.Winv) + (int64_t)b * a.inv_bs + a.kblk * NB * NB;
   typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -653,7 +674,10 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
       }
     }
   }
-  if (tid == 0) *flag = 0;
+  if (tid == 0) {
+    *flag = 0;
+    *qrcnt = 0;
+  }
   stamp(0, 5);
   wg_sync<SC1>();
   if (FUSE) {
@@ -690,11 +714,16 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
     stamp(s, 0);
     if (decltype(last)::value && wave != 0) prefetch();
     if (wave == 0) {
-      if (s > 0) {
+      if (s > 0 && !GPK_DIAG_QR_LDSBAR) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) A[aidx(s * DB + lr, (s - 1) * DB + lk + 4 * q)] = xs[q];
       }
       if (!(a.dbg & 2)) potf2_tile(A, Dinv + s * DTS, colbuf, s, lane, flag, a.j0);  // timing ablation
+      if (s > 0 && GPK_DIAG_QR_LDSBAR) {
+        lds_counter_wait(qrcnt, (NTL - 1) * s);  // (waves 1..7 are past their QR_{s-1} reads of tile (s, s - 1))
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[aidx(s * DB + lr, (s - 1) * DB + lk + 4 * q)] = xs[q];
+      }
       if (decltype(last)::value) prefetch();
     } else if (s == 0) {
       if (!(a.dbg & 8) && wr && !a.no_inv_zeros) store_inv_zeros<T, SC1>(Ib, tid - 64, DT - 64);  // waves 1..7 are idle in P_0
@@ -772,7 +801,14 @@ __device__ __forceinline__ void diag2_body(const DiagArgs& a, int b_in, double* 
       }
     }
     stamp(s, 3);
-    wg_sync<SC1>();
+    if (GPK_DIAG_QR_LDSBAR && s < NTL - 1) {
+      if (wave != 0) {
+        lds_counter_arrive(qrcnt);
+        lds_counter_wait(qrcnt, (NTL - 1) * (s + 1));
+      }
+    } else {
+      wg_sync<SC1>();
+    }
     };
   const int nsteps = (a.dbg & 16) ? 0 : NTL;
 #pragma unroll 1
