@@ -439,7 +439,7 @@ def main():
     # (f64 only: C3 on 8 f32 persistent launches side by side 428 evals/s against 469 for the f32 launch path at 4 in
     # flight, profiles/r06k_c3_f32_chain.txt -- one at a time the f32 persistent launch wins, 297 vs 236)
     persist = (args.pipeline is None and args.chain is None and not grad_mode and not sweep and batch == 1 and
-               dtn == "f64" and n <= 12288)
+               (dtn == "f64" or os.environ.get("GPK_BENCH_PERSIST_F32") == "1") and n <= 12288)
     P = max(1, args.pipeline if args.pipeline is not None else
             (DEFAULT_PIPELINE_METRIC if args.config == "metric" else
              PERSIST_PIPELINE if persist else DEFAULT_PIPELINE_OTHER))

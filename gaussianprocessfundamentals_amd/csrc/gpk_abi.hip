@@ -208,6 +208,8 @@ struct Tune {
                           // 0.059 / 0.063 / 0.073 ms, profiles/r06c_kb_c3_chunks.txt)
   int64_t chain_f32;      // f32 factorisations as one persistent launch too (chain_kernel<float>: f32 tile tasks, the
                           // diagonal blocks in f64 as the launch path's); 0: f32 keeps the launch path
+  int64_t chain_group_near;  // tile updates of the columns too near the diagonal for the deferred group: in sub-groups
+                             // of this many panels (same look-ahead rule; 1: panel by panel)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -237,7 +239,8 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_GROUP_LA", 2), env_i64("GPK_ASM_F32_FAST", 1),
                          env_i64("GPK_CHAIN_GROUP_EYE", 8),
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
-                         env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1)};
+                         env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1),
+                         env_i64("GPK_CHAIN_GROUP_NEAR", 2)};
   return t;
 }
 
@@ -269,7 +272,7 @@ const Knob kKnobs[] = {
     {"asm_f32_fast", &Tune::asm_f32_fast},
     {"chain_group_eye", &Tune::chain_group_eye}, {"chain_xcd", &Tune::chain_xcd},
     {"chain_xcd_seats", &Tune::chain_xcd_seats}, {"asm_f32_chunk", &Tune::asm_f32_chunk},
-    {"chain_f32", &Tune::chain_f32},
+    {"chain_f32", &Tune::chain_f32},         {"chain_group_near", &Tune::chain_group_near},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -403,7 +406,7 @@ struct ChainPlan {
 };
 std::mutex g_chain_mu;
 // key: device, n_pad, y_row, grid, members, eye, and every knob chain_order reads (ChainKnobs)
-std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int>, ChainPlan> g_chain_plans;
+std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int, int>, ChainPlan> g_chain_plans;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
@@ -514,7 +517,7 @@ int chain_group_for(int64_t knob, int64_t n_pad, bool f32 = false) {
 // Every tuning input of chain_order, resolved once per call from the knobs (and part of the plan cache key, so a
 // cached device plan and gpk_chain_plan_ex always agree)
 struct ChainKnobs {
-  int group, uq, group_corner, corner_tail, group_la;
+  int group, uq, group_corner, corner_tail, group_la, group_near;
 };
 ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false) {
   ChainKnobs k;
@@ -525,6 +528,7 @@ ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false
   k.group_corner = (int)std::max<int64_t>(1, std::min<int64_t>(tn.chain_group_corner, 16));
   k.corner_tail = (int)std::max<int64_t>(0, tn.chain_corner_tail);
   k.group_la = (int)std::max<int64_t>(1, tn.chain_group_la);
+  k.group_near = (int)std::max<int64_t>(1, std::min<int64_t>(tn.chain_group_near, k.group));
   return k;
 }
 
@@ -600,7 +604,7 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int nme
   // by ONE task of depth 128 (q1 - q0) when j >= q1 + L -- the column is not needed until L steps after
   // the group's last panel solve; the columns nearer the diagonal take each panel on its own (depth 128),
   // so the diagonal chain never waits for a deep update.  G = 1 disables it.
-  const int G = group, Gc = kn.group_corner, tail_c = kn.corner_tail, LA = kn.group_la;
+  const int G = group, Gc = kn.group_corner, tail_c = kn.corner_tail, LA = kn.group_la, Gn = kn.group_near;
   bool overflow = false;  // a task with more than MAXDEP dependencies (unreachable: bounded by construction)
   auto add = [&](const Task& t) {
     if (t.nd > MAXDEP) overflow = true;
@@ -707,9 +711,16 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int nme
       }
       const bool grouped = q1 - q0 > 1 && jj >= q1 + LA;
       if (grouped && k != q1 - 1) continue;  // the group's one task comes with its last panel
+      // the columns too near the diagonal for the group (chain_group_near > 1): sub-groups of Gn panels of the
+      // group, under the same rule (a column at least LA past the sub-group's last panel), else panel by panel
+      const int p0 = q0 + (k - q0) / Gn * Gn, p1 = std::min(p0 + Gn, q1);
+      const bool sub = !grouped && p1 - p0 > 1 && jj >= p1 + LA;
+      if (sub && k != p1 - 1) continue;
       for (int i = jj; i <= yb; ++i) {
         if (grouped)
           blk(q0, q1 - q0, i, jj);
+        else if (sub)
+          blk(p0, p1 - p0, i, jj);
         else
           blk(k, 1, i, jj);
       }
@@ -812,7 +823,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     // (two lists need workgroups of both roles: at least 8 per XCD)
     const int xcd = tn.chain_xcd != 0 && grid >= 64 ? 1 : 0;
     auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, nmem, eye ? 1 : 0, kn.group, kn.uq,
-                               kn.group_corner, kn.corner_tail, kn.group_la, xcd);
+                               kn.group_corner, kn.corner_tail, kn.group_la, xcd, kn.group_near);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
       std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, nmem, kn, eye);

@@ -313,6 +313,51 @@ def test_chain_plan_f32_is_the_slice_update_plan(n, m):
         nat.chain_plan(n_pad, n_pad + n, 64, eye=True, f32=True)
 
 
+@pytest.mark.parametrize("n,m", [(300, 0), (1000, 200), (3000, 40)])
+@pytest.mark.parametrize("group,near,uq", [(8, 2, 1), (8, 4, 0), (4, 2, 1), (16, 4, 2)])
+def test_chain_plan_near_subgroups(n, m, group, near, uq):
+    """chain_group_near: the tile updates of the columns too near the diagonal for the deferred group go in sub-groups
+    of `near` panels under the same look-ahead rule -- every (panel, tile) update still exactly once, deeper tasks
+    present, every wait covering its dependencies, and the blocked factorisation reproduced."""
+    _lib_or_skip()
+    n_pad, y_row, p = shape(n, m)
+    nsl = y_row // SL + 1
+    nblk, yb = n_pad // NB, y_row // NB
+    rng = np.random.default_rng(n + near)
+    with nat.thread_tune(chain_group_near=near):
+        tasks = plan(n_pad, y_row, 16, group, uq)
+    base = plan(n_pad, y_row, 16, group, uq)
+    upd = applied_panels(tasks, nblk)
+    exp = [(q, i, j) for q in range(nblk) for j in range(q + 2, yb + 1) for i in range(j, yb + 1)]
+    assert sorted(upd) == sorted(exp)
+    g = ((tasks[:, 0] >> 2) & 15) + 1
+    gb = ((base[:, 0] >> 2) & 15) + 1
+    blk_t, blk_b = (tasks[:, 0] & 3) == BLK, (base[:, 0] & 3) == BLK
+    assert int(np.sum(blk_t & (g == 1))) <= int(np.sum(blk_b & (gb == 1)))
+    if nblk >= group + 4:
+        assert int(np.sum(blk_t & (g == 1))) < int(np.sum(blk_b & (gb == 1)))
+        assert int(np.sum(blk_t & (g == near))) > 0
+    for _ in range(2):
+        simulate(tasks, nsl, 16, rng)
+    if n <= 1000:
+        W0, (xt, xs, y, noise, k) = augmented(n, m, rng)
+        W = run_tasks(W0.copy(), tasks, nblk)
+        np.testing.assert_allclose(np.tril(W[:n, :n]), np.linalg.cholesky(k(xt, xt) + noise * np.eye(n)), rtol=0,
+                                   atol=1e-12)
+
+
+def test_chain_plan_eye_near_subgroups():
+    _lib_or_skip()
+    n = 1500
+    n_pad = -(-n // NB) * NB
+    y_row = n_pad + n
+    rng = np.random.default_rng(5)
+    with nat.thread_tune(chain_group_near=2, chain_group_eye=8, chain_group=8):
+        tasks = nat.chain_plan(n_pad, y_row, 16, True)
+    for _ in range(2):
+        simulate(tasks, y_row // SL + 1, 16, rng)
+
+
 def test_chain_plan_rejects_bad_shapes():
     _lib_or_skip()
     with pytest.raises(nat.GpkError):
