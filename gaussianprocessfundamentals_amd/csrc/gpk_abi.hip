@@ -210,6 +210,8 @@ struct Tune {
                           // diagonal blocks in f64 as the launch path's); 0: f32 keeps the launch path
   int64_t chain_group_near;  // tile updates of the columns too near the diagonal for the deferred group: in sub-groups
                              // of this many panels (same look-ahead rule; 1: panel by panel)
+  int64_t chain_u128;     // the next panel's column below the next diagonal block: one 128 x 128 tile update per block
+                          // row instead of four 32-row slice updates (0: slice updates)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -240,7 +242,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_GROUP_EYE", 8),
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
                          env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1),
-                         env_i64("GPK_CHAIN_GROUP_NEAR", 2)};
+                         env_i64("GPK_CHAIN_GROUP_NEAR", 2), env_i64("GPK_CHAIN_U128", 0)};
   return t;
 }
 
@@ -273,6 +275,7 @@ const Knob kKnobs[] = {
     {"chain_group_eye", &Tune::chain_group_eye}, {"chain_xcd", &Tune::chain_xcd},
     {"chain_xcd_seats", &Tune::chain_xcd_seats}, {"asm_f32_chunk", &Tune::asm_f32_chunk},
     {"chain_f32", &Tune::chain_f32},         {"chain_group_near", &Tune::chain_group_near},
+    {"chain_u128", &Tune::chain_u128},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -406,7 +409,7 @@ struct ChainPlan {
 };
 std::mutex g_chain_mu;
 // key: device, n_pad, y_row, grid, members, eye, and every knob chain_order reads (ChainKnobs)
-std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int, int>, ChainPlan> g_chain_plans;
+std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int, int, int>, ChainPlan> g_chain_plans;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
@@ -517,7 +520,7 @@ int chain_group_for(int64_t knob, int64_t n_pad, bool f32 = false) {
 // Every tuning input of chain_order, resolved once per call from the knobs (and part of the plan cache key, so a
 // cached device plan and gpk_chain_plan_ex always agree)
 struct ChainKnobs {
-  int group, uq, group_corner, corner_tail, group_la, group_near;
+  int group, uq, group_corner, corner_tail, group_la, group_near, u128;
 };
 ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false) {
   ChainKnobs k;
@@ -529,6 +532,7 @@ ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false
   k.corner_tail = (int)std::max<int64_t>(0, tn.chain_corner_tail);
   k.group_la = (int)std::max<int64_t>(1, tn.chain_group_la);
   k.group_near = (int)std::max<int64_t>(1, std::min<int64_t>(tn.chain_group_near, k.group));
+  k.u128 = tn.chain_u128 != 0 ? 1 : 0;
   return k;
 }
 
@@ -687,6 +691,17 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int nme
         U[(size_t)k * nr + r] = uq_of[r].back();  // (not read: D(k + 1) waits for every quarter)
         continue;
       }
+      if (kn.u128 && r >= 4 * (k + 2)) {
+        // chain_u128: below the next diagonal block, the four slices of a block row take ONE 128 x 128 tile update
+        // over panel k (a BLK task: the same k-steps, half the CU time of four slice updates); it publishes every
+        // slice's counter, so each slice's next panel solve waits for the block row instead of its own slice
+        if (r % 4 == 0 || r == 4 * (k + 2)) {
+          blk(k, 1, r / 4, k + 1);
+          const int bt = last_upd[(size_t)(r / 4) * nbt + (k + 1)];
+          for (int s2 = r; s2 <= std::min(4 * (r / 4) + 3, rlast); ++s2) U[(size_t)k * nr + s2] = bt;
+        }
+        continue;
+      }
       Task t = mk(CHT_U32 | first, k, r, k + 1, dur[2]);
       t.dep(s_of(k, r));
       for (int s = 4 * (k + 1); s <= std::min(4 * (k + 1) + 3, rlast); ++s)
@@ -823,7 +838,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     // (two lists need workgroups of both roles: at least 8 per XCD)
     const int xcd = tn.chain_xcd != 0 && grid >= 64 ? 1 : 0;
     auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, nmem, eye ? 1 : 0, kn.group, kn.uq,
-                               kn.group_corner, kn.corner_tail, kn.group_la, xcd, kn.group_near);
+                               kn.group_corner, kn.corner_tail, kn.group_la, xcd, kn.group_near, kn.u128);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
       std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, nmem, kn, eye);

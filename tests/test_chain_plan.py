@@ -326,7 +326,8 @@ def test_chain_plan_near_subgroups(n, m, group, near, uq):
     rng = np.random.default_rng(n + near)
     with nat.thread_tune(chain_group_near=near):
         tasks = plan(n_pad, y_row, 16, group, uq)
-    base = plan(n_pad, y_row, 16, group, uq)
+    with nat.thread_tune(chain_group_near=1):
+        base = plan(n_pad, y_row, 16, group, uq)
     upd = applied_panels(tasks, nblk)
     exp = [(q, i, j) for q in range(nblk) for j in range(q + 2, yb + 1) for i in range(j, yb + 1)]
     assert sorted(upd) == sorted(exp)
@@ -346,16 +347,48 @@ def test_chain_plan_near_subgroups(n, m, group, near, uq):
                                    atol=1e-12)
 
 
+@pytest.mark.parametrize("n,m", [(300, 0), (1000, 200), (3000, 40)])
+@pytest.mark.parametrize("uq", [0, 1, 2])
+def test_chain_plan_u128_block_row_updates(n, m, uq):
+    """chain_u128: below the next diagonal block the next panel's column is updated by one 128 x 128 tile task (BLK
+    over one panel) per block row instead of four slice tasks -- every (panel, tile) update exactly once (the slice
+    updates left only for the next diagonal block's slices), every wait covering its dependencies, and the blocked
+    factorisation reproduced."""
+    _lib_or_skip()
+    n_pad, y_row, p = shape(n, m)
+    nsl = y_row // SL + 1
+    nblk, yb = n_pad // NB, y_row // NB
+    rng = np.random.default_rng(n + uq)
+    with nat.thread_tune(chain_u128=1):
+        tasks = plan(n_pad, y_row, 16, 4, uq)
+    upd = applied_panels(tasks, nblk)
+    exp = [(q, i, j) for q in range(nblk) for j in range(q + 2, yb + 1) for i in range(j, yb + 1)]
+    exp += [(q, i, q + 1) for q in range(nblk) for i in range(q + 2, yb + 1)]
+    assert sorted(upd) == sorted(exp)
+    for t in tasks:
+        ty, k, r, j, g = decode(t)
+        if ty == U32:
+            assert r < 4 * (k + 2)           # only the next diagonal block's slices
+    for _ in range(2):
+        simulate(tasks, nsl, 16, rng)
+    if n <= 1000:
+        W0, (xt, xs, y, noise, k) = augmented(n, m, rng)
+        W = run_tasks(W0.copy(), tasks, nblk)
+        np.testing.assert_allclose(np.tril(W[:n, :n]), np.linalg.cholesky(k(xt, xt) + noise * np.eye(n)), rtol=0,
+                                   atol=1e-12)
+
+
 def test_chain_plan_eye_near_subgroups():
     _lib_or_skip()
     n = 1500
     n_pad = -(-n // NB) * NB
     y_row = n_pad + n
     rng = np.random.default_rng(5)
-    with nat.thread_tune(chain_group_near=2, chain_group_eye=8, chain_group=8):
-        tasks = nat.chain_plan(n_pad, y_row, 16, True)
-    for _ in range(2):
-        simulate(tasks, y_row // SL + 1, 16, rng)
+    for u128 in (0, 1):
+        with nat.thread_tune(chain_group_near=2, chain_group_eye=8, chain_group=8, chain_u128=u128):
+            tasks = nat.chain_plan(n_pad, y_row, 16, True)
+        for _ in range(2):
+            simulate(tasks, y_row // SL + 1, 16, rng)
 
 
 def test_chain_plan_rejects_bad_shapes():
