@@ -436,10 +436,11 @@ def main():
     # --pipeline P: P factorisation buffers on P streams, consecutive steps round-robin over them,
     # so that one batch's exposed panel chain (start and tail of the factorisation) overlaps the
     # trailing updates of the next (the batches are independent candidate sets of the sweep)
-    # (f64 only: C3 on 8 f32 persistent launches side by side 428 evals/s against 469 for the f32 launch path at 4 in
-    # flight, profiles/r06k_c3_f32_chain.txt -- one at a time the f32 persistent launch wins, 297 vs 236)
+    # (f32 too since the block-row updates: C3 on 8 f32 persistent launches side by side 474.1-474.8 evals/s against
+    # 472.4-472.8 for the f32 launch path at 4 in flight, profiles/r06s_defaults.txt; GPK_BENCH_PERSIST_F32=0 keeps
+    # the launch path for f32)
     persist = (args.pipeline is None and args.chain is None and not grad_mode and not sweep and batch == 1 and
-               (dtn == "f64" or os.environ.get("GPK_BENCH_PERSIST_F32") == "1") and n <= 12288)
+               (dtn == "f64" or os.environ.get("GPK_BENCH_PERSIST_F32", "1") == "1") and n <= 12288)
     P = max(1, args.pipeline if args.pipeline is not None else
             (DEFAULT_PIPELINE_METRIC if args.config == "metric" else
              PERSIST_PIPELINE if persist else DEFAULT_PIPELINE_OTHER))

@@ -211,7 +211,8 @@ struct Tune {
   int64_t chain_group_near;  // tile updates of the columns too near the diagonal for the deferred group: in sub-groups
                              // of this many panels (same look-ahead rule; 1: panel by panel)
   int64_t chain_u128;     // the next panel's column below the next diagonal block: one 128 x 128 tile update per block
-                          // row instead of four 32-row slice updates (0: slice updates)
+                          // row instead of four 32-row slice updates (1; 0: slice updates; 2 auto: slice updates only
+                          // below 48 diagonal blocks on a grid of more than 2 workgroups per diagonal block)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -242,7 +243,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_GROUP_EYE", 8),
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
                          env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1),
-                         env_i64("GPK_CHAIN_GROUP_NEAR", 2), env_i64("GPK_CHAIN_U128", 0)};
+                         env_i64("GPK_CHAIN_GROUP_NEAR", 2), env_i64("GPK_CHAIN_U128", 2)};
   return t;
 }
 
@@ -522,7 +523,7 @@ int chain_group_for(int64_t knob, int64_t n_pad, bool f32 = false) {
 struct ChainKnobs {
   int group, uq, group_corner, corner_tail, group_la, group_near, u128;
 };
-ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false) {
+ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false, int grid = 0) {
   ChainKnobs k;
   const int64_t gk = eye && tn.chain_group_eye > 0 ? tn.chain_group_eye : tn.chain_group;
   k.group = std::max(1, std::min(chain_group_for(gk, n_pad, f32), 16));
@@ -532,7 +533,10 @@ ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false
   k.corner_tail = (int)std::max<int64_t>(0, tn.chain_corner_tail);
   k.group_la = (int)std::max<int64_t>(1, tn.chain_group_la);
   k.group_near = (int)std::max<int64_t>(1, std::min<int64_t>(tn.chain_group_near, k.group));
-  k.u128 = tn.chain_u128 != 0 ? 1 : 0;
+  // (auto: slice updates only for short chains on a full grid -- single N = 4096 on 256 workgroups 1.577 vs 1.595 ms;
+  // C2's 64-workgroup launches 1726 -> 1863 evals/s, N = 8192 4.50 -> 4.31 ms, C3 f32 persistent 442 -> 470,
+  // profiles/r06r_chain_u128_ab.txt)
+  k.u128 = tn.chain_u128 == 1 || (tn.chain_u128 == 2 && (n_pad / NB >= 48 || grid <= 2 * (n_pad / NB))) ? 1 : 0;
   return k;
 }
 
@@ -833,7 +837,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   size_t ctl_ints = 0;
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);
-    const ChainKnobs kn = chain_knobs(tn, lay->n_pad, eye, lay->dtype == GPK_F32);
+    const ChainKnobs kn = chain_knobs(tn, lay->n_pad, eye, lay->dtype == GPK_F32, grid);
     const int nmem = lay->batch;
     // (two lists need workgroups of both roles: at least 8 per XCD)
     const int xcd = tn.chain_xcd != 0 && grid >= 64 ? 1 : 0;
@@ -898,7 +902,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
   a.w_bs = lay->w_batch_stride;
   a.inv_bs = lay->inv_batch_stride;
   a.ctl_stride = 2 * (int64_t)plan.nblk + 2 * (int64_t)plan.nblk * plan.nsl + (int64_t)plan.nsl * plan.nbc;
-  a.uq = (int32_t)chain_knobs(tn, lay->n_pad, eye, lay->dtype == GPK_F32).uq;
+  a.uq = (int32_t)chain_knobs(tn, lay->n_pad, eye, lay->dtype == GPK_F32, grid).uq;
   // rows of L_kk^-1 behind D's early flag: later (more of the panel solve early) for short chains, where the
   // diagonal chain is all there is; earlier for long ones, where the S tasks' waiting CUs cost tile-update time
   // (N = 4096: 112 rows 1.501 vs 96 rows 1.515 ms; 6144 / 8192 2.42 / 4.44 vs 2.37 / 4.39, profiles/r04ab_*)
@@ -2184,7 +2188,7 @@ int chain_plan_impl(int64_t n_pad, int64_t y_row, int32_t grid, int32_t flags, i
   if (eye && (y_row - n_pad < 1 || y_row - n_pad > n_pad))
     return fail_arg(2, "y_row (identity extra rows: n_pad + n with 0 < n <= n_pad)");
   if (!ntasks) return fail_arg(ap_ntasks, "ntasks");
-  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, 1, chain_knobs(tune_now(), n_pad, eye, f32), eye);
+  const std::vector<int32_t> ord = chain_order(n_pad, y_row, grid, 1, chain_knobs(tune_now(), n_pad, eye, f32, grid), eye);
   if (ord.empty()) {
     return fail_hip(hipErrorUnknown, "chain_order: a task exceeds the device's dependency bound");
   }

@@ -220,8 +220,8 @@ def run_tasks(W, tasks, nblk):
     return W
 
 
-def plan(n_pad, y_row, grid, group, uq=1, eye=False):
-    with nat.thread_tune(chain_group=group, chain_group_eye=group, chain_uq=uq):
+def plan(n_pad, y_row, grid, group, uq=1, eye=False, u128=0):
+    with nat.thread_tune(chain_group=group, chain_group_eye=group, chain_uq=uq, chain_u128=u128):
         return nat.chain_plan(n_pad, y_row, grid, eye)
 
 
@@ -293,14 +293,14 @@ def test_chain_plan_f32_is_the_slice_update_plan(n, m):
     n_pad, y_row, p = shape(n, m)
     nblk = n_pad // NB
     for uq in (0, 1, 2):
-        with nat.thread_tune(chain_uq=uq):
+        with nat.thread_tune(chain_uq=uq, chain_u128=0):
             t32 = nat.chain_plan(n_pad, y_row, 64, f32=True)
         assert np.array_equal(t32, plan(n_pad, y_row, 64, 8, uq=0))
         assert not any(is_sq(t) for t in t32)
         assert int(np.sum(((t32[:, 0] & 3) == U32) & (((t32[:, 0] >> 2) & 15) > 0))) == 0
     if nblk >= 18:
         assert (t32[(t32[:, 0] & 3) == BLK, 0] >> 2).max() == 7
-    with nat.thread_tune(chain_group=4):
+    with nat.thread_tune(chain_group=4, chain_u128=0):
         assert np.array_equal(nat.chain_plan(n_pad, y_row, 64, f32=True), plan(n_pad, y_row, 64, 4, uq=0))
     if n <= 3000:
         rng = np.random.default_rng(11)
@@ -359,8 +359,7 @@ def test_chain_plan_u128_block_row_updates(n, m, uq):
     nsl = y_row // SL + 1
     nblk, yb = n_pad // NB, y_row // NB
     rng = np.random.default_rng(n + uq)
-    with nat.thread_tune(chain_u128=1):
-        tasks = plan(n_pad, y_row, 16, 4, uq)
+    tasks = plan(n_pad, y_row, 16, 4, uq, u128=1)
     upd = applied_panels(tasks, nblk)
     exp = [(q, i, j) for q in range(nblk) for j in range(q + 2, yb + 1) for i in range(j, yb + 1)]
     exp += [(q, i, q + 1) for q in range(nblk) for i in range(q + 2, yb + 1)]
@@ -376,6 +375,23 @@ def test_chain_plan_u128_block_row_updates(n, m, uq):
         W = run_tasks(W0.copy(), tasks, nblk)
         np.testing.assert_allclose(np.tril(W[:n, :n]), np.linalg.cholesky(k(xt, xt) + noise * np.eye(n)), rtol=0,
                                    atol=1e-12)
+
+
+def test_chain_plan_u128_auto():
+    """chain_u128 2 (auto, the default): slice updates for short chains on a full grid (fewer than 48 diagonal blocks and
+    more than two workgroups per diagonal block), block-row updates otherwise."""
+    _lib_or_skip()
+
+    def has_row_updates(n, grid):
+        n_pad, y_row, _ = shape(n, 0)
+        with nat.thread_tune(chain_u128=2):
+            t = nat.chain_plan(n_pad, y_row, grid)
+        return any(decode(x)[0] == BLK and decode(x)[3] == decode(x)[1] + 1 for x in t)
+
+    assert not has_row_updates(4096, 256)
+    assert has_row_updates(4096, 64)
+    assert has_row_updates(8192, 256)
+    assert not has_row_updates(2048, 256)
 
 
 def test_chain_plan_eye_near_subgroups():
