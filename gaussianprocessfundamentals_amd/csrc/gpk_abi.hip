@@ -213,6 +213,7 @@ struct Tune {
   int64_t chain_u128;     // the next panel's column below the next diagonal block: one 128 x 128 tile update per block
                           // row instead of four 32-row slice updates (1; 0: slice updates; 2 auto: slice updates only
                           // below 48 diagonal blocks on a grid of more than 2 workgroups per diagonal block)
+  int64_t chain_near_la;  // chain_group_near's sub-groups cover the columns at least this many past their last panel
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -243,7 +244,8 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_GROUP_EYE", 8),
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
                          env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1),
-                         env_i64("GPK_CHAIN_GROUP_NEAR", 2), env_i64("GPK_CHAIN_U128", 2)};
+                         env_i64("GPK_CHAIN_GROUP_NEAR", 2), env_i64("GPK_CHAIN_U128", 2),
+                         env_i64("GPK_CHAIN_NEAR_LA", 2)};
   return t;
 }
 
@@ -276,7 +278,7 @@ const Knob kKnobs[] = {
     {"chain_group_eye", &Tune::chain_group_eye}, {"chain_xcd", &Tune::chain_xcd},
     {"chain_xcd_seats", &Tune::chain_xcd_seats}, {"asm_f32_chunk", &Tune::asm_f32_chunk},
     {"chain_f32", &Tune::chain_f32},         {"chain_group_near", &Tune::chain_group_near},
-    {"chain_u128", &Tune::chain_u128},
+    {"chain_u128", &Tune::chain_u128},         {"chain_near_la", &Tune::chain_near_la},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -410,7 +412,8 @@ struct ChainPlan {
 };
 std::mutex g_chain_mu;
 // key: device, n_pad, y_row, grid, members, eye, and every knob chain_order reads (ChainKnobs)
-std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int, int, int>, ChainPlan> g_chain_plans;
+std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int, int, int, int>, ChainPlan>
+    g_chain_plans;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
 
@@ -521,7 +524,7 @@ int chain_group_for(int64_t knob, int64_t n_pad, bool f32 = false) {
 // Every tuning input of chain_order, resolved once per call from the knobs (and part of the plan cache key, so a
 // cached device plan and gpk_chain_plan_ex always agree)
 struct ChainKnobs {
-  int group, uq, group_corner, corner_tail, group_la, group_near, u128;
+  int group, uq, group_corner, corner_tail, group_la, group_near, u128, near_la;
 };
 ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false, int grid = 0) {
   ChainKnobs k;
@@ -533,6 +536,7 @@ ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false
   k.corner_tail = (int)std::max<int64_t>(0, tn.chain_corner_tail);
   k.group_la = (int)std::max<int64_t>(1, tn.chain_group_la);
   k.group_near = (int)std::max<int64_t>(1, std::min<int64_t>(tn.chain_group_near, k.group));
+  k.near_la = (int)std::max<int64_t>(1, tn.chain_near_la);
   // (auto: slice updates only for short chains on a full grid -- single N = 4096 on 256 workgroups 1.577 vs 1.595 ms;
   // C2's 64-workgroup launches 1726 -> 1863 evals/s, N = 8192 4.50 -> 4.31 ms, C3 f32 persistent 442 -> 470,
   // profiles/r06r_chain_u128_ab.txt)
@@ -733,7 +737,7 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int nme
       // the columns too near the diagonal for the group (chain_group_near > 1): sub-groups of Gn panels of the
       // group, under the same rule (a column at least LA past the sub-group's last panel), else panel by panel
       const int p0 = q0 + (k - q0) / Gn * Gn, p1 = std::min(p0 + Gn, q1);
-      const bool sub = !grouped && p1 - p0 > 1 && jj >= p1 + LA;
+      const bool sub = !grouped && p1 - p0 > 1 && jj >= p1 + kn.near_la;
       if (sub && k != p1 - 1) continue;
       for (int i = jj; i <= yb; ++i) {
         if (grouped)
@@ -842,7 +846,8 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     // (two lists need workgroups of both roles: at least 8 per XCD)
     const int xcd = tn.chain_xcd != 0 && grid >= 64 ? 1 : 0;
     auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, nmem, eye ? 1 : 0, kn.group, kn.uq,
-                               kn.group_corner, kn.corner_tail, kn.group_la, xcd, kn.group_near, kn.u128);
+                               kn.group_corner, kn.corner_tail, kn.group_la, xcd, kn.group_near, kn.u128,
+                               kn.near_la);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
       std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, nmem, kn, eye);

@@ -314,8 +314,9 @@ def test_chain_plan_f32_is_the_slice_update_plan(n, m):
 
 
 @pytest.mark.parametrize("n,m", [(300, 0), (1000, 200), (3000, 40)])
-@pytest.mark.parametrize("group,near,uq", [(8, 2, 1), (8, 4, 0), (4, 2, 1), (16, 4, 2)])
-def test_chain_plan_near_subgroups(n, m, group, near, uq):
+@pytest.mark.parametrize("group,near,uq,nla", [(8, 2, 1, 2), (8, 4, 0, 2), (4, 2, 1, 2), (16, 4, 2, 2), (8, 2, 1, 1),
+                                                (4, 2, 0, 1)])
+def test_chain_plan_near_subgroups(n, m, group, near, uq, nla):
     """chain_group_near: the tile updates of the columns too near the diagonal for the deferred group go in sub-groups
     of `near` panels under the same look-ahead rule -- every (panel, tile) update still exactly once, deeper tasks
     present, every wait covering its dependencies, and the blocked factorisation reproduced."""
@@ -324,7 +325,7 @@ def test_chain_plan_near_subgroups(n, m, group, near, uq):
     nsl = y_row // SL + 1
     nblk, yb = n_pad // NB, y_row // NB
     rng = np.random.default_rng(n + near)
-    with nat.thread_tune(chain_group_near=near):
+    with nat.thread_tune(chain_group_near=near, chain_near_la=nla):
         tasks = plan(n_pad, y_row, 16, group, uq)
     with nat.thread_tune(chain_group_near=1):
         base = plan(n_pad, y_row, 16, group, uq)
