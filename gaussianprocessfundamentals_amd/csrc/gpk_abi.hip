@@ -214,6 +214,8 @@ struct Tune {
                           // row instead of four 32-row slice updates (1; 0: slice updates; 2 auto: slice updates only
                           // below 48 diagonal blocks on a grid of more than 2 workgroups per diagonal block)
   int64_t chain_near_la;  // chain_group_near's sub-groups cover the columns at least this many past their last panel
+                          // (1: C2 1866 -> 1884 evals/s, C3 474 -> 480, value + gradient N = 8192 10.6 -> 10.43 ms
+                          // against 2, profiles/r06u_near_la_ab.txt)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -245,7 +247,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
                          env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1),
                          env_i64("GPK_CHAIN_GROUP_NEAR", 2), env_i64("GPK_CHAIN_U128", 2),
-                         env_i64("GPK_CHAIN_NEAR_LA", 2)};
+                         env_i64("GPK_CHAIN_NEAR_LA", 1)};
   return t;
 }
 
