@@ -216,6 +216,8 @@ struct Tune {
   int64_t chain_near_la;  // chain_group_near's sub-groups cover the columns at least this many past their last panel
                           // (1: C2 1866 -> 1884 evals/s, C3 474 -> 480, value + gradient N = 8192 10.6 -> 10.43 ms
                           // against 2, profiles/r06u_near_la_ab.txt)
+  int64_t chain_s128;     // the panel solves below the next diagonal block: one task per block row (its slices one after
+                          // another) instead of one per 32-row slice (1; 0: per slice; 2 auto: chain_u128's rule)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -247,7 +249,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
                          env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1),
                          env_i64("GPK_CHAIN_GROUP_NEAR", 2), env_i64("GPK_CHAIN_U128", 2),
-                         env_i64("GPK_CHAIN_NEAR_LA", 1)};
+                         env_i64("GPK_CHAIN_NEAR_LA", 1), env_i64("GPK_CHAIN_S128", 0)};
   return t;
 }
 
@@ -281,6 +283,7 @@ const Knob kKnobs[] = {
     {"chain_xcd_seats", &Tune::chain_xcd_seats}, {"asm_f32_chunk", &Tune::asm_f32_chunk},
     {"chain_f32", &Tune::chain_f32},         {"chain_group_near", &Tune::chain_group_near},
     {"chain_u128", &Tune::chain_u128},         {"chain_near_la", &Tune::chain_near_la},
+    {"chain_s128", &Tune::chain_s128},
 };
 
 int64_t Tune::*knob_field(const char* key) {
@@ -414,7 +417,7 @@ struct ChainPlan {
 };
 std::mutex g_chain_mu;
 // key: device, n_pad, y_row, grid, members, eye, and every knob chain_order reads (ChainKnobs)
-std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int, int, int, int>, ChainPlan>
+std::map<std::tuple<int, int64_t, int64_t, int, int, int, int, int, int, int, int, int, int, int, int, int>, ChainPlan>
     g_chain_plans;
 
 enum { CHT_D = 0, CHT_S = 1, CHT_U32 = 2, CHT_BLK = 3 };
@@ -526,7 +529,7 @@ int chain_group_for(int64_t knob, int64_t n_pad, bool f32 = false) {
 // Every tuning input of chain_order, resolved once per call from the knobs (and part of the plan cache key, so a
 // cached device plan and gpk_chain_plan_ex always agree)
 struct ChainKnobs {
-  int group, uq, group_corner, corner_tail, group_la, group_near, u128, near_la;
+  int group, uq, group_corner, corner_tail, group_la, group_near, u128, near_la, s128;
 };
 ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false, int grid = 0) {
   ChainKnobs k;
@@ -543,6 +546,7 @@ ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false
   // C2's 64-workgroup launches 1726 -> 1863 evals/s, N = 8192 4.50 -> 4.31 ms, C3 f32 persistent 442 -> 470,
   // profiles/r06r_chain_u128_ab.txt)
   k.u128 = tn.chain_u128 == 1 || (tn.chain_u128 == 2 && (n_pad / NB >= 48 || grid <= 2 * (n_pad / NB))) ? 1 : 0;
+  k.s128 = tn.chain_s128 == 1 || (tn.chain_s128 == 2 && (n_pad / NB >= 48 || grid <= 2 * (n_pad / NB))) ? 1 : 0;
   return k;
 }
 
@@ -664,6 +668,27 @@ std::vector<int32_t> chain_order(int64_t n_pad, int64_t y_row, int grid, int nme
     D[k] = add(d);
     for (int r = 4 * (k + 1); r <= rlast; ++r) {
       if (!live(r / 4, k)) continue;
+      if (kn.s128 && r >= 4 * (k + 2)) {
+        // chain_s128: below the next diagonal block, a block row's slices take ONE panel-solve task (S with g = the
+        // slice count in the type word's bits 2..5: the slices solved one after another, each as its own S task would)
+        if (r % 4 != 0) continue;
+        const int g = std::min(4, rlast - r + 1);
+        Task t = mk(CHT_S | ((g - 1) << 2), k, r, 0, dur[1] * (0.5f + 0.5f * (float)g));
+        t.dep(D[k]);
+        if (k > 0 && live(r / 4, k - 1)) {
+          for (int s2 = r; s2 < r + g; ++s2) {
+            const int u = u_of(k - 1, s2);
+            bool dup = false;
+            for (int e = 0; e < t.nd && e < MAXDEP; ++e) dup = dup || t.deps[e] == u;
+            if (!dup) t.dep(u);
+          }
+        } else if (k > 0) {
+          t.ty |= kChainFirst;
+        }
+        const int id = add(t);
+        for (int s2 = r; s2 < r + g; ++s2) S[(size_t)k * nr + s2] = id;
+        continue;
+      }
       // chain_uq 2: the next diagonal block's slices take SQ tasks -- the panel solve followed by the slice's lower
       // quarters of that block (chain_sq), which need the siblings' solved rows (claimed before: lower slices first)
       const bool sqt = sq && k + 1 < nblk && r < 4 * (k + 2);
@@ -849,7 +874,7 @@ int chain_potrf(const gpk_layout* lay, void* W, void* Winv, int32_t* info_dev, c
     const int xcd = tn.chain_xcd != 0 && grid >= 64 ? 1 : 0;
     auto key = std::make_tuple(dev, lay->n_pad, lay->y_row, grid, nmem, eye ? 1 : 0, kn.group, kn.uq,
                                kn.group_corner, kn.corner_tail, kn.group_la, xcd, kn.group_near, kn.u128,
-                               kn.near_la);
+                               kn.near_la, kn.s128);
     auto it = g_chain_plans.find(key);
     if (it == g_chain_plans.end()) {
       std::vector<int32_t> ord = chain_order(lay->n_pad, lay->y_row, grid, nmem, kn, eye);

@@ -1314,9 +1314,14 @@ __device__ __forceinline__ bool chain_deps(const ChainArgs& a, int ty, int kprev
     }
     return chain_wait_set<4>(a, p, v, t0);
   } else if (ty == CH_S) {
-    const int32_t* p[2] = {dflag + k, ucnt + (int64_t)r * a.nbc + k};
-    const int32_t v[2] = {1, kprev};
-    return chain_wait_set<2>(a, p, v, t0);
+    // (g > 1, chain_s128: slices r .. r + g - 1 of one block row; unused slots repeat the first, always met)
+    const int32_t* p[5] = {dflag + k, dflag + k, dflag + k, dflag + k, dflag + k};
+    int32_t v[5] = {1, 1, 1, 1, 1};
+    for (int i = 0; i < g; ++i) {
+      p[1 + i] = ucnt + (int64_t)(r + i) * a.nbc + k;
+      v[1 + i] = kprev;
+    }
+    return chain_wait_set<5>(a, p, v, t0);
   } else if (ty == CH_U32) {
     const int32_t* sd = sdone + (int64_t)k * a.nsl;
     const int32_t* p[6];
@@ -1414,7 +1419,7 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
     // S (GPK_CHAIN_SPREF): its slice of the panel is final once the slice's last update is published, before
     // L_kk^-1 is: wait for that first, start the slice's LDS-DMA, then wait for D(k) -- the slice's load leaves
     // the critical chain D(k) -> S
-    const bool spref = GPK_CHAIN_SPREF && ty == CH_S;
+    const bool spref = GPK_CHAIN_SPREF && ty == CH_S && g == 1;
     const bool shalf = GPK_CHAIN_SHALF && spref && (r >> 2) == k + 1;  // (the S tasks on the diagonal chain)
     if (wave == 0) {
       if (a.times) a.times[6 * t] = __builtin_amdgcn_s_memrealtime();
@@ -1479,7 +1484,10 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       } else if (spref) {
         chain_s_staged(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
       } else if (ty == CH_S) {
-        chain_s(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+        for (int i = 0; i < g; ++i) {  // (g > 1: a block row's slices, chain_s128)
+          if (i > 0) wg_sync<true>();  // (every wave done reading the previous slice's rows in LDS)
+          chain_s(Wm, a.ld, Wi, k, r + i, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+        }
       } else if (ty == CH_U32 && g > 1) {
         chain_uq(Wm, a.ld, k, r, j, g - 2, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
       } else if (ty == CH_U32) {
@@ -1496,7 +1504,10 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       } else if (spref) {
         chain_s32_staged(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
       } else if (ty == CH_S) {
-        chain_s32(Wm, a.ld, Wi, k, r, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+        for (int i = 0; i < g; ++i) {
+          if (i > 0) wg_sync<true>();
+          chain_s32(Wm, a.ld, Wi, k, r + i, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
+        }
       } else if (ty == CH_U32) {
         chain_u32_f32(Wm, a.ld, k, r, j, a.times ? a.times + 6 * t : nullptr, reinterpret_cast<char*>(sm));
       } else {
@@ -1519,7 +1530,7 @@ __global__ __launch_bounds__(DT) void chain_kernel(ChainArgs a) {
       } else if (sq) {
         st_flag(a.qdone + co + (int64_t)k * a.nsl + r, 1);  // (its sdone went out before the quarters)
       } else if (ty == CH_S) {
-        st_flag(a.sdone + co + (int64_t)k * a.nsl + r, 1);
+        for (int i = 0; i < g; ++i) st_flag(a.sdone + co + (int64_t)k * a.nsl + r + i, 1);
       } else if (ty == CH_U32 && g > 1) {
         // +1 from lane 0 only (every lane of wave 0 executes this: an add of 1 would count 64; the compiler
         // reduces the lanes' values and issues one atomic)

@@ -70,8 +70,8 @@ def cells(task, nsl, uq=False):
         rl = r - 4 * (k + 1)
         rd = {(r, k), ("inv", k), (r, k + 1)} | {(s, k) for s in range(4 * (k + 1), r)}
         return rd, {(r, k)} | {("q", r, k + 1, q) for q in range(rl + 1)}
-    if ty == S:
-        return {(r, k), ("inv", k)}, {(r, k)}
+    if ty == S:   # (g > 1: the block row's slices r .. r + g - 1, chain_s128)
+        return {(r + i, k) for i in range(g)} | {("inv", k)}, {(r + i, k) for i in range(g)}
     if ty == U32 and g > 1:
         q = g - 2
         return {(r, k), (4 * j + q, k), (r, j)}, {("q", r, j, q)}
@@ -96,7 +96,7 @@ def waits(task, nsl, uq=False):
     elif ty == S:
         out.append(("dflag", k, 1))
         if kprev > 0:
-            out.append(("ucnt", (r, k), kprev))
+            out += [("ucnt", (r + i, k), kprev) for i in range(g)]
         if is_sq(task):
             if k > 0:
                 out.append(("ucnt", (r, k + 1), k))
@@ -125,7 +125,7 @@ def publishes(task, nsl):
     if ty == S and is_sq(task):
         return [("sdone", (k, r), 1), ("qdone", (k, r), 1)]
     if ty == S:
-        return [("sdone", (k, r), 1)]
+        return [("sdone", (k, r + i), 1) for i in range(g)]
     if ty == U32 and g > 1:
         return [("qdone", (k, r), "+1")]
     if ty == U32:
@@ -201,7 +201,7 @@ def run_tasks(W, tasks, nblk):
             W[K, K] = L
             inv[k] = np.linalg.inv(L)
         elif ty == S:
-            R = slice(SL * r, SL * r + SL)
+            R = slice(SL * r, SL * r + SL * g)
             W[R, K] = W[R, K] @ inv[k].T
             if is_sq(task):
                 for q in range(r - 4 * (k + 1) + 1):
@@ -220,8 +220,8 @@ def run_tasks(W, tasks, nblk):
     return W
 
 
-def plan(n_pad, y_row, grid, group, uq=1, eye=False, u128=0):
-    with nat.thread_tune(chain_group=group, chain_group_eye=group, chain_uq=uq, chain_u128=u128):
+def plan(n_pad, y_row, grid, group, uq=1, eye=False, u128=0, s128=0):
+    with nat.thread_tune(chain_group=group, chain_group_eye=group, chain_uq=uq, chain_u128=u128, chain_s128=s128):
         return nat.chain_plan(n_pad, y_row, grid, eye)
 
 
@@ -293,14 +293,14 @@ def test_chain_plan_f32_is_the_slice_update_plan(n, m):
     n_pad, y_row, p = shape(n, m)
     nblk = n_pad // NB
     for uq in (0, 1, 2):
-        with nat.thread_tune(chain_uq=uq, chain_u128=0):
+        with nat.thread_tune(chain_uq=uq, chain_u128=0, chain_s128=0):
             t32 = nat.chain_plan(n_pad, y_row, 64, f32=True)
         assert np.array_equal(t32, plan(n_pad, y_row, 64, 8, uq=0))
         assert not any(is_sq(t) for t in t32)
         assert int(np.sum(((t32[:, 0] & 3) == U32) & (((t32[:, 0] >> 2) & 15) > 0))) == 0
     if nblk >= 18:
         assert (t32[(t32[:, 0] & 3) == BLK, 0] >> 2).max() == 7
-    with nat.thread_tune(chain_group=4, chain_u128=0):
+    with nat.thread_tune(chain_group=4, chain_u128=0, chain_s128=0):
         assert np.array_equal(nat.chain_plan(n_pad, y_row, 64, f32=True), plan(n_pad, y_row, 64, 4, uq=0))
     if n <= 3000:
         rng = np.random.default_rng(11)
@@ -369,6 +369,38 @@ def test_chain_plan_u128_block_row_updates(n, m, uq):
         ty, k, r, j, g = decode(t)
         if ty == U32:
             assert r < 4 * (k + 2)           # only the next diagonal block's slices
+    for _ in range(2):
+        simulate(tasks, nsl, 16, rng)
+    if n <= 1000:
+        W0, (xt, xs, y, noise, k) = augmented(n, m, rng)
+        W = run_tasks(W0.copy(), tasks, nblk)
+        np.testing.assert_allclose(np.tril(W[:n, :n]), np.linalg.cholesky(k(xt, xt) + noise * np.eye(n)), rtol=0,
+                                   atol=1e-12)
+
+
+@pytest.mark.parametrize("n,m", [(300, 0), (1000, 200), (3000, 40)])
+@pytest.mark.parametrize("uq,u128", [(1, 1), (0, 0), (2, 1)])
+def test_chain_plan_s128_block_row_solves(n, m, uq, u128):
+    """chain_s128: below the next diagonal block a block row's slices take one panel-solve task (S with g = its slice
+    count) -- every slice of every panel solved exactly once, every wait covering its dependencies, the blocked
+    factorisation reproduced."""
+    _lib_or_skip()
+    n_pad, y_row, p = shape(n, m)
+    nsl = y_row // SL + 1
+    nblk = n_pad // NB
+    rng = np.random.default_rng(n + uq)
+    tasks = plan(n_pad, y_row, 16, 4, uq, u128=u128, s128=1)
+    solved = []
+    for t in tasks:
+        ty, k, r, j, g = decode(t)
+        if ty == S:
+            solved += [(k, r + i) for i in range(g)]
+            if g > 1:
+                assert r % 4 == 0 and r >= 4 * (k + 2)
+    exp = [(k, r) for k in range(nblk) for r in range(4 * (k + 1), nsl)]
+    assert sorted(solved) == sorted(exp)
+    if nblk >= 3:
+        assert any(decode(t)[0] == S and decode(t)[4] > 1 for t in tasks)
     for _ in range(2):
         simulate(tasks, nsl, 16, rng)
     if n <= 1000:

@@ -1,7 +1,7 @@
 # round 6 final tree, set A: full GPU suite + smoke(), default bench with CPU baseline, rocprofv3 stats of a short
 # bench (the roofline kernel's average duration), the K-build cases
 set -o pipefail
-T=r06fin; O=gpurun_out/$T; mkdir -p $O
+T=${T:-r06fin}; O=gpurun_out/$T; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error" $O/tests.log | head -20; exit $rc; }

@@ -1,7 +1,7 @@
 # round 6 final tree, set B: every BASELINE config with roofline + cpu_baseline, C2 one at a time, --mode grad, the
 # C4 per-rank slices, the --dist rehearsals, the drop-in API latency, posterior timing
 set -o pipefail
-T=r06fin; O=gpurun_out/$T; mkdir -p $O; : > $O/configs.jsonl
+T=${T:-r06fin}; O=gpurun_out/$T; mkdir -p $O; : > $O/configs.jsonl
 export TMPDIR=/tmp
 for spec in "metric 10 3" "C2 300 30" "C3 60 10" "C4 20 3" "C5 20 4"; do
   set -- $spec

@@ -1,7 +1,7 @@
 # round 6 final tree, set C: PMC traffic of the trailing update (roofline.traffic), PMC of the C3 f32 K build, the
 # value + gradient kernel stats, rocprofv3 stats of C2 / C3 / C5
 set -o pipefail
-T=r06fin; O=gpurun_out/$T; mkdir -p $O
+T=${T:-r06fin}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_chain.py -m gpu -q --timeout 240 --timeout-method thread > $O/tests_chain.log 2>&1 || { tail -5 $O/tests_chain.log; exit 1; }
 tail -1 $O/tests_chain.log
