@@ -217,7 +217,8 @@ struct Tune {
                           // (1: C2 1866 -> 1884 evals/s, C3 474 -> 480, value + gradient N = 8192 10.6 -> 10.43 ms
                           // against 2, profiles/r06u_near_la_ab.txt)
   int64_t chain_s128;     // the panel solves below the next diagonal block: one task per block row (its slices one after
-                          // another) instead of one per 32-row slice (1; 0: per slice; 2 auto: chain_u128's rule)
+                          // another) instead of one per 32-row slice (1; 0: per slice; 2 auto: on a grid of at most 2
+                          // workgroups per diagonal block -- the CU-share launches side by side)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -249,7 +250,7 @@ Tune& tune() {
                          env_i64("GPK_CHAIN_XCD", 0), env_i64("GPK_CHAIN_XCD_SEATS", 16),
                          env_i64("GPK_ASM_F32_CHUNK", 4), env_i64("GPK_CHAIN_F32", 1),
                          env_i64("GPK_CHAIN_GROUP_NEAR", 2), env_i64("GPK_CHAIN_U128", 2),
-                         env_i64("GPK_CHAIN_NEAR_LA", 1), env_i64("GPK_CHAIN_S128", 0)};
+                         env_i64("GPK_CHAIN_NEAR_LA", 1), env_i64("GPK_CHAIN_S128", 2)};
   return t;
 }
 
@@ -546,7 +547,9 @@ ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false
   // C2's 64-workgroup launches 1726 -> 1863 evals/s, N = 8192 4.50 -> 4.31 ms, C3 f32 persistent 442 -> 470,
   // profiles/r06r_chain_u128_ab.txt)
   k.u128 = tn.chain_u128 == 1 || (tn.chain_u128 == 2 && (n_pad / NB >= 48 || grid <= 2 * (n_pad / NB))) ? 1 : 0;
-  k.s128 = tn.chain_s128 == 1 || (tn.chain_s128 == 2 && (n_pad / NB >= 48 || grid <= 2 * (n_pad / NB))) ? 1 : 0;
+  // (auto: the CU-share launches only -- C3 on 8 f32 launches of 64 workgroups 476 -> 495 evals/s, C2 neutral, while a
+  // single N = 8192 on 256 workgroups lost 2 %: 4.27 -> 4.37 ms, profiles/r06x_chain_s128_ab.txt)
+  k.s128 = tn.chain_s128 == 1 || (tn.chain_s128 == 2 && grid > 0 && grid <= 2 * (n_pad / NB)) ? 1 : 0;
   return k;
 }
 

@@ -135,7 +135,7 @@ def test_knob_defaults_land_in_their_fields(lib):
               "chain_max_batch": 8, "chain_batch_max_rows": 17500, "chain_uq": 1, "group": 8, "lookahead": 2,
               "fuse_kbuild": 1, "diag_version": 2, "chain_group_corner": 16, "chain_corner_tail": 8,
               "chain_group_la": 2, "asm_f32_fast": 1, "chain_group_eye": 8, "chain_xcd": 0, "chain_xcd_seats": 16,
-              "asm_f32_chunk": 4, "chain_f32": 1, "chain_group_near": 2, "chain_u128": 2, "chain_near_la": 1, "chain_s128": 0}
+              "asm_f32_chunk": 4, "chain_f32": 1, "chain_group_near": 2, "chain_u128": 2, "chain_near_la": 1, "chain_s128": 2}
     for k, v in expect.items():
         if os.environ.get("GPK_" + k.upper()):
             continue

@@ -421,6 +421,14 @@ def test_chain_plan_u128_auto():
             t = nat.chain_plan(n_pad, y_row, grid)
         return any(decode(x)[0] == BLK and decode(x)[3] == decode(x)[1] + 1 for x in t)
 
+    def has_row_solves(n, grid):
+        n_pad, y_row, _ = shape(n, 0)
+        with nat.thread_tune(chain_s128=2):
+            t = nat.chain_plan(n_pad, y_row, grid)
+        return any(decode(x)[0] == S and decode(x)[4] > 1 for x in t)
+
+    assert has_row_solves(8192, 64) and has_row_solves(4096, 64)
+    assert not has_row_solves(8192, 256) and not has_row_solves(4096, 256)
     assert not has_row_updates(4096, 256)
     assert has_row_updates(4096, 64)
     assert has_row_updates(8192, 256)
