@@ -218,7 +218,8 @@ struct Tune {
                           // against 2, profiles/r06u_near_la_ab.txt)
   int64_t chain_s128;     // the panel solves below the next diagonal block: one task per block row (its slices one after
                           // another) instead of one per 32-row slice (1; 0: per slice; 2 auto: on a grid of at most 2
-                          // workgroups per diagonal block -- the CU-share launches side by side)
+                          // workgroups per diagonal block -- the CU-share launches side by side -- and for
+                          // identity-augmented plans of at least 48 diagonal blocks)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -549,7 +550,10 @@ ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false
   k.u128 = tn.chain_u128 == 1 || (tn.chain_u128 == 2 && (n_pad / NB >= 48 || grid <= 2 * (n_pad / NB))) ? 1 : 0;
   // (auto: the CU-share launches only -- C3 on 8 f32 launches of 64 workgroups 476 -> 495 evals/s, C2 neutral, while a
   // single N = 8192 on 256 workgroups lost 2 %: 4.27 -> 4.37 ms, profiles/r06x_chain_s128_ab.txt)
-  k.s128 = tn.chain_s128 == 1 || (tn.chain_s128 == 2 && grid > 0 && grid <= 2 * (n_pad / NB)) ? 1 : 0;
+  // and the long identity-augmented plans (value + gradient N = 8192 10.43-10.48 -> 10.32-10.35 ms)
+  k.s128 = tn.chain_s128 == 1 ||
+                   (tn.chain_s128 == 2 && ((grid > 0 && grid <= 2 * (n_pad / NB)) || (eye && n_pad / NB >= 48)))
+               ? 1 : 0;
   return k;
 }
 

@@ -429,6 +429,11 @@ def test_chain_plan_u128_auto():
 
     assert has_row_solves(8192, 64) and has_row_solves(4096, 64)
     assert not has_row_solves(8192, 256) and not has_row_solves(4096, 256)
+    with nat.thread_tune(chain_s128=2):
+        te = nat.chain_plan(8192, 2 * 8192, 256, True)
+        te4 = nat.chain_plan(4096, 2 * 4096, 256, True)
+    assert any(decode(x)[0] == S and decode(x)[4] > 1 for x in te)
+    assert not any(decode(x)[0] == S and decode(x)[4] > 1 for x in te4)
     assert not has_row_updates(4096, 256)
     assert has_row_updates(4096, 64)
     assert has_row_updates(8192, 256)
@@ -553,14 +558,17 @@ def test_chain_plan_eye_waits_cover_every_dependency(n, group, uq):
 
 
 @pytest.mark.parametrize("n", [200, 300, 1100])
-@pytest.mark.parametrize("group,uq", [(1, 0), (4, 1), (4, 2)])
-def test_chain_plan_eye_reproduces_the_inverse(n, group, uq):
+@pytest.mark.parametrize("group,uq,rows", [(1, 0, 0), (4, 1, 0), (4, 2, 0), (4, 1, 1)])
+def test_chain_plan_eye_reproduces_the_inverse(n, group, uq, rows):
     """Run in list order on the identity-augmented matrix: L, the extra rows L^-T, the corner -K^-1 and its y row
-    -alpha^T (the layout gpk_nlml_grad reads, include/gpk.h)."""
+    -alpha^T (the layout gpk_nlml_grad reads, include/gpk.h); rows: with block-row updates and panel solves."""
     _lib_or_skip()
     rng = np.random.default_rng(11)
     W0, Kn, y, n_pad, y_row = augmented_eye(n, rng)
-    tasks = plan(n_pad, y_row, 64, group, uq, eye=True)
+    tasks = plan(n_pad, y_row, 64, group, uq, eye=True, u128=rows, s128=rows)
+    if rows:
+        for _ in range(2):
+            simulate(tasks, y_row // SL + 1, 16, rng)
     W = run_tasks(W0.copy(), tasks, n_pad // NB)
     L = np.linalg.cholesky(Kn)
     np.testing.assert_allclose(np.tril(W[:n, :n]), L, rtol=0, atol=1e-12)
