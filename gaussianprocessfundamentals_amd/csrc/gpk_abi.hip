@@ -219,7 +219,7 @@ struct Tune {
   int64_t chain_s128;     // the panel solves below the next diagonal block: one task per block row (its slices one after
                           // another) instead of one per 32-row slice (1; 0: per slice; 2 auto: on a grid of at most 2
                           // workgroups per diagonal block -- the CU-share launches side by side -- and for
-                          // identity-augmented plans of at least 48 diagonal blocks)
+                          // identity-augmented plans of at least 64 diagonal blocks; N = 6144 within the spread either way)
   // (new fields go last: tune() initialises the struct positionally)
 };
 
@@ -552,7 +552,7 @@ ChainKnobs chain_knobs(const Tune& tn, int64_t n_pad, bool eye, bool f32 = false
   // single N = 8192 on 256 workgroups lost 2 %: 4.27 -> 4.37 ms, profiles/r06x_chain_s128_ab.txt)
   // and the long identity-augmented plans (value + gradient N = 8192 10.43-10.48 -> 10.32-10.35 ms)
   k.s128 = tn.chain_s128 == 1 ||
-                   (tn.chain_s128 == 2 && ((grid > 0 && grid <= 2 * (n_pad / NB)) || (eye && n_pad / NB >= 48)))
+                   (tn.chain_s128 == 2 && ((grid > 0 && grid <= 2 * (n_pad / NB)) || (eye && n_pad / NB >= 64)))
                ? 1 : 0;
   return k;
 }
