@@ -427,6 +427,14 @@ int gpk_timing_reset(void);
  * "chain_f32" (1: f32 factorisations without identity rows take the persistent launch under the same rules --
  * chain_kernel<float>: f32 MFMA panel solves and tile updates, the diagonal blocks as the launch path's; bitwise
  * the f32 launch path's results; one slice-update task per slice whatever "chain_uq"; 0: the launch path).
+ * Planner knobs of the persistent launch (all part of the plan cache key, all bitwise the launch path's results):
+ * "chain_group_near" (2: the tile updates of the columns too near the diagonal for the deferred group go in
+ * sub-groups of this many panels, for columns at least "chain_near_la" (1) past the sub-group's last panel; 1: one
+ * panel at a time), "chain_u128" (2 auto, 1, 0: below the next diagonal block the next panel's column is updated by
+ * one 128 x 128 tile task per block row instead of four 32-row slice tasks; auto: except below 48 diagonal blocks on
+ * a grid of more than 2 workgroups per block), "chain_s128" (2 auto, 1, 0: the panel solves below the next diagonal
+ * block as one task per block row; auto: on grids of at most 2 workgroups per diagonal block -- the CU-share launches
+ * side by side -- and identity-augmented plans of at least 64 diagonal blocks).
  * "asm_feat" (1: the K build of a two-leaf SE + periodic tree at D = 4 or 8 computes the per-point features in a
  * pre-pass and runs its interior tiles on the f64 MFMA fast-tile kernel; 0: every tile stages its points itself
  * -- the same bits, slower; A/B).
